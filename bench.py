@@ -1,0 +1,260 @@
+"""bench.py — edge-messages/s of the D-MPNN forward (ChempropBlock + Sum readout) on MI355X.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
+``torch.distributed.run`` (one rank per GPU, RCCL).  Rank 0 prints ONE JSON line.
+
+Workload (BASELINE.json configs[1]): per GPU a 4096-molecule QM9-shaped batch (synthetic, seeded
+per rank -> weak scaling), hidden 300, depth 3, fp32, ReLU, residual, sum reduce, reference
+collate semantics (rev offset by nodes).  A "step" = one forward of ChempropBlock + Sum readout
+with the collated graph (incl. its CSR layout) and the embedded features already resident in HBM.
+value = sum over ranks of E_r * depth * K / max over ranks of the timed seconds.
+
+Also reported: ``roofline`` for the dominant kernel (nt_dmpnn_update; per-launch duration from
+torch.cuda events recorded on the launch stream around every launch inside the timed region) and
+``cpu_baseline`` (the oracle restatement on the host CPU, rank 0, N=1, bounded sample).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from notorch_amd.shard import aggregate_throughput, dist_env  # noqa: E402
+
+METRIC = "edge-messages/sec D-MPNN depth=3 h=300, QM9-shaped batches, 1/2/4/8 MI355X"
+PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
+PEAK_HBM_GBPS = 8000.0
+
+WORKLOADS = {
+    # name: (generator, molecules per GPU, hidden, depth)
+    "qm9-4096": ("qm9", 4096, 300, 3),  # BASELINE config 2 (the metric's configuration)
+    "qm9-32k": ("qm9", 32768, 300, 3),  # HBM-scale batch (working set >> Infinity Cache)
+    "zinc-4096": ("zinc", 4096, 512, 5),  # config 3 shape, run in fp32
+    "polymer-16": ("polymer", 16, 300, 3),  # config 5 shape
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=50)
+    p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--workload", default="qm9-4096", choices=sorted(WORKLOADS))
+    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--pmc-csv", default=None, help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
+    return p.parse_args()
+
+
+def forward_bytes_flops(V, E, B, h, d, b=4):
+    """SURVEY §8(d) minimal-traffic model of the fused forward + its MFMA flops."""
+    rows = b * h * ((2 * d + 3) * (E + V) + B)
+    idx = 4 * ((3 * d + 2) * E + (d + 1) * (V + 1) + (B + 1))
+    wts = d * (h * h + h) * b
+    return rows + idx + wts, 2 * d * E * h * h
+
+
+def update_bytes(V, E, h, b=4):
+    """Algorithmic HBM bytes of ONE nt_dmpnn_update launch: read H[e], gather S[src[e]] and
+    H[rev[e]], write H_out[e] (4 rows per edge), src+rev int64, weights once."""
+    return 4 * E * h * b + 16 * E + (h * h + h) * b
+
+
+def cpu_baseline(G, Xv, Xe, Ws, bs, depth, budget_s):
+    """Oracle restatement (ATen CPU) timed on the host; median of runs within the budget."""
+    from oracle import dmpnn_ref
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    threads = max(1, min(16, cores))
+    torch.set_num_threads(threads)
+    ei, rev, bni, B = G.edge_index.cpu(), G.rev_index.cpu(), G.batch_node_index.cpu(), len(G)
+    Xv, Xe = Xv.cpu(), Xe.cpu()
+    Ws = [w.detach().cpu() for w in Ws]
+    bs = [b.detach().cpu() for b in bs]
+
+    def one():
+        with torch.inference_mode():
+            n, _ = dmpnn_ref.chemprop_block(Xv, Xe, ei, rev, Ws, bs)
+            dmpnn_ref.readout(n, bni, B, "sum")
+
+    one()  # warm-up
+    times, t_start = [], time.perf_counter()
+    while (time.perf_counter() - t_start < budget_s and len(times) < 200) or len(times) < 3:
+        t0 = time.perf_counter()
+        one()
+        times.append(time.perf_counter() - t0)
+    med = statistics.median(times)
+    E = ei.shape[1]
+    return {
+        "value": E * depth / med,
+        "unit": "edge-messages/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle/dmpnn_ref.py (ATen CPU restatement of chemprop.py+agg.py) on the same "
+        f"{B}-molecule batch, fp32, torch.set_num_threads({threads}), median of {len(times)} "
+        f"forwards ({med * 1e3:.1f} ms each) after 1 warm-up; host cpus visible {cores}",
+    }
+
+
+def read_pmc_traffic(path, kernel_substr="dmpnn_update"):
+    """Average HBM bytes per launch of the kernel from a rocprofv3 --pmc counter_collection CSV.
+    gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads 1/2 of wide streaming reads
+    -> x2; WRITE_SIZE is exact for 16-B stores.  Both are in KB."""
+    import csv
+
+    fetch, write, n_f, n_w = 0.0, 0.0, set(), set()
+    with open(path) as f:
+        for row in csv.DictReader(f):
+            if kernel_substr not in row.get("Kernel_Name", ""):
+                continue
+            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
+            did = row.get("Dispatch_Id")
+            if name == "FETCH_SIZE":
+                fetch += val
+                n_f.add(did)
+            elif name == "WRITE_SIZE":
+                write += val
+                n_w.add(did)
+    if not n_f and not n_w:
+        return None
+    per = 0.0
+    if n_f:
+        per += 2.0 * fetch / len(n_f) * 1024
+    if n_w:
+        per += write / len(n_w) * 1024
+    return per
+
+
+def main():
+    args = parse()
+    env = dist_env()
+    if env.distributed:
+        torch.cuda.set_device(env.local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", env.local_rank))
+    dev = torch.device("cuda", env.local_rank)
+
+    from notorch_amd import _lib
+    from notorch_amd.data.synth import make_batch
+    from notorch_amd.nn import ChempropBlock, Sum
+    from notorch_amd.nn.gnn import _engine
+
+    _lib.load()  # fail loudly if the HIP extension is missing
+    kind, n_mols, h, depth = WORKLOADS[args.workload]
+    torch.manual_seed(0)
+    batch = make_batch(kind, n_mols, seed=1000 + env.rank)
+    G = batch.collate("nodes")
+    emb_v = torch.nn.EmbeddingBag(42, h, mode="sum")
+    emb_e = torch.nn.EmbeddingBag(13, h, mode="sum")
+    with torch.no_grad():
+        Xv, Xe = emb_v(G.node_feats), emb_e(G.edge_feats)
+    block = ChempropBlock(hidden_dim=h, depth=depth).eval()
+    readout = Sum()
+    Ws = [l.linear.weight.detach().clone() for l in block._chemprop_layers()]
+    bs = [l.linear.bias.detach().clone() for l in block._chemprop_layers()]
+    block = block.to(dev)
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(dev)
+    V, E, B = G.num_nodes, G.num_edges, len(G)
+    torch.cuda.synchronize(dev)
+
+    def step():
+        out = block(Gd)
+        return readout(out)
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+        events = []
+        _engine.UPDATE_EVENTS = events
+        if env.distributed:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        if env.distributed:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+        _engine.UPDATE_EVENTS = None
+
+    upd_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
+    units, secs, rate = aggregate_throughput(E * depth * args.steps, elapsed, device=dev)
+    if env.rank != 0:
+        if env.distributed:
+            dist.destroy_process_group()
+        return
+
+    flops_upd = 2 * E * h * h
+    achieved = flops_upd / (upd_ms * 1e-3) / 1e12
+    traffic = read_pmc_traffic(args.pmc_csv) if args.pmc_csv else None
+    fwd_bytes, fwd_flops = forward_bytes_flops(V, E, B, h, depth)
+    t_step = secs / args.steps
+    t_min = max(fwd_bytes / (PEAK_HBM_GBPS * 1e9), fwd_flops / (PEAK_FP32_MFMA_TFLOPS * 1e12))
+    line = {
+        "metric": METRIC,
+        "value": rate,
+        "unit": "edge-messages/s",
+        "n_gpus": env.world_size,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": t_step * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded QM9-shaped molecules per rank, random-init EmbeddingBag + weights)",
+        "config": {
+            "workload": f"{args.workload}: {n_mols} {kind}-shaped molecules per GPU, D-MPNN depth={depth} "
+            f"hidden={h}, ChempropBlock + Sum readout, reference collate (rev offset by nodes)",
+            "molecules_per_gpu": n_mols,
+            "V_per_gpu": V,
+            "E_per_gpu": E,
+            "hidden": h,
+            "depth": depth,
+            "parallelism": f"molecule-sharded x{env.world_size}, no collective on the forward path",
+        },
+        "roofline": {
+            "kernel": "nt_dmpnn_update (dmpnn_update_f32, fp32 MFMA 16x16x4)",
+            "bound": "mfma",
+            "achieved": achieved,
+            "peak": PEAK_FP32_MFMA_TFLOPS,
+            "unit": "TFLOP/s",
+            "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
+            "traffic": traffic,
+            "launch_ms": upd_ms,
+            "launches_timed": len(events),
+            "flops_per_launch": flops_upd,
+            "alg_bytes_per_launch": update_bytes(V, E, h),
+            "alg_hbm_gbps": update_bytes(V, E, h) / (upd_ms * 1e-3) / 1e9,
+        },
+        "forward_roofline": {
+            "alg_bytes": fwd_bytes,
+            "flops": fwd_flops,
+            "hbm_frac": fwd_bytes / t_step / (PEAK_HBM_GBPS * 1e9),
+            "mfma_frac": fwd_flops / t_step / (PEAK_FP32_MFMA_TFLOPS * 1e12),
+            "binding_frac": t_min / t_step,
+        },
+    }
+    if not args.no_cpu_baseline and env.world_size == 1:
+        line["cpu_baseline"] = cpu_baseline(G, Xv, Xe, Ws, bs, depth, args.cpu_seconds)
+    else:
+        line["cpu_baseline"] = None
+    print(json.dumps(line), flush=True)
+    if env.distributed:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

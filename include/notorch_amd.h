@@ -1,0 +1,128 @@
+/*
+ * notorch_amd.h — C ABI of the MI355X-native D-MPNN message-passing engine.
+ *
+ * This is the drop-in boundary for the bond-message D-MPNN forward of davidegraff/notorch
+ * (`ChempropBlock` + readout + batched-graph collate).  The reference has no native code of its
+ * own: its arithmetic lives in ATen (`index`, `addmm`) and torch_scatter (`scatter_add_`).  Each
+ * entry point below replaces the reference call site named in its comment (paths are relative to
+ * the reference repository root).
+ *
+ * Conventions (all entry points):
+ *   - plain C types only; device pointers are `void*` / typed pointers into memory the CALLER owns
+ *     (PyTorch's caching allocator).  The library never allocates, frees or retains device memory.
+ *   - `stream` is a `hipStream_t` passed as `void*` (NULL = the legacy default stream).  Every call
+ *     is stream-ordered and asynchronous: no device synchronisation, no host<->device copies, so a
+ *     caller may capture the sequence into a hipGraph.
+ *   - return value: 0 = NT_OK; nonzero = error, message via nt_last_error() (thread-local).
+ *   - row-major feature matrices with leading dimension == h (contiguous rows).
+ *   - reference index tensors (edge_index, rev_index, batch_node_index) are int64 exactly as the
+ *     reference stores them (graph.py:208-211); engine-built CSR arrays are int32.
+ */
+#ifndef NOTORCH_AMD_H
+#define NOTORCH_AMD_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define NT_ABI_VERSION 1
+
+#if defined(NT_BUILD)
+#define NT_API __attribute__((visibility("default")))
+#else
+#define NT_API
+#endif
+
+enum nt_status { NT_OK = 0, NT_EINVAL = 1, NT_EHIP = 2, NT_EUNSUPPORTED = 3 };
+
+/* element type of feature matrices */
+enum nt_dtype { NT_F32 = 0, NT_BF16 = 1 };
+
+/* reduce domain of notorch.types.Reduction (types.py:57) with torch_scatter semantics:
+ * sum; mean = sum / max(count, 1); max/min of an empty segment = 0. */
+enum nt_reduce { NT_SUM = 0, NT_MEAN = 1, NT_MAX = 2, NT_MIN = 3 };
+
+/* element-wise activation applied to messages (ChempropLayer.act, chemprop.py:24,37) */
+enum nt_act {
+  NT_ACT_IDENTITY = 0,
+  NT_ACT_RELU = 1,
+  NT_ACT_LEAKY_RELU = 2, /* alpha = negative_slope */
+  NT_ACT_ELU = 3,        /* alpha */
+  NT_ACT_GELU = 4,       /* erf form */
+  NT_ACT_SILU = 5,
+  NT_ACT_TANH = 6,
+  NT_ACT_SIGMOID = 7
+};
+
+/* ABI version of the loaded library (== NT_ABI_VERSION of the header it was built from). */
+NT_API int nt_abi_version(void);
+
+/* Message of the last failed call on this thread ("" if none). */
+NT_API const char* nt_last_error(void);
+
+/* Number of bytes of device workspace nt_csr_build needs for n indices into nseg segments. */
+NT_API size_t nt_csr_workspace_bytes(int64_t n, int64_t nseg);
+
+/*
+ * Build a CSR (segment) view of an int64 index vector: seg_ptr[nseg+1], perm[n] such that
+ * perm[seg_ptr[s] .. seg_ptr[s+1]) lists every i with idx[i] == s in ASCENDING i (stable), which
+ * is the accumulation order of the CPU `scatter_add_` the reference runs.
+ * Replaces the implicit segmentation inside torch_scatter.scatter(..., dest, dim_size=V)
+ * (notorch/nn/gnn/chemprop.py:39, :86) and scatter_*(..., batch_node_index, dim_size=len(G))
+ * (notorch/nn/gnn/agg.py:27, :36, :45).
+ * err_flag (device int32, may be NULL): set to 1 if any idx is outside [0, nseg)  (such entries
+ * are dropped from the CSR instead of being written out of bounds).
+ */
+NT_API int nt_csr_build(const int64_t* idx, int64_t n, int64_t nseg, int32_t* seg_ptr, int32_t* perm,
+                 void* workspace, size_t workspace_bytes, int32_t* err_flag, void* stream);
+
+/*
+ * Initial edge hidden state, optionally fused with the first layer's aggregation:
+ *   H0[e] = Xv[src[e]] + Xe[e]                                  (chemprop.py:82-83)
+ *   S[v]  = reduce_{e: dst[e]=v} act(H0[e])  if S != NULL       (chemprop.py:37-39, layer 0)
+ * src = edge_index[0] (int64, E); (seg_ptr, perm) = nt_csr_build(edge_index[1], E, V).
+ */
+NT_API int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src, const int32_t* seg_ptr,
+                  const int32_t* perm, int64_t V, int64_t E, int64_t h, int act, float act_alpha,
+                  int reduce, int dtype, void* H0, void* S, void* stream);
+
+/*
+ * Segmented reduction over CSR segments:
+ *   out[s] = reduce_{j in [seg_ptr[s], seg_ptr[s+1])} act(X[perm ? perm[j] : j])
+ * Used for the per-layer message aggregation (chemprop.py:37-39), the final node scatter
+ * (chemprop.py:86, act = identity) and the Sum/Mean/Max readouts (agg.py:23-47).
+ */
+NT_API int nt_segment_reduce(const void* X, const int32_t* seg_ptr, const int32_t* perm, int64_t nseg,
+                      int64_t h, int reduce, int act, float act_alpha, int dtype, void* out,
+                      void* stream);
+
+/* Bytes of the packed weight image for one h x h layer (see nt_dmpnn_pack_weight). */
+NT_API size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype);
+
+/*
+ * Repack `nlayers` nn.Linear weights W_l [h_out = h][h_in = h] (row-major, chemprop.py:26) into
+ * the MFMA fragment image nt_dmpnn_update consumes.  W points at nlayers contiguous h*h matrices
+ * (or use nlayers = 1 per layer); Wp at nlayers * nt_dmpnn_packed_weight_bytes(h) bytes.
+ */
+NT_API int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, int dtype, void* Wp,
+                         void* stream);
+
+/*
+ * One fused D-MPNN layer (ChempropLayer.forward, chemprop.py:28-43, wrapped by Residual,
+ * residual.py:27-28), for every directed edge e:
+ *   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b
+ * H, S: E x h and V x h; src = edge_index[0], rev = rev_index (int64, arbitrary gather index);
+ * Wp = nt_dmpnn_pack_weight image of W; b may be NULL (bias=False).  H_out must not alias H.
+ */
+NT_API int nt_dmpnn_update(const void* H, const void* S, const int64_t* src, const int64_t* rev,
+                    const void* Wp, const void* b, int64_t V, int64_t E, int64_t h, int residual,
+                    int act, float act_alpha, int dtype, void* H_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NOTORCH_AMD_H */

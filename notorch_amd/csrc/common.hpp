@@ -1,0 +1,90 @@
+// Shared helpers for the notorch_amd HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/notorch_amd.h"
+
+namespace nt {
+
+// ---- error plumbing (thread-local last error, returned through nt_last_error) ----
+void set_error(const std::string& msg);
+void clear_error();
+
+#define NT_REQUIRE(cond, code, msg)                      \
+  do {                                                   \
+    if (!(cond)) {                                       \
+      ::nt::set_error(std::string(__func__) + ": " + (msg)); \
+      return (code);                                     \
+    }                                                    \
+  } while (0)
+
+#define NT_HIP(expr)                                                                    \
+  do {                                                                                  \
+    hipError_t _e = (expr);                                                             \
+    if (_e != hipSuccess) {                                                             \
+      ::nt::set_error(std::string(__func__) + ": " #expr " -> " + hipGetErrorString(_e)); \
+      return NT_EHIP;                                                                   \
+    }                                                                                   \
+  } while (0)
+
+// launch-error check (kernel launches are asynchronous; this catches bad configurations)
+#define NT_LAUNCH_CHECK() NT_HIP(hipGetLastError())
+
+inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+constexpr int kWave = 64;  // CDNA wavefront width
+
+// ---- element-wise activations (torch formulas; nn.ReLU, nn.LeakyReLU, nn.ELU, nn.GELU, ...) ----
+__device__ __forceinline__ float act_apply(float x, int act, float alpha) {
+  switch (act) {
+    case NT_ACT_RELU: return x > 0.f ? x : 0.f;
+    case NT_ACT_LEAKY_RELU: return x > 0.f ? x : x * alpha;
+    case NT_ACT_ELU: return x > 0.f ? x : alpha * expm1f(x);
+    case NT_ACT_GELU: return 0.5f * x * (1.f + erff(x * 0.70710678118654752f));
+    case NT_ACT_SILU: return x / (1.f + expf(-x));
+    case NT_ACT_TANH: return tanhf(x);
+    case NT_ACT_SIGMOID: return 1.f / (1.f + expf(-x));
+    default: return x;
+  }
+}
+
+// compile-time specialisation for the hot combinations (relu / identity) so the inner loops carry
+// no switch; ACT < 0 means "runtime act".
+template <int ACT>
+__device__ __forceinline__ float act_t(float x, int act, float alpha) {
+  if constexpr (ACT == NT_ACT_IDENTITY) return x;
+  else if constexpr (ACT == NT_ACT_RELU) return x > 0.f ? x : 0.f;
+  else return act_apply(x, act, alpha);
+}
+
+__device__ __forceinline__ float4 act4(float4 v, int act, float alpha) {
+  return make_float4(act_apply(v.x, act, alpha), act_apply(v.y, act, alpha),
+                     act_apply(v.z, act, alpha), act_apply(v.w, act, alpha));
+}
+template <int ACT>
+__device__ __forceinline__ float4 act4_t(float4 v, int act, float alpha) {
+  return make_float4(act_t<ACT>(v.x, act, alpha), act_t<ACT>(v.y, act, alpha),
+                     act_t<ACT>(v.z, act, alpha), act_t<ACT>(v.w, act, alpha));
+}
+
+__device__ __forceinline__ float4 operator+(float4 a, float4 b) {
+  return make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+}
+__device__ __forceinline__ float4 operator-(float4 a, float4 b) {
+  return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
+}
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+inline int grid_for(int64_t work, int block, int cap = 256 * 16) {
+  int64_t g = (work + block - 1) / block;
+  if (g < 1) g = 1;
+  if (g > cap) g = cap;
+  return (int)g;
+}
+
+}  // namespace nt

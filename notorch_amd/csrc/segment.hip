@@ -1,0 +1,256 @@
+// Segmented reductions over a CSR view, and the fused initial-gather + first aggregation.
+//
+//   nt_segment_reduce : out[s] = R_{j in seg s} act(X[perm[j]])       (chemprop.py:37-39, :86;
+//                                                                       agg.py:23-47)
+//   nt_dmpnn_init     : H0[e] = Xv[src[e]] + Xe[e]; S[v] = R_{e->v} act(H0[e])   (chemprop.py:82-83
+//                       fused with layer 0's chemprop.py:37-39)
+//
+// Mapping: one lane per (segment, 16-B column chunk).  Consecutive lanes walk one row, so every
+// gathered row is read as whole 16-B-per-lane contiguous pieces (HBM-coalesced), and the sum over a
+// segment is a sequential loop in ascending edge id — the CPU scatter_add_ order, so the only fp32
+// difference left against the reference is none at all for the sum itself.
+// These kernels are HBM-bound: bytes per segment = (rows read + 1 row written) * h * 4.
+#include <float.h>
+
+#include "common.hpp"
+
+namespace nt {
+
+template <int R>
+struct Reducer {
+  float acc;
+  int n;
+  __device__ __forceinline__ void init() {
+    n = 0;
+    if constexpr (R == NT_MAX) acc = -FLT_MAX;
+    else if constexpr (R == NT_MIN) acc = FLT_MAX;
+    else acc = 0.f;
+  }
+  __device__ __forceinline__ void push(float x) {
+    ++n;
+    if constexpr (R == NT_MAX) acc = (n == 1 || x > acc) ? x : acc;
+    else if constexpr (R == NT_MIN) acc = (n == 1 || x < acc) ? x : acc;
+    else acc += x;
+  }
+  __device__ __forceinline__ float result() const {
+    if constexpr (R == NT_MEAN) return acc / (float)(n > 1 ? n : 1);
+    else if constexpr (R == NT_MAX || R == NT_MIN) return n == 0 ? 0.f : acc;
+    else return acc;
+  }
+};
+
+template <int R>
+struct Reducer4 {
+  Reducer<R> x, y, z, w;
+  __device__ __forceinline__ void init() { x.init(); y.init(); z.init(); w.init(); }
+  __device__ __forceinline__ void push(float4 v) { x.push(v.x); y.push(v.y); z.push(v.z); w.push(v.w); }
+  __device__ __forceinline__ float4 result() const {
+    return make_float4(x.result(), y.result(), z.result(), w.result());
+  }
+};
+
+// ---------------- segment reduce ----------------
+template <int R, int ACT>
+__global__ void __launch_bounds__(256) segment_reduce_vec4(
+    const float4* __restrict__ X, const int32_t* __restrict__ seg_ptr,
+    const int32_t* __restrict__ perm, int64_t nseg, int64_t hv, int act, float alpha,
+    float4* __restrict__ out) {
+  const int64_t total = nseg * hv;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = t / hv, c = t - s * hv;
+    const int32_t b = seg_ptr[s], e = seg_ptr[s + 1];
+    Reducer4<R> r;
+    r.init();
+    for (int32_t j = b; j < e; ++j) {
+      const int64_t row = perm ? perm[j] : j;
+      r.push(act4_t<ACT>(X[row * hv + c], act, alpha));
+    }
+    out[t] = r.result();
+  }
+}
+
+template <int R, int ACT>
+__global__ void __launch_bounds__(256) segment_reduce_scalar(
+    const float* __restrict__ X, const int32_t* __restrict__ seg_ptr,
+    const int32_t* __restrict__ perm, int64_t nseg, int64_t h, int act, float alpha,
+    float* __restrict__ out) {
+  const int64_t total = nseg * h;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = t / h, c = t - s * h;
+    const int32_t b = seg_ptr[s], e = seg_ptr[s + 1];
+    Reducer<R> r;
+    r.init();
+    for (int32_t j = b; j < e; ++j) {
+      const int64_t row = perm ? perm[j] : j;
+      r.push(act_t<ACT>(X[row * h + c], act, alpha));
+    }
+    out[t] = r.result();
+  }
+}
+
+// ---------------- fused init + first aggregation ----------------
+template <int R, int ACT>
+__global__ void __launch_bounds__(256) init_aggregate_vec4(
+    const float4* __restrict__ Xv, const float4* __restrict__ Xe, const int64_t* __restrict__ src,
+    const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm, int64_t V, int64_t hv,
+    int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S) {
+  const int64_t total = V * hv;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = t / hv, c = t - v * hv;
+    const int32_t b = seg_ptr[v], e = seg_ptr[v + 1];
+    Reducer4<R> r;
+    r.init();
+    for (int32_t j = b; j < e; ++j) {
+      const int64_t ed = perm[j];
+      const float4 x = Xv[src[ed] * hv + c] + Xe[ed * hv + c];
+      H0[ed * hv + c] = x;
+      r.push(act4_t<ACT>(x, act, alpha));
+    }
+    S[t] = r.result();
+  }
+}
+
+template <int R, int ACT>
+__global__ void __launch_bounds__(256) init_aggregate_scalar(
+    const float* __restrict__ Xv, const float* __restrict__ Xe, const int64_t* __restrict__ src,
+    const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm, int64_t V, int64_t h,
+    int act, float alpha, float* __restrict__ H0, float* __restrict__ S) {
+  const int64_t total = V * h;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = t / h, c = t - v * h;
+    const int32_t b = seg_ptr[v], e = seg_ptr[v + 1];
+    Reducer<R> r;
+    r.init();
+    for (int32_t j = b; j < e; ++j) {
+      const int64_t ed = perm[j];
+      const float x = Xv[src[ed] * h + c] + Xe[ed * h + c];
+      H0[ed * h + c] = x;
+      r.push(act_t<ACT>(x, act, alpha));
+    }
+    S[t] = r.result();
+  }
+}
+
+// plain init (no aggregation): one lane per (edge, column chunk)
+__global__ void __launch_bounds__(256) init_only_vec4(const float4* __restrict__ Xv,
+                                                      const float4* __restrict__ Xe,
+                                                      const int64_t* __restrict__ src, int64_t E,
+                                                      int64_t hv, float4* __restrict__ H0) {
+  const int64_t total = E * hv;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / hv, c = t - e * hv;
+    H0[t] = Xv[src[e] * hv + c] + Xe[t];
+  }
+}
+__global__ void __launch_bounds__(256) init_only_scalar(const float* __restrict__ Xv,
+                                                        const float* __restrict__ Xe,
+                                                        const int64_t* __restrict__ src, int64_t E,
+                                                        int64_t h, float* __restrict__ H0) {
+  const int64_t total = E * h;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / h, c = t - e * h;
+    H0[t] = Xv[src[e] * h + c] + Xe[t];
+  }
+}
+
+// ---- dispatch helpers: (reduce, act) -> template instance ----
+#define NT_DISPATCH_RA(REDUCE, ACT, LAUNCH)                                  \
+  do {                                                                       \
+    switch (REDUCE) {                                                        \
+      case NT_SUM: { constexpr int R_ = NT_SUM; NT_DISPATCH_A(ACT, LAUNCH); } break;   \
+      case NT_MEAN: { constexpr int R_ = NT_MEAN; NT_DISPATCH_A(ACT, LAUNCH); } break; \
+      case NT_MAX: { constexpr int R_ = NT_MAX; NT_DISPATCH_A(ACT, LAUNCH); } break;   \
+      case NT_MIN: { constexpr int R_ = NT_MIN; NT_DISPATCH_A(ACT, LAUNCH); } break;   \
+    }                                                                        \
+  } while (0)
+#define NT_DISPATCH_A(ACT, LAUNCH)                                                      \
+  do {                                                                                  \
+    if ((ACT) == NT_ACT_IDENTITY) { constexpr int A_ = NT_ACT_IDENTITY; LAUNCH; }        \
+    else if ((ACT) == NT_ACT_RELU) { constexpr int A_ = NT_ACT_RELU; LAUNCH; }           \
+    else { constexpr int A_ = -1; LAUNCH; }                                             \
+  } while (0)
+
+static bool valid_reduce(int r) { return r >= NT_SUM && r <= NT_MIN; }
+static bool valid_act(int a) { return a >= NT_ACT_IDENTITY && a <= NT_ACT_SIGMOID; }
+
+}  // namespace nt
+
+extern "C" int nt_segment_reduce(const void* X, const int32_t* seg_ptr, const int32_t* perm,
+                                 int64_t nseg, int64_t h, int reduce, int act, float act_alpha,
+                                 int dtype, void* out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for segment_reduce");
+  NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
+  NT_REQUIRE(nseg >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  if (nseg == 0) return NT_OK;
+  NT_REQUIRE(X && seg_ptr && out, NT_EINVAL, "NULL pointer");
+  hipStream_t stream = as_stream(stream_);
+  const bool vec = (h % 4 == 0) && aligned16(X) && aligned16(out);
+  if (vec) {
+    const int64_t hv = h / 4;
+    const int grid = grid_for(nseg * hv, 256, 256 * 32);
+    NT_DISPATCH_RA(reduce, act,
+                   (segment_reduce_vec4<R_, A_><<<grid, 256, 0, stream>>>(
+                       (const float4*)X, seg_ptr, perm, nseg, hv, act, act_alpha, (float4*)out)));
+  } else {
+    const int grid = grid_for(nseg * h, 256, 256 * 32);
+    NT_DISPATCH_RA(reduce, act,
+                   (segment_reduce_scalar<R_, A_><<<grid, 256, 0, stream>>>(
+                       (const float*)X, seg_ptr, perm, nseg, h, act, act_alpha, (float*)out)));
+  }
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
+                             const int32_t* seg_ptr, const int32_t* perm, int64_t V, int64_t E,
+                             int64_t h, int act, float act_alpha, int reduce, int dtype, void* H0,
+                             void* S, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for dmpnn_init");
+  NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
+  NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  hipStream_t stream = as_stream(stream_);
+  const bool vec = (h % 4 == 0) && aligned16(Xv) && aligned16(Xe) && aligned16(H0) &&
+                   (S == nullptr || aligned16(S));
+  if (S != nullptr) {
+    if (V == 0) return NT_OK;
+    NT_REQUIRE(seg_ptr && perm, NT_EINVAL, "fused aggregation needs the dst CSR");
+    NT_REQUIRE(E == 0 || (Xv && Xe && src && H0), NT_EINVAL, "NULL pointer");
+    if (vec) {
+      const int64_t hv = h / 4;
+      const int grid = grid_for(V * hv, 256, 256 * 32);
+      NT_DISPATCH_RA(reduce, act,
+                     (init_aggregate_vec4<R_, A_><<<grid, 256, 0, stream>>>(
+                         (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
+                         act_alpha, (float4*)H0, (float4*)S)));
+    } else {
+      const int grid = grid_for(V * h, 256, 256 * 32);
+      NT_DISPATCH_RA(reduce, act,
+                     (init_aggregate_scalar<R_, A_><<<grid, 256, 0, stream>>>(
+                         (const float*)Xv, (const float*)Xe, src, seg_ptr, perm, V, h, act,
+                         act_alpha, (float*)H0, (float*)S)));
+    }
+  } else {
+    if (E == 0) return NT_OK;
+    NT_REQUIRE(Xv && Xe && src && H0, NT_EINVAL, "NULL pointer");
+    if (vec) {
+      const int64_t hv = h / 4;
+      init_only_vec4<<<grid_for(E * hv, 256, 256 * 32), 256, 0, stream>>>(
+          (const float4*)Xv, (const float4*)Xe, src, E, hv, (float4*)H0);
+    } else {
+      init_only_scalar<<<grid_for(E * h, 256, 256 * 32), 256, 0, stream>>>(
+          (const float*)Xv, (const float*)Xe, src, E, h, (float*)H0);
+    }
+  }
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}

@@ -1,0 +1,347 @@
+// Fused D-MPNN layer update on fp32 MFMA (v_mfma_f32_16x16x4_f32, exact f32 fma chain):
+//
+//   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b
+//
+// = ChempropLayer.forward (notorch/nn/gnn/chemprop.py:36-43: gather-sub at :40, nn.Linear at :41)
+//   wrapped in Residual (notorch/nn/residual.py:27-28).  One launch per layer replaces the
+//   reference's two gathers, a subtract, an addmm, a bias add and the residual add.
+//
+// Tiling (one workgroup = 4 waves = 256 lanes, BM edges x all h output columns):
+//   1. gather: the BM rows A[r] = S[src[e0+r]] - act(H[rev[e0+r]]) are formed in registers from
+//      16-B-per-lane coalesced row reads and written to an LDS tile [BM][Kpad+8] (the +8 float pad
+//      makes the ds_read_b128 fragment reads bank-conflict-free).  rev is an
+//      arbitrary gather index (the reference collate does not produce rev = e^1, graph.py:200).
+//   2. MFMA: wave w owns output column tiles [w*CPW, (w+1)*CPW) x all BM rows.  Per 16-deep k
+//      block a lane reads its A fragments with one ds_read_b128 per 16-row tile and its B
+//      fragments with one global_load_dwordx4 per column tile from the pre-packed weight image
+//      (L2-resident, 1 KiB per wave-instruction, prefetched one k-block ahead).  The 16-deep k
+//      block is consumed as 4 MFMAs whose k-lanes are permuted identically in A and B (lane group
+//      g = lane>>4 takes k = 16kb + 4g + s at step s), which lets both operands be 16-B vectors.
+//   3. epilogue: the accumulators go through LDS (reusing the A tile) so that bias, residual and
+//      the store are done with 16-B coalesced row accesses.
+//
+// Roofline: 2*h^2 flop per edge (MFMA) against (3 rows read + 1 row written) * 4h bytes per edge;
+// at h = 300 that is 51 flop/B > the fp32 ridge (~20), i.e. bound by the 157 TF fp32 MFMA peak.
+#include "common.hpp"
+
+namespace nt {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 256;
+constexpr int kWaves = 4;
+
+struct UpdateGeom {
+  int KB;   // 16-deep k blocks (Kpad = 16*KB >= h)
+  int NT;   // 16-wide output column tiles (Npad = 16*NT >= h)
+  int CPW;  // column tiles per wave = ceil(NT / 4)
+  int LDA;  // LDS row stride of the A tile (floats)
+  int LDO;  // LDS row stride of the output tile (floats)
+};
+
+static UpdateGeom geom_for(int64_t h) {
+  UpdateGeom g;
+  g.KB = (int)((h + 15) / 16);
+  g.NT = g.KB;
+  g.CPW = (g.NT + kWaves - 1) / kWaves;
+  g.LDA = g.KB * 16 + 8;  // == 8 (mod 16): conflict-free ds_read_b128 fragment reads
+  g.LDO = g.NT * 16 + 4;  // == 4 (mod 8): conflict-free ds_write_b32 of the 16x16 C layout
+  return g;
+}
+
+template <int BM>
+static size_t lds_bytes(const UpdateGeom& g) {
+  size_t tile = (size_t)BM * (size_t)(g.LDA > g.LDO ? g.LDA : g.LDO) * sizeof(float);
+  return tile + (size_t)BM * 2 * sizeof(int64_t);
+}
+
+// Packed weight image: Wp[kb][nt][lane] is a float4 whose element j is W[n][k] with
+// n = 16nt + (lane & 15), k = 16kb + 4(lane >> 4) + j (zero outside [0,h)).  nn.Linear stores
+// W as [out][in] (chemprop.py:26), so y = A W^T means B[k][n] = W[n][k].
+__global__ void __launch_bounds__(256) pack_weight_f32(const float* __restrict__ W, int64_t nlayers,
+                                                       int64_t h, int KB, int NT,
+                                                       float4* __restrict__ Wp) {
+  const int64_t per_layer = (int64_t)KB * NT * 64;
+  const int64_t total = nlayers * per_layer;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = t / per_layer;
+    int64_t r = t - l * per_layer;
+    const int lane = (int)(r & 63);
+    r >>= 6;
+    const int nt = (int)(r % NT);
+    const int kb = (int)(r / NT);
+    const int64_t n = 16 * nt + (lane & 15);
+    const int64_t k0 = 16 * kb + 4 * (lane >> 4);
+    const float* Wl = W + l * h * h;
+    float v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = (n < h && k0 + j < h) ? Wl[n * h + k0 + j] : 0.f;
+    Wp[t] = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+template <int BM, int CPW, int ACT, bool VEC>
+__global__ void __launch_bounds__(kThreads, 2) dmpnn_update_f32(
+    const float* __restrict__ H, const float* __restrict__ S, const int64_t* __restrict__ src,
+    const int64_t* __restrict__ rev, const float4* __restrict__ Wp, const float* __restrict__ bias,
+    int64_t V, int64_t E, int h, int KB, int NT, int LDA, int LDO, int residual, int act,
+    float alpha, float* __restrict__ H_out) {
+  constexpr int MT = BM / 16;  // 16-row tiles per workgroup
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int64_t e0 = (int64_t)blockIdx.x * BM;
+  const int tile_floats = BM * (LDA > LDO ? LDA : LDO);
+  int64_t* s_src = reinterpret_cast<int64_t*>(smem + tile_floats);
+  int64_t* s_rev = s_src + BM;
+
+  // ---- 0. edge indices of this tile -> LDS (out-of-range indices become -1 = zero row) ----
+  if (tid < BM) {
+    const int64_t e = e0 + tid;
+    int64_t s = -1, q = -1;
+    if (e < E) {
+      s = src[e];
+      q = rev[e];
+      if (s < 0 || s >= V) s = -1;
+      if (q < 0 || q >= E) q = -1;
+    }
+    s_src[tid] = s;
+    s_rev[tid] = q;
+  }
+  __syncthreads();
+
+  // ---- 1. gather A = S[src] - act(H[rev]) into the LDS tile (k padded with zeros to 16*KB) ----
+  if constexpr (VEC) {
+    const int kv = KB * 4;  // float4 chunks per padded row
+    const int hv = h >> 2;
+    const float4* S4 = reinterpret_cast<const float4*>(S);
+    const float4* H4 = reinterpret_cast<const float4*>(H);
+    for (int i = tid; i < BM * kv; i += kThreads) {
+      const int r = i / kv;
+      const int c = i - r * kv;
+      float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (c < hv) {
+        const int64_t s = s_src[r], q = s_rev[r];
+        const float4 sv = s >= 0 ? S4[s * hv + c] : a;
+        const float4 mv = q >= 0 ? act4_t<ACT>(H4[q * hv + c], act, alpha) : a;
+        a = sv - mv;
+      }
+      *reinterpret_cast<float4*>(&smem[r * LDA + 4 * c]) = a;
+    }
+  } else {
+    const int kp = KB * 16;
+    for (int i = tid; i < BM * kp; i += kThreads) {
+      const int r = i / kp;
+      const int c = i - r * kp;
+      float a = 0.f;
+      if (c < h) {
+        const int64_t s = s_src[r], q = s_rev[r];
+        const float sv = s >= 0 ? S[s * h + c] : 0.f;
+        const float mv = q >= 0 ? act_t<ACT>(H[q * h + c], act, alpha) : 0.f;
+        a = sv - mv;
+      }
+      smem[r * LDA + c] = a;
+    }
+  }
+  __syncthreads();
+
+  // ---- 2. MFMA: acc[mt][ct] += A[16mt.., k] * B[k, 16(nt0+ct)..] ----
+  const int nt0 = wave * CPW;
+  f32x4 acc[MT][CPW];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int ct = 0; ct < CPW; ++ct) acc[mt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 bcur[CPW], bnext[CPW];
+#pragma unroll
+  for (int ct = 0; ct < CPW; ++ct) {
+    const int nt = nt0 + ct;
+    bcur[ct] = nt < NT ? Wp[(int64_t)nt * 64 + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  const float* a_base = smem + (lane & 15) * LDA + 4 * (lane >> 4);
+  for (int kb = 0; kb < KB; ++kb) {
+    if (kb + 1 < KB) {
+#pragma unroll
+      for (int ct = 0; ct < CPW; ++ct) {
+        const int nt = nt0 + ct;
+        bnext[ct] = nt < NT ? Wp[((int64_t)(kb + 1) * NT + nt) * 64 + lane]
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+    float4 a[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+      a[mt] = *reinterpret_cast<const float4*>(a_base + mt * 16 * LDA + 16 * kb);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+        const float av = s == 0 ? a[mt].x : s == 1 ? a[mt].y : s == 2 ? a[mt].z : a[mt].w;
+#pragma unroll
+        for (int ct = 0; ct < CPW; ++ct) {
+          const float bv = s == 0 ? bcur[ct].x : s == 1 ? bcur[ct].y : s == 2 ? bcur[ct].z : bcur[ct].w;
+          acc[mt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[mt][ct], 0, 0, 0);
+        }
+      }
+    }
+#pragma unroll
+    for (int ct = 0; ct < CPW; ++ct) bcur[ct] = bnext[ct];
+  }
+  __syncthreads();  // every wave is done reading the A tile
+
+  // ---- 3. epilogue: C fragments -> LDS (C/D map: col = lane&15, row = 4*(lane>>4) + j) ----
+#pragma unroll
+  for (int ct = 0; ct < CPW; ++ct) {
+    const int nt = nt0 + ct;
+    if (nt < NT) {
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int row = 16 * mt + 4 * (lane >> 4) + j;
+          smem[row * LDO + 16 * nt + (lane & 15)] = acc[mt][ct][j];
+        }
+      }
+    }
+  }
+  __syncthreads();
+
+  if constexpr (VEC) {
+    const int hv = h >> 2;
+    const float4* H4 = reinterpret_cast<const float4*>(H);
+    const float4* b4 = reinterpret_cast<const float4*>(bias);
+    float4* O4 = reinterpret_cast<float4*>(H_out);
+    for (int i = tid; i < BM * hv; i += kThreads) {
+      const int r = i / hv;
+      const int c = i - r * hv;
+      const int64_t e = e0 + r;
+      if (e < E) {
+        float4 o = *reinterpret_cast<const float4*>(&smem[r * LDO + 4 * c]);
+        if (bias) o = o + b4[c];
+        if (residual) o = H4[e * hv + c] + o;
+        O4[e * hv + c] = o;
+      }
+    }
+  } else {
+    for (int i = tid; i < BM * h; i += kThreads) {
+      const int r = i / h;
+      const int c = i - r * h;
+      const int64_t e = e0 + r;
+      if (e < E) {
+        float o = smem[r * LDO + c];
+        if (bias) o = o + bias[c];
+        if (residual) o = H[e * h + c] + o;
+        H_out[e * h + c] = o;
+      }
+    }
+  }
+}
+
+template <int BM, int CPW, int ACT, bool VEC>
+static int launch_update(const float* H, const float* S, const int64_t* src, const int64_t* rev,
+                         const float4* Wp, const float* b, int64_t V, int64_t E, int h,
+                         const UpdateGeom& g, int residual, int act, float alpha, float* H_out,
+                         hipStream_t stream) {
+  const size_t lds = lds_bytes<BM>(g);
+  NT_REQUIRE(lds <= 160 * 1024, NT_EUNSUPPORTED, "hidden size too large for the LDS tile");
+  auto kern = dmpnn_update_f32<BM, CPW, ACT, VEC>;
+  if (lds > 64 * 1024) NT_HIP(hipFuncSetAttribute((const void*)kern,
+                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                  (int)lds));
+  const int64_t grid = (E + BM - 1) / BM;
+  NT_REQUIRE(grid < (int64_t(1) << 31), NT_EINVAL, "too many edges");
+  kern<<<(unsigned)grid, kThreads, lds, stream>>>(H, S, src, rev, Wp, b, V, E, h, g.KB, g.NT,
+                                                  g.LDA, g.LDO, residual, act, alpha, H_out);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+template <int BM, int CPW>
+static int dispatch_act_vec(const float* H, const float* S, const int64_t* src, const int64_t* rev,
+                            const float4* Wp, const float* b, int64_t V, int64_t E, int h,
+                            const UpdateGeom& g, int residual, int act, float alpha, float* H_out,
+                            bool vec, hipStream_t stream) {
+  if (act == NT_ACT_RELU) {
+    return vec ? launch_update<BM, CPW, NT_ACT_RELU, true>(H, S, src, rev, Wp, b, V, E, h, g,
+                                                           residual, act, alpha, H_out, stream)
+               : launch_update<BM, CPW, NT_ACT_RELU, false>(H, S, src, rev, Wp, b, V, E, h, g,
+                                                            residual, act, alpha, H_out, stream);
+  }
+  return vec ? launch_update<BM, CPW, -1, true>(H, S, src, rev, Wp, b, V, E, h, g, residual, act,
+                                                alpha, H_out, stream)
+             : launch_update<BM, CPW, -1, false>(H, S, src, rev, Wp, b, V, E, h, g, residual, act,
+                                                 alpha, H_out, stream);
+}
+
+template <int BM>
+static int dispatch_cpw(const float* H, const float* S, const int64_t* src, const int64_t* rev,
+                        const float4* Wp, const float* b, int64_t V, int64_t E, int h,
+                        const UpdateGeom& g, int residual, int act, float alpha, float* H_out,
+                        bool vec, hipStream_t stream) {
+#define NT_CASE(C)                                                                          \
+  case C:                                                                                   \
+    return dispatch_act_vec<BM, C>(H, S, src, rev, Wp, b, V, E, h, g, residual, act, alpha, \
+                                   H_out, vec, stream);
+  switch (g.CPW) {
+    NT_CASE(1) NT_CASE(2) NT_CASE(3) NT_CASE(4) NT_CASE(5) NT_CASE(6) NT_CASE(7) NT_CASE(8)
+    default:
+      set_error("nt_dmpnn_update: hidden size > 512 is not supported by the fp32 MFMA kernel");
+      return NT_EUNSUPPORTED;
+  }
+#undef NT_CASE
+}
+
+}  // namespace nt
+
+extern "C" size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype) {
+  (void)dtype;
+  if (h <= 0) return 0;
+  const nt::UpdateGeom g = nt::geom_for(h);
+  return (size_t)g.KB * g.NT * 64 * sizeof(float4);
+}
+
+extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, int dtype, void* Wp,
+                                    void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for pack_weight");
+  NT_REQUIRE(nlayers >= 0 && h > 0 && h <= 512, NT_EINVAL, "bad sizes (1 <= h <= 512)");
+  if (nlayers == 0) return NT_OK;
+  NT_REQUIRE(W && Wp && aligned16(Wp), NT_EINVAL, "NULL or misaligned pointer");
+  const UpdateGeom g = geom_for(h);
+  const int64_t total = nlayers * g.KB * g.NT * 64;
+  pack_weight_f32<<<grid_for(total, 256), 256, 0, as_stream(stream_)>>>(
+      (const float*)W, nlayers, h, g.KB, g.NT, (float4*)Wp);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
+                               const int64_t* rev, const void* Wp, const void* b, int64_t V,
+                               int64_t E, int64_t h, int residual, int act, float act_alpha,
+                               int dtype, void* H_out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for dmpnn_update");
+  NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
+  NT_REQUIRE(V >= 0 && E >= 0 && h > 0 && h <= 512, NT_EINVAL, "bad sizes (1 <= h <= 512)");
+  if (E == 0) return NT_OK;
+  NT_REQUIRE(H && S && src && rev && Wp && H_out, NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(H != H_out, NT_EINVAL, "H_out must not alias H");
+  NT_REQUIRE(aligned16(Wp), NT_EINVAL, "Wp must be 16-byte aligned");
+  const UpdateGeom g = geom_for(h);
+  const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(S) && aligned16(H_out) &&
+                   (b == nullptr || aligned16(b));
+  hipStream_t stream = as_stream(stream_);
+  // 64-edge tiles while two workgroups still fit one CU's LDS (h <= 304), else 32-edge tiles.
+  if (lds_bytes<64>(g) <= 80 * 1024)
+    return dispatch_cpw<64>((const float*)H, (const float*)S, src, rev, (const float4*)Wp,
+                            (const float*)b, V, E, (int)h, g, residual, act, act_alpha,
+                            (float*)H_out, vec, stream);
+  return dispatch_cpw<32>((const float*)H, (const float*)S, src, rev, (const float4*)Wp,
+                          (const float*)b, V, E, (int)h, g, residual, act, act_alpha,
+                          (float*)H_out, vec, stream);
+}

@@ -1,0 +1,263 @@
+"""Graph / BatchedGraph with the reference's field names and semantics, plus the device layout.
+
+Mirrors ``notorch/data/models/graph.py`` (Graph :14-164, BatchedGraph :167-247) and
+``notorch/utils/utils.py:34-40`` (``UpdateMixin.update``): same dataclass fields, ``num_nodes``,
+``num_edges``, ``device``, ``.to``, ``len()`` and shallow-copy ``update``.
+
+What is new is :class:`DeviceLayout`, the CSR view the kernels consume:
+
+* ``dst_ptr[V+1]`` / ``dst_perm[E]`` (int32): in-edges of every node in ascending edge id
+  (stable), i.e. the order in which the reference's CPU ``scatter_add_`` accumulates.
+* ``mol_ptr[B+1]`` / ``mol_perm[V]`` (int32, ``mol_perm`` None when ``batch_node_index`` is
+  sorted, which the collate guarantees): the nodes of every molecule, for the readouts.
+
+``BatchedGraph.from_graphs`` (the collate, reference ``graph.py:186-223``) is vectorised and
+builds that layout on the host, so it ships to the device with ``.to``.  A graph that arrives
+without a layout (built by hand, or edited) gets one on the device via ``nt_csr_build``.
+
+The reference collate offsets ``rev_index`` by the cumulative NODE count (``graph.py:200`` with
+``:204``) instead of the cumulative edge count.  ``rev_offset="nodes"`` (default) reproduces that
+bit for bit; ``rev_offset="edges"`` is the corrected collate.
+"""
+from __future__ import annotations
+
+from copy import copy
+from dataclasses import InitVar, dataclass, field
+from typing import Iterable, Literal, Optional
+
+import numpy as np
+import torch
+from torch import Tensor
+
+RevOffset = Literal["nodes", "edges"]
+
+
+class UpdateMixin:
+    """``notorch/utils/utils.py:34-40``: ``update`` returns a shallow copy (or self) with fields set."""
+
+    def update(self, in_place: bool = False, **kwargs):
+        other = self if in_place else copy(self)
+        for key, val in kwargs.items():
+            setattr(other, key, val)
+        return other
+
+
+@dataclass(eq=False)
+class DeviceLayout:
+    """CSR view of a (batched) graph consumed by the kernels.  All int32."""
+
+    dst_ptr: Optional[Tensor] = None
+    dst_perm: Optional[Tensor] = None
+    mol_ptr: Optional[Tensor] = None
+    mol_perm: Optional[Tensor] = None
+    # identity of the tensors the layout was derived from (cache validity)
+    edge_index: Optional[Tensor] = None
+    batch_node_index: Optional[Tensor] = None
+    validated: bool = False  # src/dst in [0,V), rev in [0,E) checked
+
+    def to(self, device, edge_index: Tensor, batch_node_index: Optional[Tensor]) -> "DeviceLayout":
+        mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731
+        return DeviceLayout(
+            mv(self.dst_ptr),
+            mv(self.dst_perm),
+            mv(self.mol_ptr),
+            mv(self.mol_perm),
+            edge_index,
+            batch_node_index,
+            self.validated,
+        )
+
+
+@dataclass(repr=False, eq=False)
+class Graph(UpdateMixin):
+    """A single graph: ``node_feats`` V x *, ``edge_feats`` E x *, ``edge_index`` 2 x E,
+    ``rev_index`` E (reference ``graph.py:14-39``)."""
+
+    node_feats: Tensor
+    edge_feats: Tensor
+    edge_index: Tensor
+    rev_index: Tensor
+    device_: InitVar[object] = field(default=None, kw_only=True)
+
+    def __post_init__(self, device_):
+        self._device = device_
+        self._nt_layout: Optional[DeviceLayout] = None
+        self.to(device_)
+
+    @property
+    def num_nodes(self) -> int:
+        return len(self.node_feats)
+
+    @property
+    def num_edges(self) -> int:
+        return len(self.edge_feats)
+
+    @property
+    def device(self):
+        return self._device
+
+    def to(self, device):
+        self._device = device
+        self.node_feats = self.node_feats.to(device)
+        self.edge_feats = self.edge_feats.to(device)
+        self.edge_index = self.edge_index.to(device)
+        self.rev_index = self.rev_index.to(device)
+        self._move_layout(device)
+        return self
+
+    def _move_layout(self, device):
+        lay = getattr(self, "_nt_layout", None)
+        if lay is not None and device is not None:
+            self._nt_layout = lay.to(device, self.edge_index, getattr(self, "batch_node_index", None))
+
+    @property
+    def A(self) -> Tensor:
+        """Dense adjacency matrix (reference ``graph.py:55-64``)."""
+        src, dest = self.edge_index.unbind(0)
+        A = torch.zeros(self.num_nodes, self.num_nodes)
+        A[src, dest] = 1
+        return A
+
+    @property
+    def P(self) -> Tensor:
+        """Markov transition matrix (reference ``graph.py:66-72``)."""
+        A = self.A
+        return A / A.sum(1, keepdim=True)
+
+    @property
+    def dense2sparse(self) -> Tensor:
+        """V x V map from a dense (u, v) pair to its edge id, -1 if absent (``graph.py:74-94``)."""
+        src, dest = self.edge_index.unbind(0)
+        index = -torch.ones(self.num_nodes, self.num_nodes, dtype=torch.long)
+        index[src, dest] = torch.arange(self.edge_index.shape[1])
+        return index
+
+    def __repr__(self) -> str:
+        return (
+            f"{type(self).__name__}(node_feats: Tensor(shape={tuple(self.node_feats.shape)}), "
+            f"edge_feats: Tensor(shape={tuple(self.edge_feats.shape)}), device={self._device})"
+        )
+
+
+@dataclass(repr=False, eq=False, kw_only=True)
+class BatchedGraph(Graph):
+    """A batch of graphs (reference ``graph.py:167-247``)."""
+
+    batch_node_index: Tensor
+    batch_edge_index: Tensor
+    size: InitVar[Optional[int]] = None
+
+    def __post_init__(self, device_, size):
+        super().__post_init__(device_)
+        # reference graph.py:184 stores a 0-d tensor when size is None (len() then fails);
+        # we store an int either way.
+        self._size = int(self.batch_node_index.max()) + 1 if size is None else int(size)
+
+    def __len__(self) -> int:
+        return self._size
+
+    def to(self, device):
+        self._device = device
+        self.node_feats = self.node_feats.to(device)
+        self.edge_feats = self.edge_feats.to(device)
+        self.edge_index = self.edge_index.to(device)
+        self.rev_index = self.rev_index.to(device)
+        self.batch_node_index = self.batch_node_index.to(device)
+        self.batch_edge_index = self.batch_edge_index.to(device)
+        self._move_layout(device)
+        return self
+
+    @classmethod
+    def from_graphs(cls, Gs: Iterable[Graph], rev_offset: RevOffset = "nodes") -> "BatchedGraph":
+        """Collate (reference ``graph.py:186-223``), vectorised, + host-built CSR layout.
+
+        ``rev_offset="nodes"`` reproduces the reference exactly, including the offset of
+        ``rev_index`` by the cumulative node count (``graph.py:200``); ``"edges"`` fixes it.
+        """
+        Gs = list(Gs)
+        if len(Gs) == 0:
+            raise ValueError("from_graphs needs at least one graph")
+        if rev_offset not in ("nodes", "edges"):
+            raise ValueError(f"rev_offset must be 'nodes' or 'edges', got {rev_offset!r}")
+        n_nodes = torch.tensor([len(G.node_feats) for G in Gs], dtype=torch.long)
+        n_edges = torch.tensor([len(G.edge_feats) for G in Gs], dtype=torch.long)
+        node_off = torch.cumsum(n_nodes, 0) - n_nodes
+        edge_off = torch.cumsum(n_edges, 0) - n_edges
+        B = len(Gs)
+        graph_ids = torch.arange(B)
+        node_feats = torch.cat([G.node_feats for G in Gs], dim=0)
+        edge_feats = torch.cat([G.edge_feats for G in Gs], dim=0)
+        n_ei = torch.tensor([G.edge_index.shape[-1] for G in Gs], dtype=torch.long)
+        n_rev = torch.tensor([len(G.rev_index) for G in Gs], dtype=torch.long)
+        edge_index = torch.cat([G.edge_index.reshape(2, -1).long() for G in Gs], dim=1)
+        edge_index = edge_index + torch.repeat_interleave(node_off, n_ei).unsqueeze(0)
+        rev_base = node_off if rev_offset == "nodes" else edge_off
+        rev_index = torch.cat([G.rev_index.long() for G in Gs], dim=0)
+        rev_index = rev_index + torch.repeat_interleave(rev_base, n_rev)
+        batch_node_index = torch.repeat_interleave(graph_ids, n_nodes)
+        batch_edge_index = torch.repeat_interleave(graph_ids, n_edges)
+        BG = cls(
+            node_feats,
+            edge_feats,
+            edge_index,
+            rev_index,
+            device_=None,
+            batch_node_index=batch_node_index,
+            batch_edge_index=batch_edge_index,
+            size=B,
+        )
+        BG._nt_layout = host_layout(edge_index, rev_index, len(node_feats), batch_node_index, B)
+        if Gs[-1].device is not None:  # reference passes device_=G.device of the last graph
+            BG.to(Gs[-1].device)
+        return BG
+
+    def __repr__(self) -> str:
+        return super().__repr__()[:-1] + f", batch_size={len(self)})"
+
+
+def host_layout(
+    edge_index: Tensor,
+    rev_index: Tensor,
+    num_nodes: int,
+    batch_node_index: Optional[Tensor] = None,
+    num_graphs: Optional[int] = None,
+) -> DeviceLayout:
+    """Build the CSR layout on the host (numpy stable argsort == ascending edge id per node)."""
+    ei = edge_index.detach().cpu().numpy()
+    E = ei.shape[1]
+    src, dst = ei[0], ei[1]
+    rev = rev_index.detach().cpu().numpy()
+    validated = bool(
+        E == 0
+        or (
+            src.min() >= 0
+            and src.max() < num_nodes
+            and dst.min() >= 0
+            and dst.max() < num_nodes
+            and rev.min() >= 0
+            and rev.max() < E
+        )
+    )
+    if not validated:
+        # leave the layout to the device path, which raises IndexError like the reference's gather
+        return None  # type: ignore[return-value]
+    dst_perm = np.argsort(dst, kind="stable").astype(np.int32)
+    counts = np.bincount(dst, minlength=num_nodes)
+    dst_ptr = np.zeros(num_nodes + 1, dtype=np.int32)
+    np.cumsum(counts, out=dst_ptr[1:])
+    lay = DeviceLayout(
+        torch.from_numpy(dst_ptr),
+        torch.from_numpy(dst_perm),
+        edge_index=edge_index,
+        validated=True,
+    )
+    if batch_node_index is not None and num_graphs is not None:
+        b = batch_node_index.detach().cpu().numpy()
+        if b.size == 0 or (b.min() >= 0 and b.max() < num_graphs):
+            mol_ptr = np.zeros(num_graphs + 1, dtype=np.int32)
+            np.cumsum(np.bincount(b, minlength=num_graphs), out=mol_ptr[1:])
+            sorted_ = b.size < 2 or bool(np.all(b[1:] >= b[:-1]))
+            lay.mol_ptr = torch.from_numpy(mol_ptr)
+            lay.mol_perm = None if sorted_ else torch.from_numpy(np.argsort(b, kind="stable").astype(np.int32))
+            lay.batch_node_index = batch_node_index
+    return lay

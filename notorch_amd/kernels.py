@@ -1,0 +1,255 @@
+"""Tensor-level wrappers over the C-ABI (``include/notorch_amd.h``).
+
+Each wrapper validates device / dtype / shape / contiguity up front (raising ``TypeError`` /
+``ValueError`` the way the reference's ATen ops would raise for bad inputs), allocates outputs with
+``torch.empty`` on the tensor's device (PyTorch's caching allocator owns all memory) and launches on
+``torch.cuda.current_stream()``.  Nothing here computes on the host: a CPU tensor is an error.
+"""
+from __future__ import annotations
+
+import torch
+from torch import Tensor
+
+from notorch_amd import _lib
+from notorch_amd._lib import NT_F32, REDUCE_CODES, check
+
+__all__ = [
+    "csr_build",
+    "dmpnn_init",
+    "segment_reduce",
+    "pack_weights",
+    "dmpnn_update",
+    "act_code",
+    "reduce_code",
+]
+
+
+def _ptr(t: Tensor | None) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def _stream(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _require_device(*ts: Tensor | None) -> torch.device:
+    dev = None
+    for t in ts:
+        if t is None:
+            continue
+        if t.device.type != "cuda":
+            raise RuntimeError(
+                "notorch_amd kernels run on ROCm devices only; got a tensor on "
+                f"'{t.device}'. Move the graph with G.to('cuda') first."
+            )
+        if dev is None:
+            dev = t.device
+        elif t.device != dev:
+            raise ValueError(f"tensors on different devices: {dev} vs {t.device}")
+    assert dev is not None
+    return dev
+
+
+def _require_f32(name: str, t: Tensor) -> None:
+    if t.dtype != torch.float32:
+        raise TypeError(f"{name} must be float32 on the fp32 kernel path, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _require_i64(name: str, t: Tensor) -> None:
+    if t.dtype != torch.int64:
+        raise TypeError(f"{name} must be int64 (reference index dtype), got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def reduce_code(reduce: str) -> int:
+    try:
+        return REDUCE_CODES[reduce]
+    except KeyError:
+        raise ValueError(f"unsupported reduce '{reduce}', expected one of {list(REDUCE_CODES)}")
+
+
+def act_code(act: torch.nn.Module) -> tuple[int, float]:
+    """Map an activation module instance to the kernel's (code, alpha)."""
+    nn = torch.nn
+    if isinstance(act, nn.ReLU):
+        return _lib.NT_ACT_RELU, 0.0
+    if isinstance(act, nn.Identity):
+        return _lib.NT_ACT_IDENTITY, 0.0
+    if isinstance(act, nn.LeakyReLU):
+        return _lib.NT_ACT_LEAKY_RELU, float(act.negative_slope)
+    if isinstance(act, nn.ELU):
+        return _lib.NT_ACT_ELU, float(act.alpha)
+    if isinstance(act, nn.GELU):
+        if act.approximate != "none":
+            raise NotImplementedError("GELU(approximate='tanh') is not implemented in the kernels")
+        return _lib.NT_ACT_GELU, 0.0
+    if isinstance(act, nn.SiLU):
+        return _lib.NT_ACT_SILU, 0.0
+    if isinstance(act, nn.Tanh):
+        return _lib.NT_ACT_TANH, 0.0
+    if isinstance(act, nn.Sigmoid):
+        return _lib.NT_ACT_SIGMOID, 0.0
+    raise NotImplementedError(
+        f"activation {type(act).__name__} has no kernel implementation "
+        "(supported: ReLU, Identity, LeakyReLU, ELU, GELU, SiLU, Tanh, Sigmoid)"
+    )
+
+
+def csr_build(idx: Tensor, nseg: int, *, check_bounds: bool = True) -> tuple[Tensor, Tensor]:
+    """Stable CSR of an int64 index vector: (seg_ptr[nseg+1] int32, perm[n] int32).
+
+    ``check_bounds`` synchronises once to raise ``IndexError`` for out-of-range indices, like the
+    reference's scatter would; the kernel itself never reads or writes out of bounds.
+    """
+    dev = _require_device(idx)
+    _require_i64("idx", idx)
+    if idx.dim() != 1:
+        raise ValueError("idx must be 1-D")
+    n = idx.numel()
+    if nseg < 0:
+        raise ValueError("nseg must be >= 0")
+    lib = _lib.load()
+    seg_ptr = torch.empty(nseg + 1, dtype=torch.int32, device=dev)
+    perm = torch.empty(max(n, 1), dtype=torch.int32, device=dev)[:n]
+    ws_bytes = lib.nt_csr_workspace_bytes(n, nseg)
+    ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
+    err = torch.zeros(1, dtype=torch.int32, device=dev)
+    check(
+        lib.nt_csr_build(
+            _ptr(idx), n, nseg, _ptr(seg_ptr), _ptr(perm), _ptr(ws), ws_bytes, _ptr(err), _stream(dev)
+        )
+    )
+    if check_bounds and n > 0 and int(err.item()) != 0:
+        raise IndexError(f"index out of range for a scatter into {nseg} rows")
+    return seg_ptr, perm
+
+
+def dmpnn_init(
+    Xv: Tensor,
+    Xe: Tensor,
+    src: Tensor,
+    seg_ptr: Tensor | None = None,
+    perm: Tensor | None = None,
+    *,
+    act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
+    reduce: str = "sum",
+) -> tuple[Tensor, Tensor | None]:
+    """H0 = Xv[src] + Xe, optionally fused with S = scatter(act(H0), dst) (needs the dst CSR)."""
+    dev = _require_device(Xv, Xe, src, seg_ptr, perm)
+    _require_f32("node_feats", Xv)
+    _require_f32("edge_feats", Xe)
+    _require_i64("src", src)
+    if Xv.dim() != 2 or Xe.dim() != 2 or Xv.shape[1] != Xe.shape[1]:
+        raise RuntimeError(
+            f"node_feats {tuple(Xv.shape)} and edge_feats {tuple(Xe.shape)} must be V x h and E x h"
+        )
+    V, h = Xv.shape
+    E = Xe.shape[0]
+    if src.numel() != E:
+        raise ValueError("src must have one entry per edge")
+    H0 = torch.empty(E, h, dtype=Xv.dtype, device=dev)
+    S = None
+    if seg_ptr is not None:
+        S = torch.empty(V, h, dtype=Xv.dtype, device=dev)
+    lib = _lib.load()
+    check(
+        lib.nt_dmpnn_init(
+            _ptr(Xv), _ptr(Xe), _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h, act[0], act[1],
+            reduce_code(reduce), NT_F32, _ptr(H0), _ptr(S), _stream(dev),
+        )
+    )
+    return H0, S
+
+
+def segment_reduce(
+    X: Tensor,
+    seg_ptr: Tensor,
+    perm: Tensor | None,
+    nseg: int,
+    *,
+    reduce: str = "sum",
+    act: tuple[int, float] = (_lib.NT_ACT_IDENTITY, 0.0),
+    out: Tensor | None = None,
+) -> Tensor:
+    """out[s] = reduce over rows X[perm[j]] (j in segment s) of act(row); empty segment -> 0."""
+    dev = _require_device(X, seg_ptr, perm)
+    _require_f32("X", X)
+    if X.dim() != 2:
+        raise ValueError("X must be 2-D")
+    if seg_ptr.dtype != torch.int32 or seg_ptr.numel() != nseg + 1:
+        raise ValueError("seg_ptr must be int32 of length nseg + 1")
+    h = X.shape[1]
+    if out is None:
+        out = torch.empty(nseg, h, dtype=X.dtype, device=dev)
+    lib = _lib.load()
+    check(
+        lib.nt_segment_reduce(
+            _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce), act[0], act[1], NT_F32,
+            _ptr(out), _stream(dev),
+        )
+    )
+    return out
+
+
+def packed_weight_numel(h: int) -> int:
+    return _lib.load().nt_dmpnn_packed_weight_bytes(h, NT_F32) // 4
+
+
+def pack_weights(W: Tensor) -> Tensor:
+    """Pack one nn.Linear weight [h, h] (or a stack [L, h, h]) into the MFMA fragment image."""
+    dev = _require_device(W)
+    _require_f32("weight", W)
+    if W.dim() == 2:
+        W3 = W.unsqueeze(0)
+    else:
+        W3 = W
+    L, h, h2 = W3.shape
+    if h != h2:
+        raise ValueError(f"ChempropLayer weight must be square, got {tuple(W.shape)}")
+    Wp = torch.empty(L, packed_weight_numel(h), dtype=torch.float32, device=dev)
+    lib = _lib.load()
+    check(lib.nt_dmpnn_pack_weight(_ptr(W3), L, h, NT_F32, _ptr(Wp), _stream(dev)))
+    return Wp[0] if W.dim() == 2 else Wp
+
+
+def dmpnn_update(
+    H: Tensor,
+    S: Tensor,
+    src: Tensor,
+    rev: Tensor,
+    Wp: Tensor,
+    bias: Tensor | None,
+    *,
+    residual: bool = True,
+    act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
+    out: Tensor | None = None,
+) -> Tensor:
+    """H_out = (residual ? H : 0) + (S[src] - act(H[rev])) @ W^T + b   (one fused launch)."""
+    dev = _require_device(H, S, src, rev, Wp, bias, out)
+    _require_f32("H", H)
+    _require_f32("S", S)
+    _require_i64("src", src)
+    _require_i64("rev_index", rev)
+    E, h = H.shape
+    V = S.shape[0]
+    if S.shape[1] != h or src.numel() != E or rev.numel() != E:
+        raise ValueError("shape mismatch between H, S, src and rev_index")
+    if Wp.numel() != packed_weight_numel(h):
+        raise ValueError("Wp is not a packed weight image for this hidden size")
+    if bias is not None:
+        _require_f32("bias", bias)
+        if bias.numel() != h:
+            raise ValueError("bias must have h entries")
+    if out is None:
+        out = torch.empty_like(H)
+    lib = _lib.load()
+    check(
+        lib.nt_dmpnn_update(
+            _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
+            act[0], act[1], NT_F32, _ptr(out), _stream(dev),
+        )
+    )
+    return out

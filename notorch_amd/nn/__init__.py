@@ -1,0 +1,15 @@
+from notorch_amd.nn.gnn import (
+    Aggregation,
+    ChempropBlock,
+    ChempropLayer,
+    GraphEmbedding,
+    Max,
+    Mean,
+    Min,
+    Sum,
+)
+from notorch_amd.nn.residual import Residual
+
+__all__ = [
+    "Aggregation", "ChempropBlock", "ChempropLayer", "GraphEmbedding", "Max", "Mean", "Min", "Sum", "Residual",
+]

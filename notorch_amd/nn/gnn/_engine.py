@@ -1,0 +1,245 @@
+"""Device engine behind ChempropBlock / readouts: layout management, the fused layer loop and the
+autograd wrapper.
+
+Forward (per call, all on ``torch.cuda.current_stream()``, inputs already resident):
+
+    nt_dmpnn_init       H0 = Xv[src] + Xe  fused with  S = scatter(act(H0), dst)   chemprop.py:82-83,37-39
+    for l in 0..d-1:
+      nt_dmpnn_update   H_{l+1} = H_l + W_l (S[src] - act(H_l)[rev]) + b_l         chemprop.py:40-41, residual.py:28
+      nt_segment_reduce S = scatter(act(H_{l+1}), dst)        (skipped after the last layer)
+    nt_segment_reduce   node = scatter(H_d, dst)                                      chemprop.py:86
+
+plus one ``nt_dmpnn_pack_weight`` per distinct layer weight.  2 + 2d launches in all.
+
+Backward (training) is, for this round, a recompute of the same math in PyTorch device ops
+followed by autograd (``_torch_block``) — correct for every option, not yet a kernel (SURVEY §8(f)
+row 1).  The forward of a training step still runs the HIP kernels.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import torch
+from torch import Tensor
+
+from notorch_amd import kernels as K
+from notorch_amd._lib import NT_ACT_IDENTITY
+from notorch_amd.data.models.graph import DeviceLayout
+
+_IDENTITY = (NT_ACT_IDENTITY, 0.0)
+
+# Optional per-launch timer for the dominant kernel (bench.py sets it): a list that receives
+# (start, end) torch.cuda.Event pairs recorded on the launch stream around every nt_dmpnn_update.
+UPDATE_EVENTS: Optional[list] = None
+
+
+# ------------------------------------------------------------------------------------ layouts
+def _validate_indices(edge_index: Tensor, rev_index: Tensor, V: int) -> None:
+    E = edge_index.shape[-1]
+    if rev_index.numel() != E:
+        raise RuntimeError(f"rev_index has {rev_index.numel()} entries for {E} edges")
+    if E == 0:
+        return
+    mm = torch.stack(
+        [edge_index.min(), edge_index.max(), rev_index.min(), rev_index.max()]
+    ).cpu()  # one sync per new graph (the collate path validates on the host instead)
+    if mm[0] < 0 or mm[1] >= V:
+        raise IndexError(f"edge_index out of range for {V} nodes")
+    if mm[2] < 0 or mm[3] >= E:
+        raise IndexError(f"rev_index out of range for {E} edges")
+
+
+def dst_layout(G) -> DeviceLayout:
+    """The in-edge CSR of ``G`` on its device: cached from the collate, else built with nt_csr_build."""
+    ei = G.edge_index
+    lay: Optional[DeviceLayout] = getattr(G, "_nt_layout", None)
+    if (
+        lay is not None
+        and lay.dst_ptr is not None
+        and lay.validated
+        and lay.edge_index is ei
+        and lay.dst_ptr.device == ei.device
+    ):
+        return lay
+    V = G.node_feats.shape[0]
+    _validate_indices(ei, G.rev_index, V)
+    dst = ei[1].contiguous()
+    dst_ptr, dst_perm = K.csr_build(dst, V, check_bounds=False)
+    new = DeviceLayout(dst_ptr, dst_perm, edge_index=ei, validated=True)
+    if lay is not None and lay.mol_ptr is not None and lay.mol_ptr.device == ei.device:
+        new.mol_ptr, new.mol_perm, new.batch_node_index = lay.mol_ptr, lay.mol_perm, lay.batch_node_index
+    try:
+        G._nt_layout = new
+    except AttributeError:  # a foreign graph object that refuses new attributes: no caching
+        pass
+    return new
+
+
+def mol_layout(G) -> tuple[Tensor, Optional[Tensor]]:
+    """(mol_ptr, mol_perm) of a BatchedGraph: nodes of every molecule, for the readouts."""
+    bni = G.batch_node_index
+    B = len(G)
+    lay: Optional[DeviceLayout] = getattr(G, "_nt_layout", None)
+    if (
+        lay is not None
+        and lay.mol_ptr is not None
+        and lay.batch_node_index is bni
+        and lay.mol_ptr.device == bni.device
+        and lay.mol_ptr.numel() == B + 1
+    ):
+        return lay.mol_ptr, lay.mol_perm
+    mol_ptr, mol_perm = K.csr_build(bni.contiguous(), B, check_bounds=True)
+    if lay is None:
+        lay = DeviceLayout()
+    lay.mol_ptr, lay.mol_perm, lay.batch_node_index = mol_ptr, mol_perm, bni
+    try:
+        G._nt_layout = lay
+    except AttributeError:
+        pass
+    return mol_ptr, mol_perm
+
+
+# ------------------------------------------------------------------------------------ forward
+def pack_layer_weights(weights: Sequence[Tensor]) -> list[Tensor]:
+    """One packed MFMA image per layer; shared layers (same tensor) are packed once."""
+    cache: dict[int, Tensor] = {}
+    out = []
+    for W in weights:
+        key = id(W)
+        if key not in cache:
+            cache[key] = K.pack_weights(W.detach())
+        out.append(cache[key])
+    return out
+
+
+def block_forward(
+    Xv: Tensor,
+    Xe: Tensor,
+    src: Tensor,
+    rev: Tensor,
+    lay: DeviceLayout,
+    weights: Sequence[Tensor],
+    biases: Sequence[Optional[Tensor]],
+    act: tuple[int, float],
+    reduce: str,
+    residual: bool,
+    keep_states: bool = False,
+) -> tuple[Tensor, Tensor, list[Tensor]]:
+    """Run the fused kernel sequence; returns (node, H_d, [H_0..H_d] if keep_states)."""
+    V = Xv.shape[0]
+    d = len(weights)
+    if d == 0:
+        H, _ = K.dmpnn_init(Xv, Xe, src)
+        node = K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=_IDENTITY)
+        return node, H, [H]
+    Wps = pack_layer_weights(weights)
+    H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
+    states = [H]
+    spare: Optional[Tensor] = None  # ping-pong buffer when states are not kept
+    timer = UPDATE_EVENTS
+    for l in range(d):
+        if timer is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        Hn = K.dmpnn_update(
+            H, S, src, rev, Wps[l], None if biases[l] is None else biases[l].detach(),
+            residual=residual, act=act, out=spare,
+        )
+        if timer is not None:
+            ev[1].record()
+            timer.append(ev)
+        if l < d - 1:
+            K.segment_reduce(Hn, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=act, out=S)
+        if keep_states:
+            states.append(Hn)
+        else:
+            spare = H  # H_l is dead once H_{l+1} exists: reuse its buffer for H_{l+2}
+        H = Hn
+    node = K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=_IDENTITY)
+    return node, H, states
+
+
+# ------------------------------------------------------------------------------------ autograd
+def _torch_scatter(x: Tensor, index: Tensor, dim_size: int, reduce: str) -> Tensor:
+    """torch_scatter.scatter semantics (empty segment -> 0) in device ops, for the backward."""
+    out = torch.zeros(dim_size, x.shape[1], dtype=x.dtype, device=x.device)
+    idx = index.view(-1, 1).expand_as(x)
+    if reduce == "sum":
+        return out.scatter_add(0, idx, x)
+    red = {"mean": "mean", "max": "amax", "min": "amin"}[reduce]
+    return out.scatter_reduce(0, idx, x, reduce=red, include_self=False)
+
+
+def _torch_block(Xv, Xe, edge_index, rev, weights, biases, act_mod, reduce, residual):
+    src, dst = edge_index[0], edge_index[1]
+    V = Xv.shape[0]
+    H = Xv[src] + Xe
+    for W, b in zip(weights, biases):
+        M = act_mod(H)
+        S = _torch_scatter(M, dst, V, reduce)
+        U = torch.nn.functional.linear(S[src] - M[rev], W, b)
+        H = H + U if residual else U
+    return _torch_scatter(H, dst, V, reduce), H
+
+
+class ChempropBlockFunction(torch.autograd.Function):
+    """Kernel forward, recompute-in-torch backward (interim; see module docstring)."""
+
+    @staticmethod
+    def forward(ctx, Xv, Xe, edge_index, rev, lay, act_mod, act, reduce, residual, nlayers, *params):
+        weights = list(params[:nlayers])
+        biases = list(params[nlayers:])
+        src = edge_index[0].contiguous()
+        node, H, _ = block_forward(Xv, Xe, src, rev, lay, weights, biases, act, reduce, residual)
+        ctx.save_for_backward(Xv, Xe, edge_index, rev, *[p if p is not None else torch.empty(0) for p in params])
+        ctx.cfg = (act_mod, reduce, residual, nlayers, [p is None for p in params])
+        return node, H
+
+    @staticmethod
+    def backward(ctx, dnode, dH):
+        act_mod, reduce, residual, nlayers, is_none = ctx.cfg
+        Xv, Xe, edge_index, rev, *params = ctx.saved_tensors
+        params = [None if n else p for p, n in zip(params, is_none)]
+        need = ctx.needs_input_grad
+        with torch.enable_grad():
+            leaves = []
+            Xv_ = Xv.detach().requires_grad_(need[0])
+            Xe_ = Xe.detach().requires_grad_(need[1])
+            ps = [None if p is None else p.detach().requires_grad_(True) for p in params]
+            node, H = _torch_block(Xv_, Xe_, edge_index, rev, ps[:nlayers], ps[nlayers:], act_mod, reduce, residual)
+            leaves = [t for t in [Xv_, Xe_] + ps if t is not None and t.requires_grad]
+            outs, grads = [], []
+            for o, g in ((node, dnode), (H, dH)):
+                if g is not None:
+                    outs.append(o)
+                    grads.append(g)
+            got = torch.autograd.grad(outs, leaves, grads, allow_unused=True)
+        it = iter(got)
+        res_inputs = [next(it) if need[0] else None, next(it) if need[1] else None]
+        res_params = [None if p is None else next(it) for p in ps]
+        return (*res_inputs, None, None, None, None, None, None, None, None, *res_params)
+
+
+def segment_reduce_readout(X: Tensor, mol_ptr: Tensor, mol_perm: Optional[Tensor], B: int, reduce: str,
+                           batch_node_index: Tensor) -> Tensor:
+    if torch.is_grad_enabled() and X.requires_grad:
+        return ReadoutFunction.apply(X, mol_ptr, mol_perm, B, reduce, batch_node_index)
+    return K.segment_reduce(X, mol_ptr, mol_perm, B, reduce=reduce, act=_IDENTITY)
+
+
+class ReadoutFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, X, mol_ptr, mol_perm, B, reduce, batch_node_index):
+        ctx.save_for_backward(X, batch_node_index)
+        ctx.cfg = (B, reduce)
+        return K.segment_reduce(X, mol_ptr, mol_perm, B, reduce=reduce, act=_IDENTITY)
+
+    @staticmethod
+    def backward(ctx, dout):
+        X, bni = ctx.saved_tensors
+        B, reduce = ctx.cfg
+        with torch.enable_grad():
+            X_ = X.detach().requires_grad_(True)
+            out = _torch_scatter(X_, bni, B, reduce)
+            (dX,) = torch.autograd.grad(out, X_, dout)
+        return dX, None, None, None, None, None

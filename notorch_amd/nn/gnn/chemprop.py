@@ -1,0 +1,182 @@
+"""``ChempropLayer`` / ``ChempropBlock`` — drop-in replacements for
+``notorch/nn/gnn/chemprop.py:13-88`` whose forward runs on the notorch_amd HIP kernels.
+
+Same constructor signatures, attribute names, module tree and therefore ``state_dict`` keys
+(``layers.{i}.module.update.0.{weight,bias}`` with ``residual=True``, ``layers.{i}.update.0.*``
+without; one shared layer object repeated when ``shared=True``, chemprop.py:65-73), same
+``forward(G) -> G.update(node_feats=..., edge_feats=...)`` contract (chemprop.py:81-88).
+
+Differences by design:
+
+* the forward runs only on ROCm device tensors; a CPU graph raises ``RuntimeError`` (there is no
+  CPU fallback — the CPU restatement lives in ``oracle/`` and is test-only);
+* ``dropout > 0`` in training mode raises ``NotImplementedError`` (eval mode, or dropout 0, is the
+  reference's inference path and is fully supported);
+* ``act`` must be one of ReLU, Identity, LeakyReLU, ELU, GELU, SiLU, Tanh, Sigmoid.
+"""
+from __future__ import annotations
+
+from collections import OrderedDict
+
+import torch
+import torch.nn as nn
+from torch import Tensor
+
+from notorch_amd import kernels as K
+from notorch_amd._lib import NT_ACT_IDENTITY
+from notorch_amd.nn.gnn import _engine
+from notorch_amd.nn.residual import Residual
+
+Reduction = str  # Literal["mean", "sum", "min", "max"]  (notorch/types.py:57)
+_REDUCTIONS = ("mean", "sum", "min", "max")
+
+
+def _check_reduce(reduce: str) -> str:
+    if reduce not in _REDUCTIONS:
+        raise ValueError(f"reduce must be one of {_REDUCTIONS}, got {reduce!r}")
+    return reduce
+
+
+def _check_dropout(module: "ChempropLayer") -> None:
+    p = module.update[1].p
+    if module.training and p > 0 and torch.is_grad_enabled():
+        raise NotImplementedError(
+            "ChempropLayer dropout > 0 in training mode is not implemented on the HIP path yet"
+        )
+
+
+class ChempropLayer(nn.Module):
+    """One bond-message update (chemprop.py:13-46)."""
+
+    def __init__(
+        self,
+        hidden_dim: int,
+        act: type[nn.Module] = nn.ReLU,
+        bias: bool = True,
+        dropout: float = 0.0,
+        reduce: Reduction = "sum",
+    ):
+        super().__init__()
+        self.act = act()
+        self.reduce = _check_reduce(reduce)
+        self.update = nn.Sequential(nn.Linear(hidden_dim, hidden_dim, bias), nn.Dropout(dropout))
+        self._csr_cache: "OrderedDict[int, tuple]" = OrderedDict()
+
+    @property
+    def linear(self) -> nn.Linear:
+        return self.update[0]
+
+    def _csr(self, edge_index: Tensor, rev_index: Tensor, V: int):
+        key = id(edge_index)
+        hit = self._csr_cache.get(key)
+        if hit is not None and hit[0] is edge_index and hit[1] == V:
+            return hit[2], hit[3]
+        _engine._validate_indices(edge_index, rev_index, V)
+        seg_ptr, perm = K.csr_build(edge_index[1].contiguous(), V, check_bounds=False)
+        self._csr_cache[key] = (edge_index, V, seg_ptr, perm)
+        while len(self._csr_cache) > 4:
+            self._csr_cache.popitem(last=False)
+        return seg_ptr, perm
+
+    def forward(self, edge_feats: Tensor, node_feats: Tensor, edge_index: Tensor, rev_index: Tensor) -> Tensor:
+        """U = Dropout(Linear(S[src] - act(H)[rev])), S = scatter(act(H), dst) — no residual here."""
+        _check_dropout(self)
+        V = len(node_feats)
+        act = K.act_code(self.act)
+        if torch.is_grad_enabled() and (edge_feats.requires_grad or self.linear.weight.requires_grad):
+            # training through a standalone layer: route through the block function with depth 1
+            # and no residual, then subtract nothing (the block function returns H_1 = U).
+            lay = _engine.DeviceLayout(*self._csr(edge_index, rev_index, V), edge_index=edge_index, validated=True)
+            Xv = torch.zeros(V, edge_feats.shape[1], device=edge_feats.device)
+            # H0 = Xv[src] + Xe = edge_feats exactly (adding +0.0)
+            _, H = _engine.ChempropBlockFunction.apply(
+                Xv, edge_feats, edge_index, rev_index.contiguous(), lay, self.act, act, self.reduce,
+                False, 1, self.linear.weight, self.linear.bias,
+            )
+            return H
+        seg_ptr, perm = self._csr(edge_index, rev_index, V)
+        H = edge_feats.contiguous()
+        S = K.segment_reduce(H, seg_ptr, perm, V, reduce=self.reduce, act=act)
+        Wp = K.pack_weights(self.linear.weight.detach())
+        b = None if self.linear.bias is None else self.linear.bias.detach()
+        return K.dmpnn_update(
+            H, S, edge_index[0].contiguous(), rev_index.contiguous(), Wp, b, residual=False, act=act
+        )
+
+    def extra_repr(self):
+        return f"(reduce): {self.reduce}"
+
+
+class ChempropBlock(nn.Module):
+    """``depth`` bond-message layers + final node scatter (chemprop.py:49-88)."""
+
+    def __init__(
+        self,
+        hidden_dim: int = 256,
+        act: type[nn.Module] = nn.ReLU,
+        bias: bool = True,
+        dropout: float = 0.0,
+        depth: int = 3,
+        residual: bool = True,
+        shared: bool = False,
+        reduce: Reduction = "sum",
+    ):
+        super().__init__()
+        if shared:
+            layers = [ChempropLayer(hidden_dim, act, bias, dropout, reduce)] * depth
+        else:
+            layers = [ChempropLayer(hidden_dim, act, bias, dropout, reduce) for _ in range(depth)]
+        if residual:
+            layers = [Residual(layer) for layer in layers]
+        self.layers = nn.ModuleList(layers)
+        self.hidden_dim = hidden_dim
+        self.reduce = _check_reduce(reduce)
+        self.residual = residual
+
+    @property
+    def depth(self) -> int:
+        return len(self.layers)
+
+    def _chemprop_layers(self) -> list[ChempropLayer]:
+        return [m.module if isinstance(m, Residual) else m for m in self.layers]
+
+    def forward(self, G):
+        Xv, Xe = G.node_feats, G.edge_feats
+        if Xv.device.type != "cuda":
+            raise RuntimeError(
+                "notorch_amd.ChempropBlock runs on ROCm devices only (no CPU fallback); "
+                f"got node_feats on '{Xv.device}'"
+            )
+        if Xv.dim() != 2 or Xe.dim() != 2 or Xv.shape[1] != Xe.shape[1]:
+            raise RuntimeError(
+                f"node_feats {tuple(Xv.shape)} and edge_feats {tuple(Xe.shape)} must share the "
+                "hidden dimension (chemprop.py:83)"
+            )
+        layers = self._chemprop_layers()
+        for layer in layers:
+            _check_dropout(layer)
+        acts = {K.act_code(layer.act) for layer in layers}
+        if len(acts) > 1:
+            raise NotImplementedError("layers with different activations are not supported")
+        act = acts.pop() if acts else (NT_ACT_IDENTITY, 0.0)
+        residual = bool(layers) and isinstance(self.layers[0], Residual)
+        lay = _engine.dst_layout(G)
+        Xv = Xv.contiguous()
+        Xe = Xe.contiguous()
+        rev = G.rev_index.contiguous()
+        weights = [layer.linear.weight for layer in layers]
+        biases = [layer.linear.bias for layer in layers]
+        needs_grad = torch.is_grad_enabled() and (
+            Xv.requires_grad or Xe.requires_grad or any(p.requires_grad for p in self.parameters())
+        )
+        if needs_grad:
+            node, H = _engine.ChempropBlockFunction.apply(
+                Xv, Xe, G.edge_index, rev, lay, layers[0].act if layers else nn.Identity(), act,
+                self.reduce, residual, len(layers), *weights, *biases,
+            )
+        else:
+            src = G.edge_index[0].contiguous()
+            node, H, _ = _engine.block_forward(
+                Xv, Xe, src, rev, lay, weights, biases, act, self.reduce, residual
+            )
+        return G.update(node_feats=node, edge_feats=H)

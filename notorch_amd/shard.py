@@ -1,0 +1,70 @@
+"""Molecule-sharded data parallelism: independent units, no data-path collective.
+
+Molecules share no edges, so a batch splits into contiguous molecule ranges that each GPU
+collates and runs on its own.  The only collectives are bench bookkeeping (a barrier and two
+scalar all-reduces for max-time / total-units), never on the forward path.
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+
+def edge_balanced_ranges(edges_per_mol: np.ndarray, world_size: int) -> list[tuple[int, int]]:
+    """Contiguous [start, stop) molecule ranges, cut where the edge prefix sum crosses
+    k * E_total / world_size (edge-balanced; matters for skewed polymer batches)."""
+    e = np.asarray(edges_per_mol, dtype=np.int64)
+    B = len(e)
+    if world_size < 1:
+        raise ValueError("world_size must be >= 1")
+    if B == 0:
+        return [(0, 0)] * world_size
+    csum = np.cumsum(e)
+    total = int(csum[-1])
+    cuts = [0]
+    for k in range(1, world_size):
+        target = k * total / world_size
+        c = int(np.searchsorted(csum, target, side="left")) + 1
+        c = min(max(c, cuts[-1]), B)
+        cuts.append(c)
+    cuts.append(B)
+    return [(cuts[i], cuts[i + 1]) for i in range(world_size)]
+
+
+@dataclass
+class DistEnv:
+    rank: int
+    world_size: int
+    local_rank: int
+
+    @property
+    def distributed(self) -> bool:
+        return self.world_size > 1
+
+
+def dist_env() -> DistEnv:
+    return DistEnv(
+        int(os.environ.get("RANK", 0)),
+        int(os.environ.get("WORLD_SIZE", 1)),
+        int(os.environ.get("LOCAL_RANK", 0)),
+    )
+
+
+def aggregate_throughput(local_units: float, local_seconds: float, device=None) -> tuple[float, float, float]:
+    """(total_units, max_seconds, aggregate_rate) over all ranks; identity when not distributed.
+
+    Uses two scalar all-reduces (SUM of units, MAX of time) on the default process group.
+    """
+    import torch
+    import torch.distributed as dist
+
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return local_units, local_seconds, local_units / local_seconds
+    t = torch.tensor([local_units], dtype=torch.float64, device=device)
+    s = torch.tensor([local_seconds], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    dist.all_reduce(s, op=dist.ReduceOp.MAX)
+    units, secs = float(t.item()), float(s.item())
+    return units, secs, units / secs

@@ -1,0 +1,409 @@
+"""GPU parity: the HIP kernels (through the C ABI) against the CPU oracle on identical inputs.
+
+Criterion: fp32 normalised max error max|gpu - ref| / max|ref| <= 1e-5; integer
+outputs (CSR) bit-exact; properties (batching invariance in fixed-rev mode, determinism) bit-exact.
+"""
+import numpy as np
+import pytest
+import torch
+import torch.nn as nn
+
+from helpers import FP32_NORM_TOL, assert_parity, chain3, diatomic, load_golden
+from oracle import dmpnn_ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _K():
+    from notorch_amd import kernels
+
+    return kernels
+
+
+def _graph_tensors(kind="qm9", n=32, seed=0, rev_offset="nodes"):
+    from notorch_amd.data.synth import make_batch
+
+    return make_batch(kind, n, seed=seed).collate(rev_offset)
+
+
+def _embed(G, h, seed=0):
+    torch.manual_seed(seed)
+    nt = nn.EmbeddingBag(42, h, mode="sum")
+    et = nn.EmbeddingBag(13, h, mode="sum")
+    with torch.no_grad():
+        return nt(G.node_feats), et(G.edge_feats)
+
+
+# ------------------------------------------------------------------ native library is what runs
+def test_native_library_loaded():
+    from notorch_amd import _lib
+
+    lib = _lib.load()
+    assert lib.nt_abi_version() == _lib.ABI_VERSION
+
+
+# ------------------------------------------------------------------ CSR (bit-exact)
+@pytest.mark.parametrize("n,nseg", [(0, 5), (1, 1), (1000, 37), (77840, 36408), (200_000, 3)])
+def test_csr_build_exact(n, nseg):
+    K = _K()
+    g = torch.Generator().manual_seed(n + nseg)
+    idx = torch.randint(0, max(nseg, 1), (n,), generator=g) if nseg else torch.zeros(0, dtype=torch.long)
+    seg_ptr, perm = K.csr_build(idx.to(DEV), nseg)
+    exp_perm = np.argsort(idx.numpy(), kind="stable")
+    exp_ptr = np.concatenate([[0], np.cumsum(np.bincount(idx.numpy(), minlength=nseg))])
+    assert np.array_equal(seg_ptr.cpu().numpy(), exp_ptr)
+    assert np.array_equal(perm.cpu().numpy(), exp_perm)
+
+
+def test_csr_build_out_of_range_raises():
+    K = _K()
+    idx = torch.tensor([0, 3, 1], device=DEV)
+    with pytest.raises(IndexError):
+        K.csr_build(idx, 3)
+
+
+# ------------------------------------------------------------------ segment reduce
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
+@pytest.mark.parametrize("h", [300, 13])
+@pytest.mark.parametrize("act", [nn.Identity(), nn.ReLU(), nn.GELU(), nn.LeakyReLU(0.1)])
+def test_segment_reduce(reduce, h, act):
+    K = _K()
+    G = _graph_tensors("qm9", 64, seed=1)
+    E, V = G.edge_index.shape[1], G.num_nodes
+    X = torch.randn(E, h)
+    dst = G.edge_index[1]
+    seg_ptr, perm = K.csr_build(dst.to(DEV), V)
+    out = K.segment_reduce(X.to(DEV), seg_ptr, perm, V, reduce=reduce, act=K.act_code(act))
+    ref = dmpnn_ref.scatter(act(X), dst, V, reduce)
+    assert_parity(out, ref, 1e-6, f"segment_reduce {reduce}")
+    if reduce == "sum" and isinstance(act, nn.Identity):
+        # ascending-edge-order accumulation == CPU scatter_add_: bit-exact
+        assert torch.equal(out.cpu(), ref)
+
+
+def test_segment_reduce_empty_segments():
+    K = _K()
+    X = torch.randn(3, 8)
+    idx = torch.tensor([4, 4, 1])  # segments 0, 2, 3, 5 are empty
+    seg_ptr, perm = K.csr_build(idx.to(DEV), 6)
+    for red in ("sum", "mean", "max", "min"):
+        out = K.segment_reduce(X.to(DEV), seg_ptr, perm, 6, reduce=red)
+        assert torch.equal(out.cpu(), dmpnn_ref.scatter(X, idx, 6, red)), red
+
+
+# ------------------------------------------------------------------ fused layer update
+@pytest.mark.parametrize("h", [300, 256, 64, 100, 13, 2, 512])
+@pytest.mark.parametrize("residual", [True, False])
+def test_update_kernel(h, residual):
+    K = _K()
+    G = _graph_tensors("qm9", 48, seed=h)
+    E, V = G.edge_index.shape[1], G.num_nodes
+    g = torch.Generator().manual_seed(h)
+    H = torch.randn(E, h, generator=g)
+    S = torch.randn(V, h, generator=g)
+    lin = nn.Linear(h, h)
+    src, rev = G.edge_index[0], G.rev_index
+    out = K.dmpnn_update(
+        H.to(DEV), S.to(DEV), src.to(DEV), rev.to(DEV), K.pack_weights(lin.weight.detach().to(DEV)),
+        lin.bias.detach().to(DEV), residual=residual, act=K.act_code(nn.ReLU()),
+    )
+    with torch.no_grad():
+        A = S.double()[src] - torch.relu(H.double())[rev]
+        ref = nn.functional.linear(A, lin.weight.double(), lin.bias.double())
+        if residual:
+            ref = H.double() + ref
+    assert_parity(out, ref, FP32_NORM_TOL, f"update h={h}")
+
+
+def test_update_kernel_no_bias_and_acts():
+    K = _K()
+    G = _graph_tensors("qm9", 16, seed=3)
+    E, V, h = G.edge_index.shape[1], G.num_nodes, 64
+    H, S = torch.randn(E, h), torch.randn(V, h)
+    W = torch.randn(h, h) / 8
+    src, rev = G.edge_index[0], G.rev_index
+    for act in (nn.Identity(), nn.SiLU(), nn.Tanh(), nn.ELU(), nn.Sigmoid()):
+        out = K.dmpnn_update(
+            H.to(DEV), S.to(DEV), src.to(DEV), rev.to(DEV), K.pack_weights(W.to(DEV)), None,
+            residual=True, act=K.act_code(act),
+        )
+        ref = H + nn.functional.linear(S[src] - act(H)[rev], W)
+        assert_parity(out, ref, FP32_NORM_TOL, type(act).__name__)
+
+
+# ------------------------------------------------------------------ module-level parity
+def _module_forward(G, Xv, Xe, Ws, bs, **kw):
+    from notorch_amd.nn import ChempropBlock
+
+    h = Xv.shape[1]
+    blk = ChempropBlock(hidden_dim=h, depth=len(Ws), **kw).to(DEV).eval()
+    with torch.no_grad():
+        for m, W, b in zip(blk._chemprop_layers(), Ws, bs):
+            m.linear.weight.copy_(W)
+            if b is not None:
+                m.linear.bias.copy_(b)
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
+    with torch.no_grad():
+        return blk, Gd, blk(Gd)
+
+
+def test_kat_chain3_on_device():
+    from notorch_amd.data.models.graph import BatchedGraph
+
+    Xv, Xe, ei, rev, W, b, H1, node = chain3()
+    G = BatchedGraph(Xv, Xe, ei, rev, batch_node_index=torch.zeros(3, dtype=torch.long),
+                     batch_edge_index=torch.zeros(4, dtype=torch.long), size=1)
+    _, _, out = _module_forward(G, Xv, Xe, [W], [b])
+    assert torch.equal(out.edge_feats.cpu(), H1)
+    assert torch.equal(out.node_feats.cpu(), node)
+
+
+def test_kat_diatomic_on_device():
+    from notorch_amd.data.models.graph import Graph
+
+    Xv, Xe, ei, rev, Ws, bs = diatomic(h=300, depth=3)
+    G = Graph(Xv, Xe, ei, rev)
+    _, _, out = _module_forward(G, Xv, Xe, Ws, bs)
+    H = Xv[ei[0]] + Xe
+    for b in bs:
+        H = H + b
+    assert torch.equal(out.edge_feats.cpu(), H)
+    assert torch.equal(out.node_feats.cpu(), H[[1, 0]])
+
+
+@pytest.mark.parametrize("name", ["tiny.npz", "config1.npz"])
+def test_golden_fixture(name):
+    from notorch_amd.data.models.graph import BatchedGraph
+    from notorch_amd.nn import Sum
+
+    z = load_golden(name)
+    t = {k: torch.from_numpy(v) for k, v in z.items()}
+    G = BatchedGraph(t["node_feats"], t["edge_feats"], t["edge_index"], t["rev_index"],
+                     batch_node_index=t["batch_node_index"], batch_edge_index=t["batch_edge_index"],
+                     size=int(z["size"]))
+    _, Gd, out = _module_forward(G, t["node_feats"], t["edge_feats"], list(t["W"]), list(t["b"]))
+    assert_parity(out.edge_feats, t["out_edge"], what="edge_feats")
+    assert_parity(out.node_feats, t["out_node"], what="node_feats")
+    with torch.no_grad():
+        r = Sum()(out)
+    assert_parity(r, t["out_sum"], what="readout")
+    assert_parity(r, t["out_sum64"], what="readout vs fp64")
+
+
+@pytest.mark.parametrize(
+    "opts",
+    [
+        dict(),
+        dict(shared=True),
+        dict(residual=False),
+        dict(bias=False),
+        dict(reduce="mean"),
+        dict(reduce="max"),
+        dict(reduce="min"),
+        dict(act=nn.LeakyReLU),
+        dict(act=nn.GELU),
+    ],
+    ids=lambda o: ",".join(f"{k}={getattr(v, '__name__', v)}" for k, v in o.items()) or "default",
+)
+def test_block_options(opts):
+    G = _graph_tensors("qm9", 40, seed=7)
+    h, depth = 96, 3
+    Xv, Xe = _embed(G, h, seed=1)
+    from notorch_amd.nn import ChempropBlock
+
+    torch.manual_seed(5)
+    blk = ChempropBlock(hidden_dim=h, depth=depth, **opts).eval()
+    Ws, bs = dmpnn_ref.block_params(blk)
+    act = blk._chemprop_layers()[0].act
+    ref_n, ref_e = dmpnn_ref.chemprop_block(
+        Xv, Xe, G.edge_index, G.rev_index, Ws, bs, act=act, residual=opts.get("residual", True),
+        reduce=opts.get("reduce", "sum"),
+    )
+    blk = blk.to(DEV)
+    with torch.no_grad():
+        out = blk(G.update(node_feats=Xv, edge_feats=Xe).to(DEV))
+    assert_parity(out.edge_feats, ref_e, what="edge")
+    assert_parity(out.node_feats, ref_n, what="node")
+
+
+@pytest.mark.parametrize("depth", [0, 1, 5])
+def test_block_depths(depth):
+    G = _graph_tensors("zinc", 24, seed=depth)
+    Xv, Xe = _embed(G, 64)
+    torch.manual_seed(0)
+    Ws = [torch.randn(64, 64) / 8 for _ in range(depth)]
+    bs = [torch.randn(64) for _ in range(depth)]
+    ref_n, ref_e = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, Ws, bs)
+    _, _, out = _module_forward(G, Xv, Xe, Ws, bs)
+    assert_parity(out.edge_feats, ref_e, what="edge")
+    assert_parity(out.node_feats, ref_n, what="node")
+
+
+@pytest.mark.parametrize("reduce,cls", [("sum", "Sum"), ("mean", "Mean"), ("max", "Max"), ("min", "Min")])
+def test_readouts(reduce, cls):
+    import notorch_amd.nn as ntnn
+
+    G = _graph_tensors("qm9", 50, seed=11)
+    X = torch.randn(G.num_nodes, 300)
+    Gd = G.update(node_feats=X).to(DEV)
+    out = getattr(ntnn, cls)()(Gd)
+    ref = dmpnn_ref.readout(X, G.batch_node_index, len(G), reduce)
+    assert torch.equal(out.cpu(), ref) or reduce in ("mean",)
+    assert_parity(out, ref, 1e-6, cls)
+
+
+def test_readout_unsorted_batch_index():
+    from notorch_amd.data.models.graph import BatchedGraph
+    from notorch_amd.nn import Sum
+
+    G = _graph_tensors("qm9", 8, seed=2)
+    p = torch.randperm(G.num_nodes)
+    X = torch.randn(G.num_nodes, 32)
+    bni = G.batch_node_index[p]
+    BG = BatchedGraph(X, G.edge_feats, G.edge_index, G.rev_index, batch_node_index=bni,
+                      batch_edge_index=G.batch_edge_index, size=8).to(DEV)
+    out = Sum()(BG)
+    assert_parity(out, dmpnn_ref.readout(X, bni, 8, "sum"), 1e-6, "unsorted")
+
+
+# ------------------------------------------------------------------ full-size configs
+def test_config2_qm9_4096_parity():
+    """BASELINE config 2 shape: 4096 QM9-shaped molecules, h=300, depth=3, fp32, vs the oracle."""
+    G = _graph_tensors("qm9", 4096, seed=0)
+    h = 300
+    Xv, Xe = _embed(G, h, seed=0)
+    torch.manual_seed(1)
+    Ws = [nn.Linear(h, h).weight.detach() for _ in range(3)]
+    bs = [torch.randn(h) * 0.05 for _ in range(3)]
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    ref_n, ref_e = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, Ws, bs)
+    ref_r = dmpnn_ref.readout(ref_n, G.batch_node_index, len(G), "sum")
+    from notorch_amd.nn import Sum
+
+    _, _, out = _module_forward(G, Xv, Xe, Ws, bs)
+    with torch.no_grad():
+        r = Sum()(out)
+    assert_parity(out.edge_feats, ref_e, what="edge")
+    assert_parity(out.node_feats, ref_n, what="node")
+    assert_parity(r, ref_r, what="readout")
+
+
+def test_polymer_hubs_parity():
+    """Config 5 shape (reduced to 4 graphs): 1k-10k atoms, hub in-degree up to ~512."""
+    G = _graph_tensors("polymer", 4, seed=5, rev_offset="edges")
+    h = 128
+    Xv, Xe = _embed(G, h, seed=2)
+    torch.manual_seed(3)
+    Ws = [torch.randn(h, h) / 16 for _ in range(3)]
+    bs = [torch.randn(h) * 0.1 for _ in range(3)]
+    ref_n, ref_e = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, Ws, bs)
+    _, _, out = _module_forward(G, Xv, Xe, Ws, bs)
+    assert_parity(out.edge_feats, ref_e, what="edge")
+    assert_parity(out.node_feats, ref_n, what="node")
+
+
+def test_fixed_mode_batching_invariance_bitexact():
+    """Fixed-rev collate: forward(batch) == concat(forward(shard_i)) bit for bit, at full size."""
+    from notorch_amd.data.synth import make_batch
+
+    batch = make_batch("qm9", 4096, seed=9)
+    h = 300
+    torch.manual_seed(0)
+    Ws = [torch.randn(h, h) / 17 for _ in range(3)]
+    bs = [torch.randn(h) * 0.1 for _ in range(3)]
+    tabs = (nn.EmbeddingBag(42, h, mode="sum"), nn.EmbeddingBag(13, h, mode="sum"))
+
+    def run(b):
+        G = b.collate("edges")
+        with torch.no_grad():
+            Xv, Xe = tabs[0](G.node_feats), tabs[1](G.edge_feats)
+        return _module_forward(G, Xv, Xe, Ws, bs)[2]
+
+    whole = run(batch)
+    parts = [run(batch.subset(a, c)) for a, c in ((0, 1000), (1000, 2500), (2500, 4096))]
+    assert torch.equal(whole.edge_feats, torch.cat([p.edge_feats for p in parts]))
+    assert torch.equal(whole.node_feats, torch.cat([p.node_feats for p in parts]))
+
+
+def test_determinism_bitexact():
+    G = _graph_tensors("qm9", 512, seed=4)
+    Xv, Xe = _embed(G, 300)
+    torch.manual_seed(0)
+    Ws = [torch.randn(300, 300) / 17 for _ in range(3)]
+    bs = [torch.randn(300) for _ in range(3)]
+    blk, Gd, a = _module_forward(G, Xv, Xe, Ws, bs)
+    with torch.no_grad():
+        b = blk(Gd)
+    assert torch.equal(a.edge_feats, b.edge_feats) and torch.equal(a.node_feats, b.node_feats)
+
+
+# ------------------------------------------------------------------ contract / errors
+def test_forward_contract_and_device_layout_build():
+    """A hand-built graph without a collate layout gets its CSR on the device; input not mutated."""
+    from notorch_amd.data.models.graph import Graph
+
+    G0 = _graph_tensors("qm9", 8, seed=1)
+    Xv, Xe = _embed(G0, 32)
+    G = Graph(Xv, Xe, G0.edge_index, G0.rev_index, device_=DEV)
+    assert G._nt_layout is None
+    torch.manual_seed(0)
+    from notorch_amd.nn import ChempropBlock
+
+    blk = ChempropBlock(32, depth=2).to(DEV).eval()
+    with torch.no_grad():
+        out = blk(G)
+    assert out is not G and out.edge_index is G.edge_index and out.rev_index is G.rev_index
+    assert G.node_feats.shape == (G0.num_nodes, 32) and torch.equal(G.node_feats.cpu(), Xv)
+    Ws, bs = dmpnn_ref.block_params(blk)
+    ref_n, ref_e = dmpnn_ref.chemprop_block(Xv, Xe, G0.edge_index, G0.rev_index, Ws, bs)
+    assert_parity(out.node_feats, ref_n)
+
+
+def test_out_of_range_rev_raises_indexerror():
+    from notorch_amd.data.models.graph import Graph
+    from notorch_amd.nn import ChempropBlock
+
+    Xv, Xe, ei, rev, W, b, _, _ = chain3()
+    G = Graph(Xv, Xe, ei, torch.tensor([1, 0, 3, 9]), device_=DEV)
+    with pytest.raises(IndexError):
+        with torch.no_grad():
+            ChempropBlock(2, depth=1).to(DEV)(G)
+
+
+def test_training_forward_runs_kernels_and_grads_match():
+    """Autograd through the block: kernel forward, recompute backward; grads vs oracle autograd."""
+    from notorch_amd.nn import ChempropBlock, Sum
+
+    G = _graph_tensors("qm9", 16, seed=6)
+    h = 48
+    Xv, Xe = _embed(G, h)
+    torch.manual_seed(0)
+    blk = ChempropBlock(h, depth=2)
+    Ws = [l.linear.weight.detach().clone().requires_grad_(True) for l in blk._chemprop_layers()]
+    bs = [l.linear.bias.detach().clone().requires_grad_(True) for l in blk._chemprop_layers()]
+    Xv_r = Xv.clone().requires_grad_(True)
+    n, e = dmpnn_ref.chemprop_block(Xv_r, Xe, G.edge_index, G.rev_index, Ws, bs)
+    loss_r = dmpnn_ref.readout(n, G.batch_node_index, len(G)).pow(2).sum() + e.sum()
+    loss_r.backward()
+
+    blk = blk.to(DEV).train()
+    Xv_d = Xv.to(DEV).requires_grad_(True)
+    out = blk(G.update(node_feats=Xv_d, edge_feats=Xe).to(DEV))
+    loss = Sum()(out).pow(2).sum() + out.edge_feats.sum()
+    loss.backward()
+    assert_parity(loss.detach(), loss_r.detach(), what="loss")
+    assert_parity(Xv_d.grad, Xv_r.grad, 1e-4, "dXv")
+    for l, W in zip(blk._chemprop_layers(), Ws):
+        assert_parity(l.linear.weight.grad, W.grad, 1e-4, "dW")
+
+
+def test_cpu_graph_raises():
+    from notorch_amd.nn import ChempropBlock
+
+    Xv, Xe, ei, rev, *_ = chain3()
+    from notorch_amd.data.models.graph import Graph
+
+    with pytest.raises(RuntimeError, match="ROCm"):
+        ChempropBlock(2, depth=1)(Graph(Xv, Xe, ei, rev))
