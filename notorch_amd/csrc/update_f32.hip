@@ -22,7 +22,12 @@
 //
 // Roofline: 2*h^2 flop per edge (MFMA) against (3 rows read + 1 row written) * 4h bytes per edge;
 // at h = 300 that is 51 flop/B > the fp32 ridge (~20), i.e. bound by the 157 TF fp32 MFMA peak.
+#include <stdlib.h>
+
+#include <type_traits>
+
 #include "common.hpp"
+#include "update.hpp"
 
 namespace nt {
 
@@ -30,6 +35,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 256;
 constexpr int kWaves = 4;
+
+// kernel selection for A/B runs (read per call): NT_UPDATE_KERNEL = glds (default) | stream | tile
+static char update_kernel_choice() {
+  const char* v = getenv("NT_UPDATE_KERNEL");
+  return (v && v[0]) ? v[0] : 'g';
+}
 
 struct UpdateGeom {
   int KB;   // 16-deep k blocks (Kpad = 16*KB >= h)
@@ -240,6 +251,190 @@ __global__ void __launch_bounds__(kThreads, 2) dmpnn_update_f32(
   }
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Streamed variant (h % 4 == 0): the A tile is never materialised whole.  K advances in 16-deep
+// chunks through a 2-slot LDS ring (64 rows x 16 k, 6 KiB per slot); while the MFMAs consume
+// chunk k, the gathered S/H pieces of chunk k+1 wait in registers to be combined and written, and
+// the loads of chunk k+2 are in flight.  One workgroup barrier per chunk.  ~23 KiB of LDS and
+// <= 168 VGPRs give 3 workgroups per CU, so a CU interleaves several tiles' gathers and MFMAs.
+// Column tiles are dealt to waves as evenly as possible (ceil / floor), and a wave only issues
+// MFMAs for real tiles (no padding tiles).  Epilogue: per 16-row tile, each wave stages its
+// C fragments in a wave-private LDS slab and stores whole 16-B row pieces (+bias +residual).
+// ------------------------------------------------------------------------------------------
+#ifndef NT_STREAM_WAVES
+#define NT_STREAM_WAVES 2  // min waves per SIMD the streamed kernel is register-allocated for
+#endif
+constexpr int kBM2 = 64;   // edges per workgroup
+constexpr int kLDA2 = 24;  // ring row stride (floats): == 8 (mod 16) -> conflict-free b128 reads
+
+template <int CPW>
+struct Stream2Lds {
+  static constexpr int kRing = 2 * kBM2 * kLDA2;                 // floats
+  static constexpr int kLDE = 16 * CPW + 4;                      // == 4 (mod 8)
+  static constexpr int kEpi = kWaves * 16 * kLDE;                // floats
+  static constexpr int kFloats = (kRing > kEpi ? kRing : kEpi);
+};
+
+template <int NC, int CPW>
+__device__ __forceinline__ void mfma_chunk(f32x4 (&acc)[4][CPW], const float4 (&a)[4],
+                                           const float4* b) {
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+#pragma unroll
+    for (int mt = 0; mt < 4; ++mt) {
+      const float av = s == 0 ? a[mt].x : s == 1 ? a[mt].y : s == 2 ? a[mt].z : a[mt].w;
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct) {
+        const float bv = s == 0 ? b[ct].x : s == 1 ? b[ct].y : s == 2 ? b[ct].z : b[ct].w;
+        acc[mt][ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[mt][ct], 0, 0, 0);
+      }
+    }
+  }
+}
+
+template <int CPW, int ACT>
+__global__ void __launch_bounds__(kThreads, NT_STREAM_WAVES) dmpnn_update_f32_stream(
+    const float4* __restrict__ H4, const float4* __restrict__ S4, const int64_t* __restrict__ src,
+    const int64_t* __restrict__ rev, const float4* __restrict__ Wp, const float4* __restrict__ b4,
+    int64_t V, int64_t E, int hv, int KB, int NT, int residual, int act, float alpha,
+    float4* __restrict__ O4) {
+  using L = Stream2Lds<CPW>;
+  __shared__ __attribute__((aligned(16))) float smem[L::kFloats];
+  __shared__ int64_t s_src[kBM2], s_rev[kBM2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t e0 = (int64_t)blockIdx.x * kBM2;
+
+  if (tid < kBM2) {
+    const int64_t e = e0 + tid;
+    int64_t s = -1, q = -1;
+    if (e < E) {
+      s = src[e];
+      q = rev[e];
+      s = (s >= 0 && s < V) ? s * hv : -1;  // store float4 row offsets
+      q = (q >= 0 && q < E) ? q * hv : -1;
+    }
+    s_src[tid] = s;
+    s_rev[tid] = q;
+  }
+  // column tiles of this wave: ceil/floor split of NT over the 4 waves
+  const int base = NT >> 2, rem = NT & 3;
+  const int ncol = base + (wave < rem ? 1 : 0);
+  const int nt0 = wave * base + (wave < rem ? wave : rem);
+  __syncthreads();
+
+  // gather role of this lane: row gr, 16-B piece gc of the 64-B chunk row.  Loads are issued
+  // unconditionally from a clamped (always valid) address and masked afterwards, so the compiler
+  // emits plain global_load_dwordx4 with no exec-mask branches around them.
+  const int gr = tid >> 2, gc = tid & 3;
+  const int64_t gs_raw = s_src[gr], gq_raw = s_rev[gr];
+  const bool gs_ok = gs_raw >= 0, gq_ok = gq_raw >= 0;
+  const int64_t gs = gs_ok ? gs_raw : 0, gq = gq_ok ? gq_raw : 0;
+  const float4 zero4 = make_float4(0.f, 0.f, 0.f, 0.f);
+  // validity masks are applied when the chunk is consumed (put_chunk), never right after the
+  // load: a select on freshly loaded registers forces an early s_waitcnt and kills the prefetch.
+  auto load_chunk = [&](int kb, float4& sv, float4& hq) {
+    const int c = kb * 4 + gc;
+    const int cc = c < hv ? c : hv - 1;
+    sv = S4[gs + cc];
+    hq = H4[gq + cc];
+  };
+  auto put_chunk = [&](int kb, const float4& sv, const float4& hq) {
+    const bool in = kb * 4 + gc < hv;
+    float4 a = (in && gs_ok ? sv : zero4) - (in && gq_ok ? act4_t<ACT>(hq, act, alpha) : zero4);
+    *reinterpret_cast<float4*>(&smem[(kb & 1) * kBM2 * kLDA2 + gr * kLDA2 + 4 * gc]) = a;
+  };
+
+  f32x4 acc[4][CPW];
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt)
+#pragma unroll
+    for (int ct = 0; ct < CPW; ++ct) acc[mt][ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  float4 sv, hq;
+  load_chunk(0, sv, hq);
+  put_chunk(0, sv, hq);
+  if (KB > 1) load_chunk(1, sv, hq);
+  __syncthreads();
+
+  const float* a_base = smem + (lane & 15) * kLDA2 + 4 * (lane >> 4);
+  const float4* wp_lane = Wp + (int64_t)nt0 * 64 + lane;
+  // main loop, specialised on this wave's (wave-uniform) column-tile count NC
+  auto main_loop = [&](auto nc_tag) {
+    constexpr int NC = decltype(nc_tag)::value;
+    float4 b0[NC > 0 ? NC : 1], b1[NC > 0 ? NC : 1];
+    auto load_b = [&](int kb, float4(&b)[NC > 0 ? NC : 1]) {
+#pragma unroll
+      for (int ct = 0; ct < NC; ++ct) b[ct] = wp_lane[((int64_t)kb * NT + ct) * 64];
+    };
+    // one k-chunk: prefetch B(kb+1) into bn, MFMA on chunk kb with bc, restage the ring
+    auto step = [&](int kb, float4(&bc)[NC > 0 ? NC : 1], float4(&bn)[NC > 0 ? NC : 1]) {
+      if (kb + 1 < KB) load_b(kb + 1, bn);
+      const float* ab = a_base + (kb & 1) * kBM2 * kLDA2;
+      float4 a[4];
+#pragma unroll
+      for (int mt = 0; mt < 4; ++mt) a[mt] = *reinterpret_cast<const float4*>(ab + mt * 16 * kLDA2);
+      if constexpr (NC > 0) mfma_chunk<NC, CPW>(acc, a, bc);
+      if (kb + 1 < KB) {
+        put_chunk(kb + 1, sv, hq);
+        if (kb + 2 < KB) load_chunk(kb + 2, sv, hq);
+      }
+      __syncthreads();
+    };
+    load_b(0, b0);
+    int kb = 0;
+    for (; kb + 1 < KB; kb += 2) {  // unrolled by two: B registers ping-pong, no copies
+      step(kb, b0, b1);
+      step(kb + 1, b1, b0);
+    }
+    if (kb < KB) step(kb, b0, b1);
+  };
+  if (ncol == CPW) main_loop(std::integral_constant<int, CPW>{});
+  else main_loop(std::integral_constant<int, (CPW > 0 ? CPW - 1 : 0)>{});
+
+  // ---- epilogue: per 16-row tile, wave-private LDS slab -> 16-B row pieces ----
+  float* slab = smem + wave * 16 * L::kLDE;
+  const int nc4 = ncol * 4;  // float4 columns of this wave
+#pragma unroll
+  for (int mt = 0; mt < 4; ++mt) {
+#pragma unroll
+    for (int ct = 0; ct < CPW; ++ct) {
+      if (ct < ncol) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          slab[(4 * (lane >> 4) + j) * L::kLDE + 16 * ct + (lane & 15)] = acc[mt][ct][j];
+      }
+    }
+    __syncthreads();
+    for (int i = lane; i < 16 * nc4; i += 64) {
+      const int r = i / nc4, c = i - r * nc4;
+      const int64_t e = e0 + 16 * mt + r;
+      const int col4 = nt0 * 4 + c;
+      if (e < E && col4 < hv) {
+        float4 o = *reinterpret_cast<const float4*>(&slab[r * L::kLDE + 4 * c]);
+        if (b4) o = o + b4[col4];
+        if (residual) o = H4[e * hv + col4] + o;
+        O4[e * hv + col4] = o;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int CPW, int ACT>
+static int launch_stream(const float* H, const float* S, const int64_t* src, const int64_t* rev,
+                         const float4* Wp, const float* b, int64_t V, int64_t E, int h,
+                         const UpdateGeom& g, int residual, int act, float alpha, float* H_out,
+                         hipStream_t stream) {
+  const int64_t grid = (E + kBM2 - 1) / kBM2;
+  NT_REQUIRE(grid < (int64_t(1) << 31), NT_EINVAL, "too many edges");
+  dmpnn_update_f32_stream<CPW, ACT><<<(unsigned)grid, kThreads, 0, stream>>>(
+      (const float4*)H, (const float4*)S, src, rev, Wp, (const float4*)b, V, E, h / 4, g.KB, g.NT,
+      residual, act, alpha, (float4*)H_out);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
 template <int BM, int CPW, int ACT, bool VEC>
 static int launch_update(const float* H, const float* S, const int64_t* src, const int64_t* rev,
                          const float4* Wp, const float* b, int64_t V, int64_t E, int h,
@@ -264,6 +459,13 @@ static int dispatch_act_vec(const float* H, const float* S, const int64_t* src, 
                             const float4* Wp, const float* b, int64_t V, int64_t E, int h,
                             const UpdateGeom& g, int residual, int act, float alpha, float* H_out,
                             bool vec, hipStream_t stream) {
+  if (vec && update_kernel_choice() == 's') {
+    return act == NT_ACT_RELU
+               ? launch_stream<CPW, NT_ACT_RELU>(H, S, src, rev, Wp, b, V, E, h, g, residual, act,
+                                                 alpha, H_out, stream)
+               : launch_stream<CPW, -1>(H, S, src, rev, Wp, b, V, E, h, g, residual, act, alpha,
+                                        H_out, stream);
+  }
   if (act == NT_ACT_RELU) {
     return vec ? launch_update<BM, CPW, NT_ACT_RELU, true>(H, S, src, rev, Wp, b, V, E, h, g,
                                                            residual, act, alpha, H_out, stream)
@@ -336,6 +538,11 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
   const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(S) && aligned16(H_out) &&
                    (b == nullptr || aligned16(b));
   hipStream_t stream = as_stream(stream_);
+  if (vec && update_kernel_choice() == 'g') {
+    UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
+                 g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
+    return launch_update_glds(a);
+  }
   // 64-edge tiles while two workgroups still fit one CU's LDS (h <= 304), else 32-edge tiles.
   if (lds_bytes<64>(g) <= 80 * 1024)
     return dispatch_cpw<64>((const float*)H, (const float*)S, src, rev, (const float4*)Wp,

@@ -1,0 +1,82 @@
+"""Micro-benchmark of the individual kernels (device time via torch.cuda events, interleaved
+rounds in one process).  Usage: python tools/kbench.py [--mols 4096] [--h 300]"""
+import argparse
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from notorch_amd import kernels as K  # noqa: E402
+from notorch_amd.data.synth import make_batch  # noqa: E402
+
+
+def timeit(fn, reps=20):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    return statistics.median(ts), min(ts)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--mols", type=int, default=4096)
+    p.add_argument("--kind", default="qm9")
+    p.add_argument("--h", type=int, default=300)
+    a = p.parse_args()
+    G = make_batch(a.kind, a.mols, seed=0).collate("nodes").to("cuda")
+    V, E, h = G.num_nodes, G.num_edges, a.h
+    lay = G._nt_layout
+    H = torch.randn(E, h, device="cuda")
+    S = torch.randn(V, h, device="cuda")
+    Xv = torch.randn(V, h, device="cuda")
+    W = torch.randn(h, h, device="cuda") / 17
+    b = torch.randn(h, device="cuda")
+    Wp = K.pack_weights(W)
+    src, rev = G.edge_index[0].contiguous(), G.rev_index
+    out = torch.empty_like(H)
+    relu = K.act_code(torch.nn.ReLU())
+    def upd(variant):
+        def f():
+            os.environ["NT_UPDATE_KERNEL"] = variant
+            K.dmpnn_update(H, S, src, rev, Wp, b, act=relu, out=out)
+        return f
+
+    fns = {
+        "update": upd("glds"),
+        "update_stream": upd("stream"),
+        "update_tile": upd("tile"),
+        "aggregate": lambda: K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, act=relu, out=S),
+        "init_fused": lambda: K.dmpnn_init(Xv, H, src, lay.dst_ptr, lay.dst_perm, act=relu),
+        "node_scatter": lambda: K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V),
+        "pack": lambda: K.pack_weights(W),
+    }
+    for f in fns.values():
+        f()
+    torch.cuda.synchronize()
+    print(f"V={V} E={E} h={h}")
+    res = {n: [] for n in fns}
+    for _ in range(5):  # interleaved rounds
+        for name, f in fns.items():
+            res[name].append(timeit(f, 10))
+    for name, f in fns.items():
+        med = statistics.median(r[0] for r in res[name])
+        mn = min(r[1] for r in res[name])
+        extra = ""
+        if name.startswith("update"):
+            extra = f"  {2 * E * h * h / (med * 1e-6) / 1e12:.1f} TF/s"
+        else:
+            rows = {"aggregate": E + V, "init_fused": 3 * E + V, "node_scatter": E + V, "pack": 0}[name]
+            if rows:
+                extra = f"  {rows * h * 4 / (med * 1e-6) / 1e9:.0f} GB/s alg"
+        print(f"{name:14s} median {med:8.1f} us  min {mn:8.1f} us{extra}")
+
+
+if __name__ == "__main__":
+    main()
