@@ -26,4 +26,14 @@ struct UpdateArgs {
 // H, S, H_out, b.
 int launch_update_glds(const UpdateArgs& a);
 
+// bf16x6 fp32-emulation kernel (update_x6.hip): h % 4 == 0 and 97 <= h <= 512.
+bool x6_supported(int64_t h);
+size_t x6_image_bytes(int64_t h);
+int pack_weight_x6(const float* W, int64_t nlayers, int64_t h, int64_t layer_stride_bytes, void* Wx,
+                   hipStream_t stream);
+int launch_update_x6(const UpdateArgs& a);  // a.Wp points at the x6 image
+
+// Deeper-ring variant (S/H 2 chunks ahead); requires additionally NT <= 24.
+int launch_update_ring(const UpdateArgs& a);
+
 }  // namespace nt

@@ -36,10 +36,11 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int kThreads = 256;
 constexpr int kWaves = 4;
 
-// kernel selection for A/B runs (read per call): NT_UPDATE_KERNEL = glds (default) | stream | tile
+// kernel selection for A/B runs (read per call):
+//   NT_UPDATE_KERNEL = x6 (default: bf16x6 fp32 emulation) | glds | ring | stream | tile (fp32 MFMA)
 static char update_kernel_choice() {
   const char* v = getenv("NT_UPDATE_KERNEL");
-  return (v && v[0]) ? v[0] : 'g';
+  return (v && v[0]) ? v[0] : 'x';
 }
 
 struct UpdateGeom {
@@ -498,11 +499,20 @@ static int dispatch_cpw(const float* H, const float* S, const int64_t* src, cons
 
 }  // namespace nt
 
+// Packed image per layer: [fp32 fragment image (16x16x4 MFMA)][bf16x6 image (32x32x16 MFMA)],
+// each part 256-B aligned; the update kernel variant picks the part it consumes.
+static size_t f32_image_bytes(int64_t h) {
+  const nt::UpdateGeom g = nt::geom_for(h);
+  return ((size_t)g.KB * g.NT * 64 * sizeof(float4) + 255) & ~size_t(255);
+}
+static size_t x6_part_bytes(int64_t h) {
+  return nt::x6_supported(h) ? ((nt::x6_image_bytes(h) + 255) & ~size_t(255)) : 0;
+}
+
 extern "C" size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype) {
   (void)dtype;
   if (h <= 0) return 0;
-  const nt::UpdateGeom g = nt::geom_for(h);
-  return (size_t)g.KB * g.NT * 64 * sizeof(float4);
+  return f32_image_bytes(h) + x6_part_bytes(h);
 }
 
 extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, int dtype, void* Wp,
@@ -514,10 +524,22 @@ extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, i
   if (nlayers == 0) return NT_OK;
   NT_REQUIRE(W && Wp && aligned16(Wp), NT_EINVAL, "NULL or misaligned pointer");
   const UpdateGeom g = geom_for(h);
-  const int64_t total = nlayers * g.KB * g.NT * 64;
-  pack_weight_f32<<<grid_for(total, 256), 256, 0, as_stream(stream_)>>>(
-      (const float*)W, nlayers, h, g.KB, g.NT, (float4*)Wp);
-  NT_LAUNCH_CHECK();
+  const size_t per_layer = nt_dmpnn_packed_weight_bytes(h, dtype);
+  NT_REQUIRE(per_layer % 16 == 0, NT_EINVAL, "internal: packed layer size");
+  hipStream_t stream = as_stream(stream_);
+  // fp32 image of every layer (layer stride = per_layer bytes)
+  for (int64_t l = 0; l < nlayers; ++l) {
+    const int64_t total = (int64_t)g.KB * g.NT * 64;
+    pack_weight_f32<<<grid_for(total, 256), 256, 0, stream>>>(
+        (const float*)W + l * h * h, 1, h, g.KB, g.NT,
+        (float4*)((char*)Wp + l * per_layer));
+    NT_LAUNCH_CHECK();
+  }
+  if (x6_supported(h)) {
+    int rc = pack_weight_x6((const float*)W, nlayers, h, (int64_t)per_layer,
+                            (char*)Wp + f32_image_bytes(h), stream);
+    if (rc != NT_OK) return rc;
+  }
   return NT_OK;
 }
 
@@ -538,7 +560,19 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
   const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(S) && aligned16(H_out) &&
                    (b == nullptr || aligned16(b));
   hipStream_t stream = as_stream(stream_);
-  if (vec && update_kernel_choice() == 'g') {
+  const char choice = update_kernel_choice();
+  if (vec && choice == 'x' && x6_supported(h)) {
+    UpdateArgs a{(const float*)H, (const float*)S, src, rev, (const char*)Wp + f32_image_bytes(h),
+                 (const float*)b, V, E, h, g.KB, g.NT, residual, act, act_alpha, (float*)H_out,
+                 stream};
+    return launch_update_x6(a);
+  }
+  if (vec && choice == 'r' && g.NT <= 24) {
+    UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
+                 g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
+    return launch_update_ring(a);
+  }
+  if (vec && (choice == 'g' || choice == 'x')) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
     return launch_update_glds(a);

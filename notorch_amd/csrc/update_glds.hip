@@ -20,6 +20,8 @@
 #include "common.hpp"
 #include "update.hpp"
 
+#include <type_traits>
+
 namespace nt {
 
 namespace {
@@ -215,7 +217,219 @@ int dispatch_nt(const UpdateArgs& a, std::integer_sequence<int, NTs...>) {
   return rc;
 }
 
+
+// ------------------------------------------------------------------------------------------
+// Ring variant: S/H pieces 2 chunks ahead (3-slot ring), W tiles 1 chunk ahead (2-slot ring).
+// Every ring slot is its OWN __shared__ array and the K loop is unrolled over the ring period
+// (lcm(3,2) = 6 steps), so each step's slots are compile-time objects: hipcc then knows the
+// outstanding LDS-DMA targets other objects and puts no vmcnt wait in front of the reads.  The
+// step ends with a counted `s_waitcnt vmcnt(2)` (only this step's two S/H DMAs may stay in flight)
+// and a raw s_barrier (a __syncthreads() would drain the prefetch with vmcnt(0)).
+// ------------------------------------------------------------------------------------------
+constexpr int kRingEpiG = 3;  // epilogue column group: 2 waves x 16 x (16*3+4) floats fit 8 KiB
+
+template <int NT, int ACT>
+__global__ void __launch_bounds__(256, 2) update_ring_kernel(
+    const float4* __restrict__ H4, const float4* __restrict__ S4, const int64_t* __restrict__ src,
+    const int64_t* __restrict__ rev, const float4* __restrict__ Wp, const float4* __restrict__ b4,
+    int64_t V, int64_t E, int hv, int KB, int residual, int act, float alpha,
+    float4* __restrict__ O4) {
+  __shared__ __attribute__((aligned(16))) float sh0[2 * kRows * 16];  // S [64][16] | H [64][16]
+  __shared__ __attribute__((aligned(16))) float sh1[2 * kRows * 16];
+  __shared__ __attribute__((aligned(16))) float sh2[2 * kRows * 16];
+  __shared__ __attribute__((aligned(16))) float wb0[NT * 256];        // [NT][64 lanes][4]
+  __shared__ __attribute__((aligned(16))) float wb1[NT * 256];
+  __shared__ int64_t s_idx[2 * kRows];
+  int64_t* s_src = s_idx;
+  int64_t* s_rev = s_idx + kRows;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t e0 = (int64_t)blockIdx.x * kRows;
+
+  if (tid < kRows) {
+    const int64_t e = e0 + tid;
+    int64_t s = -1, q = -1;
+    if (e < E) {
+      s = src[e];
+      q = rev[e];
+      s = (s >= 0 && s < V) ? s * hv : -1;
+      q = (q >= 0 && q < E) ? q * hv : -1;
+    }
+    s_src[tid] = s;
+    s_rev[tid] = q;
+  }
+  __syncthreads();
+
+  const int lrow = 16 * wave + (lane >> 2), lpiece = lane & 3;
+  const int64_t ls = s_src[lrow], lq = s_rev[lrow];
+  const float4* s_row = S4 + (ls >= 0 ? ls : 0);
+  const float4* h_row = H4 + (lq >= 0 ? lq : 0);
+  const int frow = 16 * wave + (lane & 15), fg = lane >> 4;
+  const bool fs_ok = s_src[frow] >= 0, fq_ok = s_rev[frow] >= 0;
+
+  auto sh_slot = [&](auto tag) -> float* {
+    constexpr int k = decltype(tag)::value;
+    if constexpr (k == 0) return sh0;
+    else if constexpr (k == 1) return sh1;
+    else return sh2;
+  };
+  auto wb_slot = [&](auto tag) -> float* {
+    constexpr int k = decltype(tag)::value;
+    if constexpr (k == 0) return wb0;
+    else return wb1;
+  };
+  auto issue_sh = [&](int kb, float* slot) {
+    int c = 4 * kb + lpiece;
+    c = c < hv ? c : hv - 1;
+    glds16(s_row + c, slot + 16 * 16 * wave);
+    glds16(h_row + c, slot + kRows * 16 + 16 * 16 * wave);
+  };
+  auto issue_w = [&](int kb, float* slot) {
+    const float4* wk = Wp + (int64_t)kb * NT * 64 + lane;
+    for (int t = wave; t < NT; t += 4) glds16(wk + t * 64, slot + 256 * t);
+  };
+
+  f32x4 acc[NT];
+#pragma unroll
+  for (int ct = 0; ct < NT; ++ct) acc[ct] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // one K step reading S/H slot RS and W slot RW (compile-time), prefetching ahead
+  auto step = [&](int kb, auto rs_tag, auto rw_tag) {
+    constexpr int RS = decltype(rs_tag)::value, RW = decltype(rw_tag)::value;
+    const float* shs = sh_slot(std::integral_constant<int, RS>{});
+    const float* wbs = wb_slot(std::integral_constant<int, RW>{});
+    const float4 sv = *reinterpret_cast<const float4*>(shs + frow * 16 + 4 * fg);
+    const float4 hq = *reinterpret_cast<const float4*>(shs + kRows * 16 + frow * 16 + 4 * fg);
+    const float4* bl = reinterpret_cast<const float4*>(wbs) + lane;
+    float4 bf[NT];
+#pragma unroll
+    for (int ct = 0; ct < NT; ++ct) bf[ct] = bl[64 * ct];
+    // prefetch: W(kb+1) first, then S/H(kb+2), so a counted vmcnt(2) leaves only the latter
+    if (kb + 1 < KB) issue_w(kb + 1, wb_slot(std::integral_constant<int, (RW + 1) % 2>{}));
+    const bool sh_issued = kb + 2 < KB;
+    if (sh_issued) issue_sh(kb + 2, sh_slot(std::integral_constant<int, (RS + 2) % 3>{}));
+    const bool kin = 4 * kb + fg < hv;
+    const float4 mq = act4_t<ACT>(hq, act, alpha);
+    const bool use_s = kin && fs_ok, use_q = kin && fq_ok;
+    float4 a;
+    a.x = (use_s ? sv.x : 0.f) - (use_q ? mq.x : 0.f);
+    a.y = (use_s ? sv.y : 0.f) - (use_q ? mq.y : 0.f);
+    a.z = (use_s ? sv.z : 0.f) - (use_q ? mq.z : 0.f);
+    a.w = (use_s ? sv.w : 0.f) - (use_q ? mq.w : 0.f);
+#pragma unroll
+    for (int ct = 0; ct + 1 < NT; ct += 2) {
+      acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bf[ct].x, acc[ct], 0, 0, 0);
+      acc[ct + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bf[ct + 1].x, acc[ct + 1], 0, 0, 0);
+      acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bf[ct].y, acc[ct], 0, 0, 0);
+      acc[ct + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bf[ct + 1].y, acc[ct + 1], 0, 0, 0);
+      acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bf[ct].z, acc[ct], 0, 0, 0);
+      acc[ct + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bf[ct + 1].z, acc[ct + 1], 0, 0, 0);
+      acc[ct] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bf[ct].w, acc[ct], 0, 0, 0);
+      acc[ct + 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bf[ct + 1].w, acc[ct + 1], 0, 0, 0);
+    }
+    if constexpr (NT & 1) {
+      acc[NT - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, bf[NT - 1].x, acc[NT - 1], 0, 0, 0);
+      acc[NT - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, bf[NT - 1].y, acc[NT - 1], 0, 0, 0);
+      acc[NT - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, bf[NT - 1].z, acc[NT - 1], 0, 0, 0);
+      acc[NT - 1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, bf[NT - 1].w, acc[NT - 1], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (sh_issued) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  using I0 = std::integral_constant<int, 0>;
+  using I1 = std::integral_constant<int, 1>;
+  using I2 = std::integral_constant<int, 2>;
+  // prologue: W(0), S/H(0), S/H(1); wait all but S/H(1)
+  issue_w(0, wb0);
+  issue_sh(0, sh0);
+  if (KB > 1) {
+    issue_sh(1, sh1);
+    asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  int kb = 0;
+  for (; kb + 6 <= KB; kb += 6) {
+    step(kb, I0{}, I0{});
+    step(kb + 1, I1{}, I1{});
+    step(kb + 2, I2{}, I0{});
+    step(kb + 3, I0{}, I1{});
+    step(kb + 4, I1{}, I0{});
+    step(kb + 5, I2{}, I1{});
+  }
+  const int rem = KB - kb;  // 0..5, the period restarts at slots (0, 0)
+  if (rem > 0) step(kb, I0{}, I0{});
+  if (rem > 1) step(kb + 1, I1{}, I1{});
+  if (rem > 2) step(kb + 2, I2{}, I0{});
+  if (rem > 3) step(kb + 3, I0{}, I1{});
+  if (rem > 4) step(kb + 4, I1{}, I0{});
+
+  // ---- epilogue: groups of 3 column tiles, slabs in sh0 (waves 0,1) and sh1 (waves 2,3) ----
+  constexpr int kLDE = 16 * kRingEpiG + 4;
+  float* slab = (wave < 2 ? sh0 : sh1) + (wave & 1) * 16 * kLDE;
+  __syncthreads();
+#pragma unroll
+  for (int g0 = 0; g0 < NT; g0 += kRingEpiG) {
+#pragma unroll
+    for (int i = 0; i < kRingEpiG; ++i) {
+      const int ct = g0 + i;
+      if (ct < NT) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          slab[(4 * (lane >> 4) + j) * kLDE + 16 * i + (lane & 15)] = acc[ct][j];
+      }
+    }
+    __syncthreads();
+    const int ntiles = (NT - g0) < kRingEpiG ? (NT - g0) : kRingEpiG;
+    const int nc4 = ntiles * 4;
+    for (int i = lane; i < 16 * nc4; i += 64) {
+      const int r = i / nc4, c = i - r * nc4;
+      const int64_t e = e0 + 16 * wave + r;
+      const int col4 = 4 * g0 + c;
+      if (e < E && col4 < hv) {
+        float4 o = *reinterpret_cast<const float4*>(&slab[r * kLDE + 4 * c]);
+        if (b4) o = o + b4[col4];
+        if (residual) o = H4[e * hv + col4] + o;
+        O4[e * hv + col4] = o;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int NT, int ACT>
+int launch_ring(const UpdateArgs& a) {
+  const int64_t grid = (a.E + kRows - 1) / kRows;
+  NT_REQUIRE(grid < (int64_t(1) << 31), NT_EINVAL, "too many edges");
+  update_ring_kernel<NT, ACT><<<(unsigned)grid, 256, 0, a.stream>>>(
+      (const float4*)a.H, (const float4*)a.S, a.src, a.rev, (const float4*)a.Wp,
+      (const float4*)a.b, a.V, a.E, (int)(a.h / 4), a.KB, a.residual, a.act, a.alpha,
+      (float4*)a.H_out);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+template <int ACT, int... NTs>
+int dispatch_ring(const UpdateArgs& a, std::integer_sequence<int, NTs...>) {
+  int rc = NT_EUNSUPPORTED;
+  bool done = false;
+  ((a.NT == NTs + 1 ? (rc = launch_ring<NTs + 1, ACT>(a), done = true) : false), ...);
+  if (!done) set_error("nt_dmpnn_update: no ring kernel for this hidden size");
+  return rc;
+}
 }  // namespace
+
+int launch_update_ring(const UpdateArgs& a) {
+  using Seq = std::make_integer_sequence<int, 24>;  // NT <= 24: all W fragments held in VGPRs
+  if (a.act == NT_ACT_RELU) return dispatch_ring<NT_ACT_RELU>(a, Seq{});
+  return dispatch_ring<-1>(a, Seq{});
+}
 
 int launch_update_glds(const UpdateArgs& a) {
   using Seq = std::make_integer_sequence<int, 32>;

@@ -1,0 +1,287 @@
+// Fused D-MPNN layer update on bf16 MFMA with fp32 emulation ("bf16x6"):
+//
+//   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b     (chemprop.py:36-43,
+//                                                                               residual.py:27-28)
+// Numerics.  Every fp32 operand x is split exactly into three bf16 parts x = x0 + x1 + x2
+// (x0 = rne(x), x1 = rne(x - x0), x2 = rne(x - x0 - x1); 3 x 8 = 24 significant bits), and
+//   a.w ~= a0.w0 + a0.w1 + a1.w0 + a0.w2 + a1.w1 + a2.w0
+// is accumulated in fp32 by six v_mfma_f32_32x32x16_bf16.  Each bf16 x bf16 product is exact in
+// fp32; the dropped terms (a1.w2, a2.w1, a2.w2) are < 2^-24 relative, so the result carries fp32
+// GEMM accuracy (tests: <= 1e-5 normalised vs the fp32 oracle, typically ~3e-7 vs fp64) at
+// 6 x 16 = 96 MFMA cycles per 32x32x16 block instead of the 256 of fp32 MFMA (2.7x).
+//
+// Structure (one workgroup = 4 waves = 64 edges x all h output columns, K in 16-deep chunks):
+//   * 2-slot LDS rings, each slot its own __shared__ array (compile-time slot per step, loop
+//     unrolled by 2, so hipcc puts no vmcnt wait on reads of the current slot while the next
+//     slot's LDS-DMA is in flight):
+//       - S/H pieces: 64 rows x 64 B each (S[src[e]], H[rev[e]]), global_load_lds_dwordx4
+//       - W chunk:   NT32 x 3 parts x 1 KiB of the pre-split fragment image (L2-resident)
+//   * wave w computes the 32-row tile (w & 1) x column half (w >> 1): acc = 16 VGPR per 32x32
+//     tile.  The A fragment (8 k per lane) is formed as S - act(H), masked, split in registers.
+//   * epilogue: accumulators staged through LDS (reusing the W ring) in 2-tile column groups,
+//     then + bias + residual and 16-B row-piece stores.
+#include <type_traits>
+
+#include "common.hpp"
+#include "update.hpp"
+
+namespace nt {
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+constexpr int kRows = 64;
+
+// epilogue geometry: column tiles per group, slab row stride (== 4 mod 8), floats per wave slab;
+// two slabs must fit one W slot of NT32 x 3 KiB
+template <int NT32>
+struct X6Epi {
+  static constexpr int kG = NT32 >= 6 ? 2 : 1;
+  static constexpr int kLDE = 32 * kG + 4;
+  static constexpr int kSlab = 32 * kLDE;
+};
+
+__device__ __forceinline__ void glds16(const void* g, float* l) {
+  __builtin_amdgcn_global_load_lds((gbl_void*)g, (lds_void*)l, 16, 0, 0);
+}
+
+__device__ __forceinline__ void split3(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h0 = (__bf16)x[j];
+    const float r1 = x[j] - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    const float r2 = r1 - (float)h1;
+    p0[j] = h0;
+    p1[j] = h1;
+    p2[j] = (__bf16)r2;
+  }
+}
+
+template <int NT32, int ACT>
+__global__ void __launch_bounds__(256, 2) update_x6_kernel(
+    const float4* __restrict__ H4, const float4* __restrict__ S4, const int64_t* __restrict__ src,
+    const int64_t* __restrict__ rev, const uint4* __restrict__ Wx, const float4* __restrict__ b4,
+    int64_t V, int64_t E, int hv, int KB, int residual, int act, float alpha,
+    float4* __restrict__ O4) {
+  constexpr int kW = NT32 * 3 * 256;      // floats per W slot ([nt][part][lane] x 16 B)
+  constexpr int kEpiG = X6Epi<NT32>::kG, kLDE = X6Epi<NT32>::kLDE, kSlab = X6Epi<NT32>::kSlab;
+  static_assert(2 * kSlab <= kW, "epilogue slabs must fit a W slot (NT32 >= 4)");
+  __shared__ __attribute__((aligned(16))) float sh0[2 * kRows * 16];  // S [64][16] | H [64][16]
+  __shared__ __attribute__((aligned(16))) float sh1[2 * kRows * 16];
+  __shared__ __attribute__((aligned(16))) float wb0[kW];
+  __shared__ __attribute__((aligned(16))) float wb1[kW];
+  __shared__ int64_t s_idx[2 * kRows];
+  int64_t* s_src = s_idx;
+  int64_t* s_rev = s_idx + kRows;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int64_t e0 = (int64_t)blockIdx.x * kRows;
+
+  if (tid < kRows) {
+    const int64_t e = e0 + tid;
+    int64_t s = -1, q = -1;
+    if (e < E) {
+      s = src[e];
+      q = rev[e];
+      s = (s >= 0 && s < V) ? s * hv : -1;
+      q = (q >= 0 && q < E) ? q * hv : -1;
+    }
+    s_src[tid] = s;
+    s_rev[tid] = q;
+  }
+  __syncthreads();
+
+  // LDS-DMA role: piece (lane & 3) of tile row 16*wave + lane/4
+  const int lrow = 16 * wave + (lane >> 2), lpiece = lane & 3;
+  const int64_t ls = s_src[lrow], lq = s_rev[lrow];
+  const float4* s_row = S4 + (ls >= 0 ? ls : 0);
+  const float4* h_row = H4 + (lq >= 0 ? lq : 0);
+  auto issue = [&](int kb, float* shs, float* wbs) {
+    int c = 4 * kb + lpiece;
+    c = c < hv ? c : hv - 1;
+    glds16(s_row + c, shs + 16 * 16 * wave);
+    glds16(h_row + c, shs + kRows * 16 + 16 * 16 * wave);
+    const uint4* wk = Wx + (int64_t)kb * NT32 * 3 * 64 + lane;
+    for (int t = wave; t < NT32 * 3; t += 4) glds16(wk + t * 64, wbs + 256 * t);
+  };
+
+  // MFMA role: 32-row tile rt, column tiles [c0, c0 + ncol)
+  const int rt = wave & 1, ch = wave >> 1;
+  constexpr int CW = (NT32 + 1) / 2;
+  const int ncol = ch == 0 ? CW : NT32 - CW;
+  const int c0 = ch == 0 ? 0 : CW;
+  const int frow = 32 * rt + (lane & 31), fk = lane >> 5;  // fragment: k = 8 fk + j
+  const bool fs_ok = s_src[frow] >= 0, fq_ok = s_rev[frow] >= 0;
+
+  f32x16 acc[CW];
+#pragma unroll
+  for (int i = 0; i < CW; ++i)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+
+  auto body = [&](auto nc_tag) {
+    constexpr int NC = decltype(nc_tag)::value;
+    auto step = [&](int kb, const float* shs, const float* wbs, float* shn, float* wbn) {
+      if (kb + 1 < KB) issue(kb + 1, shn, wbn);
+      // A fragment: row frow, k = 16kb + 8fk + j  (two 16-B pieces of S and of H)
+      const float4* sp = reinterpret_cast<const float4*>(shs + frow * 16 + 8 * fk);
+      const float4* hp = reinterpret_cast<const float4*>(shs + kRows * 16 + frow * 16 + 8 * fk);
+      const float4 s0 = sp[0], s1 = sp[1], q0 = hp[0], q1 = hp[1];
+      const int col4 = 4 * kb + 2 * fk;
+      const bool k0 = col4 < hv, k1 = col4 + 1 < hv;
+      const float4 m0 = act4_t<ACT>(q0, act, alpha), m1 = act4_t<ACT>(q1, act, alpha);
+      const bool us0 = k0 && fs_ok, uq0 = k0 && fq_ok, us1 = k1 && fs_ok, uq1 = k1 && fq_ok;
+      float x[8];
+      x[0] = (us0 ? s0.x : 0.f) - (uq0 ? m0.x : 0.f);
+      x[1] = (us0 ? s0.y : 0.f) - (uq0 ? m0.y : 0.f);
+      x[2] = (us0 ? s0.z : 0.f) - (uq0 ? m0.z : 0.f);
+      x[3] = (us0 ? s0.w : 0.f) - (uq0 ? m0.w : 0.f);
+      x[4] = (us1 ? s1.x : 0.f) - (uq1 ? m1.x : 0.f);
+      x[5] = (us1 ? s1.y : 0.f) - (uq1 ? m1.y : 0.f);
+      x[6] = (us1 ? s1.z : 0.f) - (uq1 ? m1.z : 0.f);
+      x[7] = (us1 ? s1.w : 0.f) - (uq1 ? m1.w : 0.f);
+      bf16x8 a0, a1, a2;
+      split3(x, a0, a1, a2);
+      const bf16x8* wl = reinterpret_cast<const bf16x8*>(wbs) + lane;
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        const int t = c0 + i;
+        const bf16x8 w0 = wl[(3 * t + 0) * 64], w1 = wl[(3 * t + 1) * 64], w2 = wl[(3 * t + 2) * 64];
+        // smallest terms first
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, w0, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, w1, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w2, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, w0, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w1, acc[i], 0, 0, 0);
+        acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w0, acc[i], 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs above the barrier's vmcnt(0)
+      __syncthreads();                     // retires chunk kb+1's LDS-DMA; frees slot kb
+    };
+    int kb = 0;
+    for (; kb + 2 <= KB; kb += 2) {
+      step(kb, sh0, wb0, sh1, wb1);
+      step(kb + 1, sh1, wb1, sh0, wb0);
+    }
+    if (kb < KB) step(kb, sh0, wb0, sh1, wb1);
+  };
+
+  issue(0, sh0, wb0);
+  __syncthreads();
+  if (ncol == CW) body(std::integral_constant<int, CW>{});
+  else body(std::integral_constant<int, NT32 - CW>{});
+
+  // ---- epilogue: kEpiG-tile column groups through a wave-private slab (W ring is free now) ----
+  // C/D map of 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  float* slab = (wave < 2 ? wb0 : wb1) + (wave & 1) * kSlab;
+#pragma unroll
+  for (int g = 0; g < CW; g += kEpiG) {
+#pragma unroll
+    for (int i = 0; i < kEpiG; ++i) {
+      if (g + i < ncol) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          slab[((r & 3) + 8 * (r >> 2) + 4 * (lane >> 5)) * kLDE + 32 * i + (lane & 31)] = acc[g + i][r];
+      }
+    }
+    __syncthreads();
+    const int ntiles = (ncol - g) < kEpiG ? (ncol - g) : kEpiG;
+    const int nc4 = ntiles > 0 ? ntiles * 8 : 0;  // float4 columns in this group
+    for (int i = lane; i < 32 * nc4; i += 64) {
+      const int r = i / nc4, c = i - r * nc4;
+      const int64_t e = e0 + 32 * rt + r;
+      const int col4 = 8 * (c0 + g) + c;
+      if (e < E && col4 < hv) {
+        float4 o = *reinterpret_cast<const float4*>(&slab[r * kLDE + 4 * c]);
+        if (b4) o = o + b4[col4];
+        if (residual) o = H4[e * hv + col4] + o;
+        O4[e * hv + col4] = o;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Pre-split weight image: Wx[kb][nt][part][lane] = 8 bf16 (16 B), element j holding part `part`
+// of W[n][k] with n = 32 nt + (lane & 31), k = 16 kb + 8 (lane >> 5) + j (zero outside [0,h)).
+__global__ void __launch_bounds__(256) pack_x6(const float* __restrict__ W, int64_t nlayers,
+                                               int64_t h, int KB, int NT32, int64_t layer_stride16,
+                                               uint4* __restrict__ Wx) {
+  const int64_t per_layer = (int64_t)KB * NT32 * 64;  // (kb, nt, lane) triples
+  const int64_t total = nlayers * per_layer;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t l = t / per_layer;
+    int64_t r = t - l * per_layer;
+    const int lane = (int)(r & 63);
+    r >>= 6;
+    const int nt = (int)(r % NT32);
+    const int kb = (int)(r / NT32);
+    const int64_t n = 32 * nt + (lane & 31);
+    const int64_t k0 = 16 * kb + 8 * (lane >> 5);
+    const float* Wl = W + l * h * h;
+    float x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) x[j] = (n < h && k0 + j < h) ? Wl[n * h + k0 + j] : 0.f;
+    bf16x8 p[3];
+    split3(x, p[0], p[1], p[2]);
+    uint4* out = Wx + l * layer_stride16 + (((int64_t)kb * NT32 + nt) * 3) * 64 + lane;
+#pragma unroll
+    for (int part = 0; part < 3; ++part) out[part * 64] = *reinterpret_cast<const uint4*>(&p[part]);
+  }
+}
+
+template <int NT32, int ACT>
+int launch_x6(const UpdateArgs& a) {
+  const int64_t grid = (a.E + kRows - 1) / kRows;
+  NT_REQUIRE(grid < (int64_t(1) << 31), NT_EINVAL, "too many edges");
+  update_x6_kernel<NT32, ACT><<<(unsigned)grid, 256, 0, a.stream>>>(
+      (const float4*)a.H, (const float4*)a.S, a.src, a.rev, (const uint4*)a.Wp,
+      (const float4*)a.b, a.V, a.E, (int)(a.h / 4), (int)((a.h + 15) / 16), a.residual, a.act,
+      a.alpha, (float4*)a.H_out);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+template <int ACT, int... Ns>
+int dispatch_x6(const UpdateArgs& a, int nt32, std::integer_sequence<int, Ns...>) {
+  int rc = NT_EUNSUPPORTED;
+  bool done = false;
+  ((nt32 == Ns + 4 ? (rc = launch_x6<Ns + 4, ACT>(a), done = true) : false), ...);
+  if (!done) set_error("nt_dmpnn_update: no bf16x6 kernel for this hidden size");
+  return rc;
+}
+
+}  // namespace
+
+int x6_nt32(int64_t h) { return (int)((h + 31) / 32); }
+
+bool x6_supported(int64_t h) { return h % 4 == 0 && x6_nt32(h) >= 4 && x6_nt32(h) <= 16; }
+
+size_t x6_image_bytes(int64_t h) {
+  return (size_t)((h + 15) / 16) * x6_nt32(h) * 3 * 64 * 16;
+}
+
+int pack_weight_x6(const float* W, int64_t nlayers, int64_t h, int64_t layer_stride_bytes,
+                   void* Wx, hipStream_t stream) {
+  const int KB = (int)((h + 15) / 16), NT32 = x6_nt32(h);
+  const int64_t total = nlayers * KB * NT32 * 64;
+  pack_x6<<<grid_for(total, 256), 256, 0, stream>>>(W, nlayers, h, KB, NT32,
+                                                    layer_stride_bytes / 16, (uint4*)Wx);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+int launch_update_x6(const UpdateArgs& a) {
+  using Seq = std::make_integer_sequence<int, 13>;  // NT32 = 4 .. 16  (97 <= h <= 512)
+  const int nt32 = x6_nt32(a.h);
+  if (a.act == NT_ACT_RELU) return dispatch_x6<NT_ACT_RELU>(a, nt32, Seq{});
+  return dispatch_x6<-1>(a, nt32, Seq{});
+}
+
+}  // namespace nt

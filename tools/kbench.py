@@ -29,6 +29,8 @@ def main():
     p.add_argument("--mols", type=int, default=4096)
     p.add_argument("--kind", default="qm9")
     p.add_argument("--h", type=int, default=300)
+    p.add_argument("--only", default="", help="comma list of kernels to time")
+    p.add_argument("--rounds", type=int, default=5)
     a = p.parse_args()
     G = make_batch(a.kind, a.mols, seed=0).collate("nodes").to("cuda")
     V, E, h = G.num_nodes, G.num_edges, a.h
@@ -49,7 +51,9 @@ def main():
         return f
 
     fns = {
-        "update": upd("glds"),
+        "update": upd("x6"),
+        "update_glds": upd("glds"),
+        "update_ring": upd("ring"),
         "update_stream": upd("stream"),
         "update_tile": upd("tile"),
         "aggregate": lambda: K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, act=relu, out=S),
@@ -57,12 +61,15 @@ def main():
         "node_scatter": lambda: K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V),
         "pack": lambda: K.pack_weights(W),
     }
+    if a.only:
+        keep = a.only.split(",")
+        fns = {k: v for k, v in fns.items() if k in keep}
     for f in fns.values():
         f()
     torch.cuda.synchronize()
     print(f"V={V} E={E} h={h}")
     res = {n: [] for n in fns}
-    for _ in range(5):  # interleaved rounds
+    for _ in range(a.rounds):  # interleaved rounds
         for name, f in fns.items():
             res[name].append(timeit(f, 10))
     for name, f in fns.items():
