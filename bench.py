@@ -33,6 +33,7 @@ from notorch_amd.shard import aggregate_throughput, dist_env  # noqa: E402
 METRIC = "edge-messages/sec D-MPNN depth=3 h=300, QM9-shaped batches, 1/2/4/8 MI355X"
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
 PEAK_HBM_GBPS = 8000.0
+PEAK_BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
 
 WORKLOADS = {
     # name: (generator, molecules per GPU, hidden, depth)
@@ -51,7 +52,9 @@ def parse():
     p.add_argument("--workload", default="qm9-4096", choices=sorted(WORKLOADS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--pmc-csv", default=None, help="rocprofv3 --pmc counter CSV to fill roofline.traffic")
+    p.add_argument("--pmc-csv", default=None,
+                   help="comma-separated rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs of the "
+                   "same command (tools/profile.sh) to fill roofline.traffic")
     return p.parse_args()
 
 
@@ -108,25 +111,28 @@ def cpu_baseline(G, Xv, Xe, Ws, bs, depth, budget_s):
     }
 
 
-def read_pmc_traffic(path, kernel_substr="dmpnn_update"):
-    """Average HBM bytes per launch of the kernel from a rocprofv3 --pmc counter_collection CSV.
+def read_pmc_traffic(paths, kernel_substr="update"):
+    """Average HBM bytes per launch of the update kernel from rocprofv3 --pmc counter_collection
+    CSVs (comma-separated; FETCH_SIZE and WRITE_SIZE come from separate passes).
     gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE reads 1/2 of wide streaming reads
     -> x2; WRITE_SIZE is exact for 16-B stores.  Both are in KB."""
     import csv
 
     fetch, write, n_f, n_w = 0.0, 0.0, set(), set()
-    with open(path) as f:
-        for row in csv.DictReader(f):
-            if kernel_substr not in row.get("Kernel_Name", ""):
-                continue
-            name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
-            did = row.get("Dispatch_Id")
-            if name == "FETCH_SIZE":
-                fetch += val
-                n_f.add(did)
-            elif name == "WRITE_SIZE":
-                write += val
-                n_w.add(did)
+    for path in paths.split(","):
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                kn = row.get("Kernel_Name", "")
+                if kernel_substr not in kn or "pack" in kn:
+                    continue
+                name, val = row.get("Counter_Name"), float(row.get("Counter_Value", 0))
+                did = (path, row.get("Dispatch_Id"))
+                if name == "FETCH_SIZE":
+                    fetch += val
+                    n_f.add(did)
+                elif name == "WRITE_SIZE":
+                    write += val
+                    n_w.add(did)
     if not n_f and not n_w:
         return None
     per = 0.0
@@ -197,8 +203,34 @@ def main():
         return
 
     flops_upd = 2 * E * h * h
-    achieved = flops_upd / (upd_ms * 1e-3) / 1e12
+    upd_bytes = update_bytes(V, E, h)
+    variant = os.environ.get("NT_UPDATE_KERNEL", "x6")
+    x6 = variant.startswith("x") and h % 4 == 0 and 97 <= h <= 512
     traffic = read_pmc_traffic(args.pmc_csv) if args.pmc_csv else None
+    if x6:
+        # bf16x6 fp32 emulation: 6 bf16 MFMA products per fp32 product on 32x32x16 tiles
+        # (K padded to 16, N to 32).  Binding roof = max(HBM bytes / 8 TB/s, bf16 flops / 2.5 PF).
+        kp, np_ = 16 * ((h + 15) // 16), 32 * ((h + 31) // 32)
+        bf16_flops = 6 * 2 * E * kp * np_
+        t_hbm = upd_bytes / (PEAK_HBM_GBPS * 1e9)
+        t_mfma = bf16_flops / (PEAK_BF16_MFMA_TFLOPS * 1e12)
+        bound = "hbm" if t_hbm >= t_mfma else "mfma"
+        if bound == "hbm":
+            achieved, peak, unit = upd_bytes / (upd_ms * 1e-3) / 1e9, PEAK_HBM_GBPS, "GB/s"
+        else:
+            achieved, peak, unit = bf16_flops / (upd_ms * 1e-3) / 1e12, PEAK_BF16_MFMA_TFLOPS, "TFLOP/s"
+        kname = "nt_dmpnn_update (update_x6_kernel: bf16x6 fp32-emulating 32x32x16 MFMA + LDS-DMA gathers)"
+        extra = {
+            "mfma_bf16_tflops": bf16_flops / (upd_ms * 1e-3) / 1e12,
+            "mfma_bf16_frac": bf16_flops / (upd_ms * 1e-3) / 1e12 / PEAK_BF16_MFMA_TFLOPS,
+            "fp32_equiv_tflops": flops_upd / (upd_ms * 1e-3) / 1e12,
+            "t_min_us": max(t_hbm, t_mfma) * 1e6,
+        }
+    else:
+        bound = "mfma"
+        achieved, peak, unit = flops_upd / (upd_ms * 1e-3) / 1e12, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
+        kname = "nt_dmpnn_update (fp32 16x16x4 MFMA, variant %s)" % variant
+        extra = {"alg_hbm_gbps": upd_bytes / (upd_ms * 1e-3) / 1e9}
     fwd_bytes, fwd_flops = forward_bytes_flops(V, E, B, h, depth)
     t_step = secs / args.steps
     t_min = max(fwd_bytes / (PEAK_HBM_GBPS * 1e9), fwd_flops / (PEAK_FP32_MFMA_TFLOPS * 1e12))
@@ -214,6 +246,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
+        "mfma_numerics": "bf16x6 split (fp32-accurate)" if x6 else "fp32 MFMA",
         "data": "synthetic (seeded QM9-shaped molecules per rank, random-init EmbeddingBag + weights)",
         "config": {
             "workload": f"{args.workload}: {n_mols} {kind}-shaped molecules per GPU, D-MPNN depth={depth} "
@@ -226,18 +259,19 @@ def main():
             "parallelism": f"molecule-sharded x{env.world_size}, no collective on the forward path",
         },
         "roofline": {
-            "kernel": "nt_dmpnn_update (dmpnn_update_f32, fp32 MFMA 16x16x4)",
-            "bound": "mfma",
+            "kernel": kname,
+            "bound": bound,
             "achieved": achieved,
-            "peak": PEAK_FP32_MFMA_TFLOPS,
-            "unit": "TFLOP/s",
-            "frac": achieved / PEAK_FP32_MFMA_TFLOPS,
+            "peak": peak,
+            "unit": unit,
+            "frac": achieved / peak,
             "traffic": traffic,
             "launch_ms": upd_ms,
             "launches_timed": len(events),
-            "flops_per_launch": flops_upd,
-            "alg_bytes_per_launch": update_bytes(V, E, h),
-            "alg_hbm_gbps": update_bytes(V, E, h) / (upd_ms * 1e-3) / 1e9,
+            "alg_bytes_per_launch": upd_bytes,
+            "flops_per_launch_fp32": flops_upd,
+            "alg_hbm_gbps": upd_bytes / (upd_ms * 1e-3) / 1e9,
+            **extra,
         },
         "forward_roofline": {
             "alg_bytes": fwd_bytes,

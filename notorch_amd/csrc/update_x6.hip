@@ -20,6 +20,8 @@
 //     tile.  The A fragment (8 k per lane) is formed as S - act(H), masked, split in registers.
 //   * epilogue: accumulators staged through LDS (reusing the W ring) in 2-tile column groups,
 //     then + bias + residual and 16-B row-piece stores.
+#include <stdlib.h>
+
 #include <type_traits>
 
 #include "common.hpp"
@@ -34,15 +36,20 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void gbl_void;
 
-constexpr int kRows = 64;
-
-// epilogue geometry: column tiles per group, slab row stride (== 4 mod 8), floats per wave slab;
-// two slabs must fit one W slot of NT32 x 3 KiB
-template <int NT32>
-struct X6Epi {
-  static constexpr int kG = NT32 >= 6 ? 2 : 1;
+// Geometry: MW 32-row tiles per workgroup (2 column halves -> 2*MW waves), S/H gather ring of
+// SHR slots (SHR = 3: gathers run two K-chunks ahead), W ring of 2 slots.
+template <int NT32, int MW>
+struct X6Geom {
+  static constexpr int kWaves = 2 * MW;
+  static constexpr int kThreads = 64 * kWaves;
+  static constexpr int kRows = 32 * MW;
+  static constexpr int kSH = 2 * kRows * 16;           // floats per S/H slot: S [rows][16] | H
+  static constexpr int kW = NT32 * 3 * 256;            // floats per W slot ([nt][part][lane] 16 B)
+  // epilogue: column tiles per group kG, slab row stride (== 4 mod 8); kWaves/2 slabs per W slot
+  static constexpr int kG = ((kWaves / 2) * 32 * (32 * 2 + 4) <= kW) ? 2 : 1;
   static constexpr int kLDE = 32 * kG + 4;
   static constexpr int kSlab = 32 * kLDE;
+  static constexpr bool kFits = (kWaves / 2) * kSlab <= kW;
 };
 
 __device__ __forceinline__ void glds16(const void* g, float* l) {
@@ -62,19 +69,31 @@ __device__ __forceinline__ void split3(const float (&x)[8], bf16x8& p0, bf16x8& 
   }
 }
 
-template <int NT32, int ACT>
-__global__ void __launch_bounds__(256, 2) update_x6_kernel(
+// ABL (timing-only ablation builds, outputs wrong): 1 = no W DMA, 2 = no S/H DMA, 4 = no MFMA
+template <int NT32, int MW, int SHR, int WR, int ACT, int ABL = 0>
+__global__ void __launch_bounds__(128 * MW, 2) update_x6_kernel(
     const float4* __restrict__ H4, const float4* __restrict__ S4, const int64_t* __restrict__ src,
     const int64_t* __restrict__ rev, const uint4* __restrict__ Wx, const float4* __restrict__ b4,
     int64_t V, int64_t E, int hv, int KB, int residual, int act, float alpha,
     float4* __restrict__ O4) {
-  constexpr int kW = NT32 * 3 * 256;      // floats per W slot ([nt][part][lane] x 16 B)
-  constexpr int kEpiG = X6Epi<NT32>::kG, kLDE = X6Epi<NT32>::kLDE, kSlab = X6Epi<NT32>::kSlab;
-  static_assert(2 * kSlab <= kW, "epilogue slabs must fit a W slot (NT32 >= 4)");
-  __shared__ __attribute__((aligned(16))) float sh0[2 * kRows * 16];  // S [64][16] | H [64][16]
-  __shared__ __attribute__((aligned(16))) float sh1[2 * kRows * 16];
-  __shared__ __attribute__((aligned(16))) float wb0[kW];
-  __shared__ __attribute__((aligned(16))) float wb1[kW];
+  using G = X6Geom<NT32, MW>;
+  constexpr int kRows = G::kRows, kW = G::kW, kSH = G::kSH;
+  constexpr int kEpiG = G::kG, kLDE = G::kLDE, kSlab = G::kSlab;
+  static_assert(G::kFits, "epilogue slabs must fit the W ring");
+  static_assert(SHR == 2 || SHR == 3, "S/H ring depth");
+  static_assert(WR == 2 || (WR == 3 && SHR == 3), "W ring depth");
+  // W tiles per wave per step: every wave issues the same count (kWPW); padding loads re-read
+  // tile 0 into the spare tail of the slot, so a counted vmcnt is wave-uniform
+  constexpr int kWT = NT32 * 3;
+  constexpr int kWPW = (kWT + G::kWaves - 1) / G::kWaves;
+  // every ring slot is its own __shared__ object (see file header)
+  __shared__ __attribute__((aligned(16))) float sh0[kSH];
+  __shared__ __attribute__((aligned(16))) float sh1[kSH];
+  __shared__ __attribute__((aligned(16))) float sh2[SHR > 2 ? kSH : 4];
+  constexpr int kWS = WR == 3 ? kWPW * G::kWaves * 256 : kW;  // W slot incl. padding tiles
+  __shared__ __attribute__((aligned(16))) float wb0[kWS];
+  __shared__ __attribute__((aligned(16))) float wb1[kWS];
+  __shared__ __attribute__((aligned(16))) float wb2[WR > 2 ? kWS : 4];
   __shared__ int64_t s_idx[2 * kRows];
   int64_t* s_src = s_idx;
   int64_t* s_rev = s_idx + kRows;
@@ -96,22 +115,47 @@ __global__ void __launch_bounds__(256, 2) update_x6_kernel(
   }
   __syncthreads();
 
-  // LDS-DMA role: piece (lane & 3) of tile row 16*wave + lane/4
+  auto sh_slot = [&](auto tag) -> float* {
+    constexpr int k = decltype(tag)::value;
+    if constexpr (k == 0) return sh0;
+    else if constexpr (k == 1) return sh1;
+    else return sh2;
+  };
+  auto wb_slot = [&](auto tag) -> float* {
+    constexpr int k = decltype(tag)::value;
+    if constexpr (k == 0) return wb0;
+    else if constexpr (k == 1) return wb1;
+    else return wb2;
+  };
+
+  // LDS-DMA roles: S/H piece (lane & 3) of tile row 16*wave + lane/4; W tiles wave, wave+NW, ...
   const int lrow = 16 * wave + (lane >> 2), lpiece = lane & 3;
   const int64_t ls = s_src[lrow], lq = s_rev[lrow];
   const float4* s_row = S4 + (ls >= 0 ? ls : 0);
   const float4* h_row = H4 + (lq >= 0 ? lq : 0);
-  auto issue = [&](int kb, float* shs, float* wbs) {
+  auto issue_sh = [&](int kb, float* shs) {
+    if constexpr ((ABL & 2) != 0) return;
     int c = 4 * kb + lpiece;
     c = c < hv ? c : hv - 1;
     glds16(s_row + c, shs + 16 * 16 * wave);
     glds16(h_row + c, shs + kRows * 16 + 16 * 16 * wave);
+  };
+  auto issue_w = [&](int kb, float* wbs) {
+    if constexpr ((ABL & 1) != 0) return;
     const uint4* wk = Wx + (int64_t)kb * NT32 * 3 * 64 + lane;
-    for (int t = wave; t < NT32 * 3; t += 4) glds16(wk + t * 64, wbs + 256 * t);
+    if constexpr (WR == 3) {
+#pragma unroll
+      for (int i = 0; i < kWPW; ++i) {
+        const int t = wave + i * G::kWaves;
+        glds16(wk + (t < kWT ? t : 0) * 64, wbs + 256 * t);  // t >= kWT: padding slot tail
+      }
+    } else {
+      for (int t = wave; t < kWT; t += G::kWaves) glds16(wk + t * 64, wbs + 256 * t);
+    }
   };
 
   // MFMA role: 32-row tile rt, column tiles [c0, c0 + ncol)
-  const int rt = wave & 1, ch = wave >> 1;
+  const int rt = wave % MW, ch = wave / MW;
   constexpr int CW = (NT32 + 1) / 2;
   const int ncol = ch == 0 ? CW : NT32 - CW;
   const int c0 = ch == 0 ? 0 : CW;
@@ -126,8 +170,27 @@ __global__ void __launch_bounds__(256, 2) update_x6_kernel(
 
   auto body = [&](auto nc_tag) {
     constexpr int NC = decltype(nc_tag)::value;
-    auto step = [&](int kb, const float* shs, const float* wbs, float* shn, float* wbn) {
-      if (kb + 1 < KB) issue(kb + 1, shn, wbn);
+    auto step = [&](int kb, auto rs_tag, auto rw_tag) {
+      constexpr int RS = decltype(rs_tag)::value, RW = decltype(rw_tag)::value;
+      const float* shs = sh_slot(rs_tag);
+      const float* wbs = wb_slot(rw_tag);
+      // prefetch: W first, then S/H, so a counted vmcnt can leave the newest DMAs in flight
+      bool sh_ahead = false;
+      if constexpr (WR == 3) {
+        sh_ahead = kb + 2 < KB;
+        if (sh_ahead) {
+          issue_w(kb + 2, wb_slot(std::integral_constant<int, (RW + 2) % 3>{}));
+          issue_sh(kb + 2, sh_slot(std::integral_constant<int, (RS + 2) % 3>{}));
+        }
+      } else {
+        if (kb + 1 < KB) issue_w(kb + 1, wb_slot(std::integral_constant<int, (RW + 1) % 2>{}));
+        if constexpr (SHR == 3) {
+          sh_ahead = kb + 2 < KB;
+          if (sh_ahead) issue_sh(kb + 2, sh_slot(std::integral_constant<int, (RS + 2) % 3>{}));
+        } else {
+          if (kb + 1 < KB) issue_sh(kb + 1, sh_slot(std::integral_constant<int, (RS + 1) % 2>{}));
+        }
+      }
       // A fragment: row frow, k = 16kb + 8fk + j  (two 16-B pieces of S and of H)
       const float4* sp = reinterpret_cast<const float4*>(shs + frow * 16 + 8 * fk);
       const float4* hp = reinterpret_cast<const float4*>(shs + kRows * 16 + frow * 16 + 8 * fk);
@@ -152,6 +215,10 @@ __global__ void __launch_bounds__(256, 2) update_x6_kernel(
       for (int i = 0; i < NC; ++i) {
         const int t = c0 + i;
         const bf16x8 w0 = wl[(3 * t + 0) * 64], w1 = wl[(3 * t + 1) * 64], w2 = wl[(3 * t + 2) * 64];
+        if constexpr ((ABL & 4) != 0) {  // keep operands live, skip the MFMAs
+          asm volatile("" ::"v"(a0), "v"(a1), "v"(a2), "v"(w0), "v"(w1), "v"(w2));
+          continue;
+        }
         // smallest terms first
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a2, w0, acc[i], 0, 0, 0);
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1, w1, acc[i], 0, 0, 0);
@@ -160,25 +227,91 @@ __global__ void __launch_bounds__(256, 2) update_x6_kernel(
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w1, acc[i], 0, 0, 0);
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w0, acc[i], 0, 0, 0);
       }
-      __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs above the barrier's vmcnt(0)
-      __syncthreads();                     // retires chunk kb+1's LDS-DMA; frees slot kb
+      __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs above the barrier's wait
+      if constexpr (WR == 3) {
+        // only this step's DMAs (kWPW W + 2 S/H) may stay in flight
+        if (sh_ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kWPW + 2) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      } else if constexpr (SHR == 3) {
+        // only this step's two S/H DMAs may stay in flight (a __syncthreads() would drain them)
+        if (sh_ahead) asm volatile("s_waitcnt vmcnt(2) lgkmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        __syncthreads();  // retires chunk kb+1's LDS-DMA; frees slot kb
+      }
     };
+    using I0 = std::integral_constant<int, 0>;
+    using I1 = std::integral_constant<int, 1>;
+    using I2 = std::integral_constant<int, 2>;
     int kb = 0;
-    for (; kb + 2 <= KB; kb += 2) {
-      step(kb, sh0, wb0, sh1, wb1);
-      step(kb + 1, sh1, wb1, sh0, wb0);
+    if constexpr (WR == 3) {  // both rings of depth 3: period 3
+      for (; kb + 3 <= KB; kb += 3) {
+        step(kb, I0{}, I0{});
+        step(kb + 1, I1{}, I1{});
+        step(kb + 2, I2{}, I2{});
+      }
+      const int rem = KB - kb;
+      if (rem > 0) step(kb, I0{}, I0{});
+      if (rem > 1) step(kb + 1, I1{}, I1{});
+    } else if constexpr (SHR == 3) {  // ring period lcm(3, 2) = 6
+      for (; kb + 6 <= KB; kb += 6) {
+        step(kb, I0{}, I0{});
+        step(kb + 1, I1{}, I1{});
+        step(kb + 2, I2{}, I0{});
+        step(kb + 3, I0{}, I1{});
+        step(kb + 4, I1{}, I0{});
+        step(kb + 5, I2{}, I1{});
+      }
+      const int rem = KB - kb;
+      if (rem > 0) step(kb, I0{}, I0{});
+      if (rem > 1) step(kb + 1, I1{}, I1{});
+      if (rem > 2) step(kb + 2, I2{}, I0{});
+      if (rem > 3) step(kb + 3, I0{}, I1{});
+      if (rem > 4) step(kb + 4, I1{}, I0{});
+    } else {
+      for (; kb + 2 <= KB; kb += 2) {
+        step(kb, I0{}, I0{});
+        step(kb + 1, I1{}, I1{});
+      }
+      if (kb < KB) step(kb, I0{}, I0{});
     }
-    if (kb < KB) step(kb, sh0, wb0, sh1, wb1);
   };
 
-  issue(0, sh0, wb0);
-  __syncthreads();
+  issue_w(0, wb0);
+  issue_sh(0, sh0);
+  if constexpr (WR == 3) {
+    if (KB > 1) {
+      issue_w(1, wb1);
+      issue_sh(1, sh1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(kWPW + 2) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  } else if constexpr (SHR == 3) {
+    if (KB > 1) {
+      issue_sh(1, sh1);
+      asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+  } else {
+    __syncthreads();
+  }
   if (ncol == CW) body(std::integral_constant<int, CW>{});
   else body(std::integral_constant<int, NT32 - CW>{});
 
   // ---- epilogue: kEpiG-tile column groups through a wave-private slab (W ring is free now) ----
   // C/D map of 32x32 MFMA: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
-  float* slab = (wave < 2 ? wb0 : wb1) + (wave & 1) * kSlab;
+  __syncthreads();
+  float* slab = (wave < G::kWaves / 2 ? wb0 : wb1) + (wave % (G::kWaves / 2)) * kSlab;
 #pragma unroll
   for (int g = 0; g < CW; g += kEpiG) {
 #pragma unroll
@@ -236,11 +369,12 @@ __global__ void __launch_bounds__(256) pack_x6(const float* __restrict__ W, int6
   }
 }
 
-template <int NT32, int ACT>
+template <int NT32, int MW, int SHR, int WR, int ACT, int ABL = 0>
 int launch_x6(const UpdateArgs& a) {
-  const int64_t grid = (a.E + kRows - 1) / kRows;
+  using G = X6Geom<NT32, MW>;
+  const int64_t grid = (a.E + G::kRows - 1) / G::kRows;
   NT_REQUIRE(grid < (int64_t(1) << 31), NT_EINVAL, "too many edges");
-  update_x6_kernel<NT32, ACT><<<(unsigned)grid, 256, 0, a.stream>>>(
+  update_x6_kernel<NT32, MW, SHR, WR, ACT, ABL><<<(unsigned)grid, G::kThreads, 0, a.stream>>>(
       (const float4*)a.H, (const float4*)a.S, a.src, a.rev, (const uint4*)a.Wp,
       (const float4*)a.b, a.V, a.E, (int)(a.h / 4), (int)((a.h + 15) / 16), a.residual, a.act,
       a.alpha, (float4*)a.H_out);
@@ -248,11 +382,48 @@ int launch_x6(const UpdateArgs& a) {
   return NT_OK;
 }
 
+// x6 configuration (rows per workgroup / gather ring depth); NT_X6_CFG overrides for A/B runs:
+//   "a" = 64 rows, 2-slot rings   "b" = 128 rows, 2-slot rings
+//   "c" = 128 rows, 3-slot S/H ring   "d" = 128 rows, 3-slot S/H and W rings
+static char x6_cfg() {
+  const char* v = getenv("NT_X6_CFG");
+  return (v && v[0]) ? v[0] : 'a';
+}
+
+// static LDS bytes of a configuration (must stay <= 160 KiB)
+template <int NT32, int MW, int SHR, int WR>
+constexpr int x6_lds_bytes() {
+  using G = X6Geom<NT32, MW>;
+  constexpr int wpw = (NT32 * 3 + G::kWaves - 1) / G::kWaves;
+  constexpr int ws = WR == 3 ? wpw * G::kWaves * 256 : G::kW;
+  return 4 * (SHR * G::kSH + WR * ws) + 16 * G::kRows;
+}
+
+template <int NT32, int ACT>
+int launch_x6_cfg(const UpdateArgs& a) {
+  if constexpr (ACT == NT_ACT_RELU && X6Geom<NT32, 4>::kFits) {
+    const char c = x6_cfg();
+    if (c == 'b') return launch_x6<NT32, 4, 2, 2, ACT>(a);
+    if (c == 'c') return launch_x6<NT32, 4, 3, 2, ACT>(a);
+    if constexpr (x6_lds_bytes<NT32, 4, 3, 3>() <= 160 * 1024) {
+      if (c == 'd') return launch_x6<NT32, 4, 3, 3, ACT>(a);
+    }
+    if constexpr (NT32 == 10) {  // ablation builds (timing only) of config 'a'
+      if (c == '1') return launch_x6<NT32, 2, 2, 2, ACT, 1>(a);
+      if (c == '2') return launch_x6<NT32, 2, 2, 2, ACT, 2>(a);
+      if (c == '3') return launch_x6<NT32, 2, 2, 2, ACT, 3>(a);
+      if (c == '4') return launch_x6<NT32, 2, 2, 2, ACT, 4>(a);
+      if (c == '7') return launch_x6<NT32, 2, 2, 2, ACT, 7>(a);
+    }
+  }
+  return launch_x6<NT32, 2, 2, 2, ACT>(a);
+}
+
 template <int ACT, int... Ns>
 int dispatch_x6(const UpdateArgs& a, int nt32, std::integer_sequence<int, Ns...>) {
   int rc = NT_EUNSUPPORTED;
   bool done = false;
-  ((nt32 == Ns + 4 ? (rc = launch_x6<Ns + 4, ACT>(a), done = true) : false), ...);
+  ((nt32 == Ns + 4 ? (rc = launch_x6_cfg<Ns + 4, ACT>(a), done = true) : false), ...);
   if (!done) set_error("nt_dmpnn_update: no bf16x6 kernel for this hidden size");
   return rc;
 }

@@ -17,6 +17,7 @@ row 1).  The forward of a training step still runs the HIP kernels.
 """
 from __future__ import annotations
 
+import weakref
 from typing import Optional, Sequence
 
 import torch
@@ -100,15 +101,27 @@ def mol_layout(G) -> tuple[Tensor, Optional[Tensor]]:
 
 
 # ------------------------------------------------------------------------------------ forward
+# Packed-weight cache: the MFMA fragment image of a parameter is re-derived only when the
+# parameter changes (torch bumps Tensor._version on every in-place update, e.g. optimizer.step(),
+# and a new storage changes data_ptr), so inference forwards reuse it and training forwards
+# repack after every step.
+# (Keyed by id() with a weakref check: tensors cannot be WeakKeyDictionary keys because their
+# __eq__ is element-wise.)
+_PACKED: dict[int, tuple] = {}
+
+
 def pack_layer_weights(weights: Sequence[Tensor]) -> list[Tensor]:
     """One packed MFMA image per layer; shared layers (same tensor) are packed once."""
-    cache: dict[int, Tensor] = {}
     out = []
     for W in weights:
-        key = id(W)
-        if key not in cache:
-            cache[key] = K.pack_weights(W.detach())
-        out.append(cache[key])
+        key = (W.data_ptr(), W._version, tuple(W.shape), W.device)
+        hit = _PACKED.get(id(W))
+        if hit is None or hit[0]() is not W or hit[1] != key:
+            wid = id(W)
+            ref = weakref.ref(W, lambda _r, wid=wid: _PACKED.pop(wid, None))
+            hit = (ref, key, K.pack_weights(W.detach()))
+            _PACKED[wid] = hit
+        out.append(hit[2])
     return out
 
 

@@ -407,3 +407,23 @@ def test_cpu_graph_raises():
 
     with pytest.raises(RuntimeError, match="ROCm"):
         ChempropBlock(2, depth=1)(Graph(Xv, Xe, ei, rev))
+
+
+def test_packed_weight_cache_invalidation():
+    """In-place weight updates (optimizer steps) must invalidate the packed MFMA image."""
+    from notorch_amd.nn import ChempropBlock
+
+    G = _graph_tensors("qm9", 16, seed=8)
+    Xv, Xe = _embed(G, 64)
+    torch.manual_seed(0)
+    blk = ChempropBlock(64, depth=2).eval()
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
+    blk = blk.to(DEV)
+    with torch.no_grad():
+        blk(Gd)
+        for l in blk._chemprop_layers():
+            l.linear.weight.mul_(-0.5)
+        out = blk(Gd)
+    Ws, bs = dmpnn_ref.block_params(blk)
+    ref_n, ref_e = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, Ws, bs)
+    assert_parity(out.edge_feats, ref_e, what="edge after in-place weight update")

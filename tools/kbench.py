@@ -44,14 +44,23 @@ def main():
     src, rev = G.edge_index[0].contiguous(), G.rev_index
     out = torch.empty_like(H)
     relu = K.act_code(torch.nn.ReLU())
-    def upd(variant):
+    def upd(variant, cfg="a"):
         def f():
             os.environ["NT_UPDATE_KERNEL"] = variant
+            os.environ["NT_X6_CFG"] = cfg
             K.dmpnn_update(H, S, src, rev, Wp, b, act=relu, out=out)
         return f
 
     fns = {
         "update": upd("x6"),
+        "update_x6b": upd("x6", "b"),
+        "update_x6c": upd("x6", "c"),
+        "update_x6d": upd("x6", "d"),
+        "abl_noW": upd("x6", "1"),
+        "abl_noSH": upd("x6", "2"),
+        "abl_noDMA": upd("x6", "3"),
+        "abl_noMFMA": upd("x6", "4"),
+        "abl_none": upd("x6", "7"),
         "update_glds": upd("glds"),
         "update_ring": upd("ring"),
         "update_stream": upd("stream"),
@@ -76,7 +85,7 @@ def main():
         med = statistics.median(r[0] for r in res[name])
         mn = min(r[1] for r in res[name])
         extra = ""
-        if name.startswith("update"):
+        if name.startswith(("update", "abl")):
             extra = f"  {2 * E * h * h / (med * 1e-6) / 1e12:.1f} TF/s"
         else:
             rows = {"aggregate": E + V, "init_fused": 3 * E + V, "node_scatter": E + V, "pack": 0}[name]

@@ -1,0 +1,39 @@
+"""Copy the judged parts of a gpurun profile directory into profiles/<round>/ and write a summary.
+
+Usage: python tools/save_profile.py gpurun_out/prof_r1b profiles/r1 [bench.json ...]
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+os.makedirs(dst, exist_ok=True)
+lines = [f"# rocprofv3 summary ({src})", ""]
+for f in glob.glob(f"{src}/trace/*kernel_stats.csv"):
+    shutil.copy(f, os.path.join(dst, "kernel_stats.csv"))
+    lines += ["## --kernel-trace --stats", "", "| kernel | calls | avg us | % |", "|---|---|---|---|"]
+    for r in csv.DictReader(open(f)):
+        lines.append(f"| {r['Name'][:70]} | {r['Calls']} | {float(r['AverageNs']) / 1e3:.1f} | {float(r['Percentage']):.1f} |")
+    lines.append("")
+agg = collections.defaultdict(lambda: collections.defaultdict(list))
+for f in glob.glob(f"{src}/*/*counter_collection.csv"):
+    tag = os.path.basename(os.path.dirname(f))
+    shutil.copy(f, os.path.join(dst, f"counters_{tag}.csv"))
+    for r in csv.DictReader(open(f)):
+        agg[r["Kernel_Name"][:70]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+if agg:
+    lines += ["## PMC counters (mean per dispatch; separate --pmc passes)", ""]
+    for k, cs in agg.items():
+        lines.append(f"- **{k}**: " + ", ".join(f"{c}={sum(v) / len(v):.4g}" for c, v in sorted(cs.items())))
+    lines.append("")
+for b in sys.argv[3:]:
+    txt = open(b).read().strip().splitlines()[-1]
+    d = json.loads(txt)
+    shutil.copy(b, os.path.join(dst, os.path.basename(b)))
+    lines += [f"## bench line ({os.path.basename(b)})", "", "```json", json.dumps(d, indent=1), "```", ""]
+open(os.path.join(dst, "SUMMARY.md"), "w").write("\n".join(lines))
+print("wrote", dst)
