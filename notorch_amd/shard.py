@@ -26,7 +26,11 @@ def edge_balanced_ranges(edges_per_mol: np.ndarray, world_size: int) -> list[tup
     cuts = [0]
     for k in range(1, world_size):
         target = k * total / world_size
-        c = int(np.searchsorted(csum, target, side="left")) + 1
+        i = int(np.searchsorted(csum, target, side="left"))  # first prefix reaching the target
+        # cut before or after the molecule that crosses the target, whichever lands closer
+        before = csum[i - 1] if i > 0 else 0
+        after = csum[i] if i < B else total
+        c = i if (target - before) <= (after - target) else i + 1
         c = min(max(c, cuts[-1]), B)
         cuts.append(c)
     cuts.append(B)

@@ -1,0 +1,63 @@
+"""CPU: the C-ABI library loads and exports exactly what include/notorch_amd.h declares.
+No compute call is made (no GPU here); only pure-host entry points are exercised."""
+import ctypes
+import os
+import re
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "notorch_amd.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    return re.findall(r"^NT_API\s+[\w\s\*]+?\b(nt_\w+)\s*\(", txt, flags=re.M)
+
+
+def test_header_declares_the_boundary():
+    names = header_functions()
+    assert set(names) == {
+        "nt_abi_version", "nt_last_error", "nt_csr_workspace_bytes", "nt_csr_build",
+        "nt_dmpnn_init", "nt_segment_reduce", "nt_dmpnn_packed_weight_bytes",
+        "nt_dmpnn_pack_weight", "nt_dmpnn_update",
+    }
+
+
+def test_library_exports_every_header_symbol():
+    from notorch_amd import _lib
+
+    if not os.path.exists(_lib.LIB_PATH):
+        pytest.fail(f"{_lib.LIB_PATH} not built (run make)")
+    lib = _lib.load()
+    for name in header_functions():
+        assert hasattr(lib, name), name
+    # and the ctypes signature table covers exactly the header
+    assert set(_lib.SIGNATURES) == set(header_functions())
+
+
+def test_abi_version_and_errors_without_gpu():
+    from notorch_amd import _lib
+
+    lib = _lib.load()
+    assert lib.nt_abi_version() == _lib.ABI_VERSION == 1
+    assert lib.nt_dmpnn_packed_weight_bytes(300, 0) > 0
+    assert lib.nt_dmpnn_packed_weight_bytes(0, 0) == 0
+    # argument validation happens before any device call: EINVAL + message
+    rc = lib.nt_dmpnn_update(None, None, None, None, None, None, 0, 0, 0, 1, 1, 0.0, 0, None, None)
+    assert rc == 1 and b"bad sizes" in lib.nt_last_error()
+    rc = lib.nt_segment_reduce(None, None, None, 4, 8, 9, 0, 0.0, 0, None, None)
+    assert rc == 1 and b"reduce" in lib.nt_last_error()
+    rc = lib.nt_segment_reduce(None, None, None, 4, 8, 0, 0, 0.0, 1, None, None)
+    assert rc == 3  # NT_EUNSUPPORTED: bf16 segment reduce not implemented
+    rc = lib.nt_csr_build(None, -1, 3, None, None, None, 0, None, None)
+    assert rc == 1
+
+
+def test_check_raises_with_message():
+    from notorch_amd import _lib
+
+    lib = _lib.load()
+    lib.nt_dmpnn_pack_weight(None, 1, 0, 0, None, None)
+    with pytest.raises(_lib.NativeLibraryError, match="bad sizes"):
+        _lib.check(1)

@@ -1,0 +1,74 @@
+"""CPU: the vectorised collate is bit-identical to the restated reference collate
+(notorch/data/models/graph.py:186-223) in both rev-offset modes, and its CSR layout is exact."""
+import numpy as np
+import pytest
+import torch
+
+from notorch_amd.data.models.graph import BatchedGraph, Graph
+from notorch_amd.data.synth import make_batch
+from oracle import collate_ref
+
+FIELDS = ["node_feats", "edge_feats", "edge_index", "rev_index", "batch_node_index", "batch_edge_index"]
+
+
+@pytest.mark.parametrize("kind,n", [("qm9", 64), ("zinc", 16), ("polymer", 2)])
+@pytest.mark.parametrize("mode", ["nodes", "edges"])
+def test_from_graphs_bit_identical(kind, n, mode):
+    batch = make_batch(kind, n, seed=3)
+    Gs = batch.to_graphs()
+    ref = collate_ref.from_graphs(Gs, rev_offset=mode)
+    for BG in (BatchedGraph.from_graphs(Gs, rev_offset=mode), batch.collate(mode)):
+        for f in FIELDS:
+            assert torch.equal(getattr(BG, f), ref[f]), f
+        assert len(BG) == ref["size"]
+
+
+def test_reference_rev_offset_quirk_reproduced():
+    """graph.py:200 offsets rev_index by the node count: in a multi-molecule batch most rev entries
+    do NOT point at the reverse edge; the fixed collate makes rev == e ^ 1."""
+    G = make_batch("qm9", 256, seed=0).collate("nodes")
+    e = torch.arange(G.num_edges)
+    assert (G.rev_index != (e ^ 1)).float().mean() > 0.9
+    Gf = make_batch("qm9", 256, seed=0).collate("edges")
+    assert torch.equal(Gf.rev_index, e ^ 1)
+
+
+def test_layout_csr_exact():
+    G = make_batch("qm9", 128, seed=1).collate("nodes")
+    lay = G._nt_layout
+    dst = G.edge_index[1].numpy()
+    assert np.array_equal(lay.dst_perm.numpy(), np.argsort(dst, kind="stable"))
+    assert np.array_equal(lay.dst_ptr.numpy()[1:], np.cumsum(np.bincount(dst, minlength=G.num_nodes)))
+    assert lay.mol_perm is None  # batch_node_index sorted
+    assert np.array_equal(np.diff(lay.mol_ptr.numpy()), np.bincount(G.batch_node_index.numpy()))
+
+
+def test_edge_cases_zero_bond_molecule_and_empty():
+    # a single-atom molecule with no bonds (the reference MolToGraph would crash, quirk 2)
+    one = Graph(torch.tensor([[1, 12, 20, 25, 30, 36, 41]]), torch.zeros(0, 2, dtype=torch.long),
+                torch.zeros(2, 0, dtype=torch.long), torch.zeros(0, dtype=torch.long))
+    Gs = make_batch("qm9", 3, seed=2).to_graphs()
+    mixed = [Gs[0], one, Gs[1]]
+    BG = BatchedGraph.from_graphs(mixed)
+    ref = collate_ref.from_graphs(mixed)
+    for f in FIELDS:
+        assert torch.equal(getattr(BG, f), ref[f]), f
+    with pytest.raises(ValueError):
+        BatchedGraph.from_graphs([])
+
+
+def test_layout_travels_with_to_and_update():
+    G = make_batch("qm9", 8, seed=4).collate("nodes")
+    lay = G._nt_layout
+    G2 = G.update(node_feats=torch.zeros(G.num_nodes, 3))
+    assert G2._nt_layout is lay  # shallow copy shares the layout
+    G3 = G.to("cpu")
+    assert G3._nt_layout.edge_index is G3.edge_index
+
+
+def test_collate_is_picklable():
+    import pickle
+
+    G = make_batch("qm9", 4, seed=5).collate("nodes")
+    G2 = pickle.loads(pickle.dumps(G))
+    assert torch.equal(G2.edge_index, G.edge_index) and len(G2) == 4
