@@ -33,6 +33,10 @@ int pack_weight_x6(const float* W, int64_t nlayers, int64_t h, int64_t layer_str
                    hipStream_t stream);
 int launch_update_x6(const UpdateArgs& a);  // a.Wp points at the x6 image
 
+// Warp-specialised producer/consumer bf16x6 kernel (update_pc.hip): h % 4 == 0, 97 <= h <= 320.
+bool pc_supported(int64_t h);
+int launch_update_pc(const UpdateArgs& a);  // a.Wp points at the x6 image
+
 // Deeper-ring variant (S/H 2 chunks ahead); requires additionally NT <= 24.
 int launch_update_ring(const UpdateArgs& a);
 

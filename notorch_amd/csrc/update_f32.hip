@@ -37,7 +37,8 @@ constexpr int kThreads = 256;
 constexpr int kWaves = 4;
 
 // kernel selection for A/B runs (read per call):
-//   NT_UPDATE_KERNEL = x6 (default: bf16x6 fp32 emulation) | glds | ring | stream | tile (fp32 MFMA)
+//   NT_UPDATE_KERNEL = x6 (default: single-role bf16x6) | pc (producer/consumer bf16x6)
+//                      | glds | ring | stream | tile (exact fp32 MFMA)
 static char update_kernel_choice() {
   const char* v = getenv("NT_UPDATE_KERNEL");
   return (v && v[0]) ? v[0] : 'x';
@@ -561,7 +562,13 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                    (b == nullptr || aligned16(b));
   hipStream_t stream = as_stream(stream_);
   const char choice = update_kernel_choice();
-  if (vec && choice == 'x' && x6_supported(h)) {
+  if (vec && choice == 'p' && pc_supported(h)) {
+    UpdateArgs a{(const float*)H, (const float*)S, src, rev, (const char*)Wp + f32_image_bytes(h),
+                 (const float*)b, V, E, h, g.KB, g.NT, residual, act, act_alpha, (float*)H_out,
+                 stream};
+    return launch_update_pc(a);
+  }
+  if (vec && (choice == 'x' || choice == 'p') && x6_supported(h)) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, (const char*)Wp + f32_image_bytes(h),
                  (const float*)b, V, E, h, g.KB, g.NT, residual, act, act_alpha, (float*)H_out,
                  stream};
@@ -572,7 +579,7 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
     return launch_update_ring(a);
   }
-  if (vec && (choice == 'g' || choice == 'x')) {
+  if (vec && (choice == 'g' || choice == 'x' || choice == 'p')) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
     return launch_update_glds(a);

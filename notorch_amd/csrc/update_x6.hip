@@ -29,6 +29,10 @@
 
 namespace nt {
 
+// Diagnostic-build stamp accumulators (cycles summed over waves): issue, A read+split, MFMA
+// (incl. B reads), barrier/vmcnt wait, steps.  Only the ABL == 8 instantiation writes them.
+__device__ unsigned long long g_x6_stamps[8];
+
 namespace {
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
@@ -69,8 +73,10 @@ __device__ __forceinline__ void split3(const float (&x)[8], bf16x8& p0, bf16x8& 
   }
 }
 
-// ABL (timing-only ablation builds, outputs wrong): 1 = no W DMA, 2 = no S/H DMA, 4 = no MFMA
-template <int NT32, int MW, int SHR, int WR, int ACT, int ABL = 0>
+// ABL (timing-only ablation builds, outputs wrong): 1 = no W DMA, 2 = no S/H DMA, 4 = no MFMA;
+// ABL == 8: diagnostic stamp build (outputs right, slower; phase cycles -> g_x6_stamps)
+// RESACC: residual + bias preloaded into the accumulators (else added in the epilogue)
+template <int NT32, int MW, int SHR, int WR, int ACT, int ABL = 0, bool RESACC = false>
 __global__ void __launch_bounds__(128 * MW, 2) update_x6_kernel(
     const float4* __restrict__ H4, const float4* __restrict__ S4, const int64_t* __restrict__ src,
     const int64_t* __restrict__ rev, const uint4* __restrict__ Wx, const float4* __restrict__ b4,
@@ -133,9 +139,13 @@ __global__ void __launch_bounds__(128 * MW, 2) update_x6_kernel(
   const int64_t ls = s_src[lrow], lq = s_rev[lrow];
   const float4* s_row = S4 + (ls >= 0 ? ls : 0);
   const float4* h_row = H4 + (lq >= 0 ? lq : 0);
+  // LDS slot q of a 64-B row holds logical piece q ^ f(row), f(row) = (row >> 2) & 3: the swizzle
+  // (applied on the DMA source address; the DMA destination stays lane-linear) makes the
+  // ds_read_b128 fragment reads conflict-free.  For DMA lanes f(row) = (lane >> 4) & 3.
+  const int lsrc_piece = lpiece ^ ((lane >> 4) & 3);
   auto issue_sh = [&](int kb, float* shs) {
     if constexpr ((ABL & 2) != 0) return;
-    int c = 4 * kb + lpiece;
+    int c = 4 * kb + lsrc_piece;
     c = c < hv ? c : hv - 1;
     glds16(s_row + c, shs + 16 * 16 * wave);
     glds16(h_row + c, shs + kRows * 16 + 16 * 16 * wave);
@@ -161,17 +171,59 @@ __global__ void __launch_bounds__(128 * MW, 2) update_x6_kernel(
   const int c0 = ch == 0 ? 0 : CW;
   const int frow = 32 * rt + (lane & 31), fk = lane >> 5;  // fragment: k = 8 fk + j
   const bool fs_ok = s_src[frow] >= 0, fq_ok = s_rev[frow] >= 0;
+  const int fsw = (frow >> 2) & 3;                        // swizzle of this fragment row
+  const int fslot0 = 4 * ((2 * fk) ^ fsw), fslot1 = 4 * ((2 * fk + 1) ^ fsw);  // float offsets
 
   f32x16 acc[CW];
-#pragma unroll
-  for (int i = 0; i < CW; ++i)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
 
+  unsigned long long st[5] = {0, 0, 0, 0, 0};  // diagnostic stamp sums (ABL == 8)
   auto body = [&](auto nc_tag) {
     constexpr int NC = decltype(nc_tag)::value;
+    // RESACC: accumulators start at residual + bias (C/D layout: row = (r&3) + 8(r>>2) +
+    // 4(lane>>5), col = lane & 31), read here and overlapped with the K loop; each load is two
+    // full 128-B row segments.  Otherwise they start at 0 and the epilogue adds both.
+    if constexpr (!RESACC) {
+#pragma unroll
+      for (int i = 0; i < CW; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    } else {
+      const float* Hf = reinterpret_cast<const float*>(H4);
+      const float* bf = reinterpret_cast<const float*>(b4);
+      const int h = 4 * hv;
+#pragma unroll
+      for (int i = 0; i < NC; ++i) {
+        int col = 32 * (c0 + i) + (lane & 31);
+        col = col < h ? col : h - 1;  // padding columns: any finite value, never stored
+        const float bv = bf ? bf[col] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          int64_t e = e0 + 32 * rt + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
+          e = e < E ? e : E - 1;
+          acc[i][r] = residual ? Hf[e * h + col] + bv : bv;
+        }
+      }
+#pragma unroll
+      for (int i = NC; i < CW; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][r] = 0.f;
+    }
+    auto stamp = [&]() -> unsigned long long {
+      if constexpr (ABL == 8) {
+        unsigned long long t = 0;
+#if defined(__HIP_DEVICE_COMPILE__)
+        __builtin_amdgcn_sched_barrier(0);
+        asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+        __builtin_amdgcn_sched_barrier(0);
+#endif
+        return t;
+      } else {
+        return 0;
+      }
+    };
     auto step = [&](int kb, auto rs_tag, auto rw_tag) {
       constexpr int RS = decltype(rs_tag)::value, RW = decltype(rw_tag)::value;
+      const unsigned long long t0 = stamp();
       const float* shs = sh_slot(rs_tag);
       const float* wbs = wb_slot(rw_tag);
       // prefetch: W first, then S/H, so a counted vmcnt can leave the newest DMAs in flight
@@ -191,10 +243,14 @@ __global__ void __launch_bounds__(128 * MW, 2) update_x6_kernel(
           if (kb + 1 < KB) issue_sh(kb + 1, sh_slot(std::integral_constant<int, (RS + 1) % 2>{}));
         }
       }
+      const unsigned long long t1 = stamp();
       // A fragment: row frow, k = 16kb + 8fk + j  (two 16-B pieces of S and of H)
-      const float4* sp = reinterpret_cast<const float4*>(shs + frow * 16 + 8 * fk);
-      const float4* hp = reinterpret_cast<const float4*>(shs + kRows * 16 + frow * 16 + 8 * fk);
-      const float4 s0 = sp[0], s1 = sp[1], q0 = hp[0], q1 = hp[1];
+      const float* sp = shs + frow * 16;
+      const float* hp = shs + kRows * 16 + frow * 16;
+      const float4 s0 = *reinterpret_cast<const float4*>(sp + fslot0);
+      const float4 s1 = *reinterpret_cast<const float4*>(sp + fslot1);
+      const float4 q0 = *reinterpret_cast<const float4*>(hp + fslot0);
+      const float4 q1 = *reinterpret_cast<const float4*>(hp + fslot1);
       const int col4 = 4 * kb + 2 * fk;
       const bool k0 = col4 < hv, k1 = col4 + 1 < hv;
       const float4 m0 = act4_t<ACT>(q0, act, alpha), m1 = act4_t<ACT>(q1, act, alpha);
@@ -210,6 +266,10 @@ __global__ void __launch_bounds__(128 * MW, 2) update_x6_kernel(
       x[7] = (us1 ? s1.w : 0.f) - (uq1 ? m1.w : 0.f);
       bf16x8 a0, a1, a2;
       split3(x, a0, a1, a2);
+#if defined(__HIP_DEVICE_COMPILE__)
+      if constexpr (ABL == 8) asm volatile("" ::"v"(a0), "v"(a1), "v"(a2));
+#endif
+      const unsigned long long t2 = stamp();
       const bf16x8* wl = reinterpret_cast<const bf16x8*>(wbs) + lane;
 #pragma unroll
       for (int i = 0; i < NC; ++i) {
@@ -228,6 +288,13 @@ __global__ void __launch_bounds__(128 * MW, 2) update_x6_kernel(
         acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0, w0, acc[i], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);  // keep the MFMAs above the barrier's wait
+#if defined(__HIP_DEVICE_COMPILE__)
+      if constexpr (ABL == 8) {
+#pragma unroll
+        for (int i = 0; i < NC; ++i) asm volatile("" ::"v"(acc[i]));
+      }
+#endif
+      const unsigned long long t3 = stamp();
       if constexpr (WR == 3) {
         // only this step's DMAs (kWPW W + 2 S/H) may stay in flight
         if (sh_ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(kWPW + 2) : "memory");
@@ -242,6 +309,14 @@ __global__ void __launch_bounds__(128 * MW, 2) update_x6_kernel(
         __builtin_amdgcn_sched_barrier(0);
       } else {
         __syncthreads();  // retires chunk kb+1's LDS-DMA; frees slot kb
+      }
+      if constexpr (ABL == 8) {
+        const unsigned long long t4 = stamp();
+        st[0] += t1 - t0;
+        st[1] += t2 - t1;
+        st[2] += t3 - t2;
+        st[3] += t4 - t3;
+        st[4] += 1;
       }
     };
     using I0 = std::integral_constant<int, 0>;
@@ -331,12 +406,20 @@ __global__ void __launch_bounds__(128 * MW, 2) update_x6_kernel(
       const int col4 = 8 * (c0 + g) + c;
       if (e < E && col4 < hv) {
         float4 o = *reinterpret_cast<const float4*>(&slab[r * kLDE + 4 * c]);
-        if (b4) o = o + b4[col4];
-        if (residual) o = H4[e * hv + col4] + o;
+        if constexpr (!RESACC) {
+          if (b4) o = o + b4[col4];
+          if (residual) o = H4[e * hv + col4] + o;
+        }
         O4[e * hv + col4] = o;
       }
     }
     __syncthreads();
+  }
+  if constexpr (ABL == 8) {
+    if (lane == 0) {
+#pragma unroll
+      for (int i = 0; i < 5; ++i) atomicAdd(&g_x6_stamps[i], st[i]);
+    }
   }
 }
 
@@ -369,12 +452,12 @@ __global__ void __launch_bounds__(256) pack_x6(const float* __restrict__ W, int6
   }
 }
 
-template <int NT32, int MW, int SHR, int WR, int ACT, int ABL = 0>
+template <int NT32, int MW, int SHR, int WR, int ACT, int ABL = 0, bool RESACC = false>
 int launch_x6(const UpdateArgs& a) {
   using G = X6Geom<NT32, MW>;
   const int64_t grid = (a.E + G::kRows - 1) / G::kRows;
   NT_REQUIRE(grid < (int64_t(1) << 31), NT_EINVAL, "too many edges");
-  update_x6_kernel<NT32, MW, SHR, WR, ACT, ABL><<<(unsigned)grid, G::kThreads, 0, a.stream>>>(
+  update_x6_kernel<NT32, MW, SHR, WR, ACT, ABL, RESACC><<<(unsigned)grid, G::kThreads, 0, a.stream>>>(
       (const float4*)a.H, (const float4*)a.S, a.src, a.rev, (const uint4*)a.Wp,
       (const float4*)a.b, a.V, a.E, (int)(a.h / 4), (int)((a.h + 15) / 16), a.residual, a.act,
       a.alpha, (float4*)a.H_out);
@@ -414,6 +497,8 @@ int launch_x6_cfg(const UpdateArgs& a) {
       if (c == '3') return launch_x6<NT32, 2, 2, 2, ACT, 3>(a);
       if (c == '4') return launch_x6<NT32, 2, 2, 2, ACT, 4>(a);
       if (c == '7') return launch_x6<NT32, 2, 2, 2, ACT, 7>(a);
+      if (c == 'r') return launch_x6<NT32, 2, 2, 2, ACT, 0, true>(a);
+      if (c == 's') return launch_x6<NT32, 2, 2, 2, ACT, 8>(a);
     }
   }
   return launch_x6<NT32, 2, 2, 2, ACT>(a);
@@ -456,3 +541,19 @@ int launch_update_x6(const UpdateArgs& a) {
 }
 
 }  // namespace nt
+
+// Debug-only (not part of include/notorch_amd.h): read (and optionally reset) the stamp sums of the
+// diagnostic x6 build selected with NT_UPDATE_KERNEL=x6 NT_X6_CFG=s.
+extern "C" __attribute__((visibility("default"))) int nt_debug_x6_stamps(unsigned long long* out5,
+                                                                         int reset) {
+  if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(nt::g_x6_stamps), 5 * sizeof(unsigned long long), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return 2;
+  if (reset) {
+    unsigned long long z[8] = {0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(nt::g_x6_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) !=
+        hipSuccess)
+      return 2;
+  }
+  return 0;
+}

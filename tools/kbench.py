@@ -44,18 +44,26 @@ def main():
     src, rev = G.edge_index[0].contiguous(), G.rev_index
     out = torch.empty_like(H)
     relu = K.act_code(torch.nn.ReLU())
-    def upd(variant, cfg="a"):
+    def upd(variant, cfg="a", mode="0"):
         def f():
             os.environ["NT_UPDATE_KERNEL"] = variant
             os.environ["NT_X6_CFG"] = cfg
+            os.environ["NT_PC_MODE"] = mode
             K.dmpnn_update(H, S, src, rev, Wp, b, act=relu, out=out)
         return f
 
     fns = {
-        "update": upd("x6"),
+        "update": upd("pc"),
+        "pc_noW": upd("pc", mode="2"),
+        "pc_oneW": upd("pc", mode="4"),
+        "pc_noW_oneW": upd("pc", mode="6"),
+        "pc_noMFMA": upd("pc", mode="8"),
+        "pc_noW_noMFMA": upd("pc", mode="10"),
+        "update_x6": upd("x6"),
         "update_x6b": upd("x6", "b"),
         "update_x6c": upd("x6", "c"),
         "update_x6d": upd("x6", "d"),
+        "update_resacc": upd("x6", "r"),
         "abl_noW": upd("x6", "1"),
         "abl_noSH": upd("x6", "2"),
         "abl_noDMA": upd("x6", "3"),
@@ -85,7 +93,7 @@ def main():
         med = statistics.median(r[0] for r in res[name])
         mn = min(r[1] for r in res[name])
         extra = ""
-        if name.startswith(("update", "abl")):
+        if name.startswith(("update", "abl", "pc_")):
             extra = f"  {2 * E * h * h / (med * 1e-6) / 1e12:.1f} TF/s"
         else:
             rows = {"aggregate": E + V, "init_fused": 3 * E + V, "node_scatter": E + V, "pack": 0}[name]
