@@ -121,6 +121,38 @@ NT_API int nt_dmpnn_update(const void* H, const void* S, const int64_t* src, con
                     const void* Wp, const void* b, int64_t V, int64_t E, int64_t h, int residual,
                     int act, float act_alpha, int dtype, void* H_out, void* stream);
 
+/*
+ * Tile plan for nt_dmpnn_update_fused: cuts the dst-sorted edge order (positions of the
+ * nt_csr_build(edge_index[1]) permutation) into tiles of at most 64 positions at node boundaries,
+ * so every node's in-edges fall in one tile.  Tile k starts at dst_ptr[first v with
+ * dst_ptr[v] >= k L], L = 65 - max(max_in_degree, 1); tile_ptr[ntiles] = E.
+ * dst_sorted[p] = the node whose in-edge sits at position p.
+ * max_in_degree must be <= 32 (graphs with hubs use the unfused nt_dmpnn_update +
+ * nt_segment_reduce path); ntiles must equal nt_dmpnn_tile_count(E, max_in_degree).
+ * Replaces the per-layer segmentation implied by scatter(..., dest) (chemprop.py:39, :86).
+ */
+NT_API int64_t nt_dmpnn_tile_count(int64_t E, int max_in_degree);
+NT_API int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, int max_in_degree,
+                              int32_t* tile_ptr, int64_t ntiles, int32_t* dst_sorted, void* stream);
+
+/*
+ * One D-MPNN layer fused with the aggregation that consumes it (chemprop.py:36-43 of layer l,
+ * residual.py:27-28, then chemprop.py:37-39 of layer l+1 or, with agg_act = NT_ACT_IDENTITY, the
+ * final node scatter of chemprop.py:86):
+ *   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b
+ *   S_out[v] = reduce_{e: dst[e]=v} agg_act(H_out[e])      (ascending e; empty segment -> 0)
+ * (tile_ptr, ntiles, dst_sorted) = nt_dmpnn_tile_plan; perm = the dst CSR permutation.
+ * With tile_ptr = NULL (and perm, dst_sorted, S_out = NULL) only H_out is computed (same result as
+ * nt_dmpnn_update, persistent producer/consumer kernel).  Requires h % 4 == 0, h <= 304,
+ * 16-byte aligned feature pointers.  S_out must not alias S.
+ */
+NT_API int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* src, const int64_t* rev,
+                                 const void* Wp, const void* b, int64_t V, int64_t E, int64_t h,
+                                 int residual, int act, float act_alpha, const int32_t* tile_ptr,
+                                 int64_t ntiles, const int32_t* perm, const int32_t* dst_sorted,
+                                 int reduce, int agg_act, float agg_alpha, int dtype, void* H_out,
+                                 void* S_out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

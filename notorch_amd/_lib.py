@@ -57,6 +57,13 @@ SIGNATURES: dict[str, tuple] = {
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp],
     ),
+    "nt_dmpnn_tile_count": (_c_i64, [_c_i64, _c_int]),
+    "nt_dmpnn_tile_plan": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
+    "nt_dmpnn_update_fused": (
+        _c_int,
+        [_vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _vp, _c_i64,
+         _vp, _vp, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp],
+    ),
 }
 
 

@@ -37,6 +37,19 @@ int launch_update_x6(const UpdateArgs& a);  // a.Wp points at the x6 image
 bool pc_supported(int64_t h);
 int launch_update_pc(const UpdateArgs& a);  // a.Wp points at the x6 image
 
+// A-stationary bf16x6 kernel (update_as.hip, 16x16x32 MFMA): h % 4 == 0, h <= 304.
+bool as_supported(int64_t h);
+size_t as_image_bytes(int64_t h);
+int pack_weight_as(const float* W, int64_t nlayers, int64_t h, int64_t layer_stride_bytes, void* Wb,
+                   hipStream_t stream);
+int launch_update_as(const UpdateArgs& a);  // a.Wp points at the as16 image
+
+// Persistent producer/consumer kernel (update_ps.hip), optionally fused with the aggregation.
+bool ps_supported(int64_t h);
+int launch_update_ps(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntiles,
+                     const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
+                     float* S_out);  // u.Wp points at the as16 image
+
 // Deeper-ring variant (S/H 2 chunks ahead); requires additionally NT <= 24.
 int launch_update_ring(const UpdateArgs& a);
 

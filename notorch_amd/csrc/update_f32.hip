@@ -37,11 +37,12 @@ constexpr int kThreads = 256;
 constexpr int kWaves = 4;
 
 // kernel selection for A/B runs (read per call):
-//   NT_UPDATE_KERNEL = x6 (default: single-role bf16x6) | pc (producer/consumer bf16x6)
+//   NT_UPDATE_KERNEL = as (default: A-stationary bf16x6) | x6 (LDS-ring bf16x6)
+//                      | pc (producer/consumer bf16x6)
 //                      | glds | ring | stream | tile (exact fp32 MFMA)
 static char update_kernel_choice() {
   const char* v = getenv("NT_UPDATE_KERNEL");
-  return (v && v[0]) ? v[0] : 'x';
+  return (v && v[0]) ? v[0] : 'a';
 }
 
 struct UpdateGeom {
@@ -500,8 +501,9 @@ static int dispatch_cpw(const float* H, const float* S, const int64_t* src, cons
 
 }  // namespace nt
 
-// Packed image per layer: [fp32 fragment image (16x16x4 MFMA)][bf16x6 image (32x32x16 MFMA)],
-// each part 256-B aligned; the update kernel variant picks the part it consumes.
+// Packed image per layer: [fp32 fragment image (16x16x4 MFMA)][bf16x6 image (32x32x16 MFMA)]
+// [bf16x6 image (16x16x32 MFMA)], each part 256-B aligned; the update kernel variant picks the
+// part it consumes.
 static size_t f32_image_bytes(int64_t h) {
   const nt::UpdateGeom g = nt::geom_for(h);
   return ((size_t)g.KB * g.NT * 64 * sizeof(float4) + 255) & ~size_t(255);
@@ -510,10 +512,14 @@ static size_t x6_part_bytes(int64_t h) {
   return nt::x6_supported(h) ? ((nt::x6_image_bytes(h) + 255) & ~size_t(255)) : 0;
 }
 
+static size_t as_part_bytes(int64_t h) {
+  return nt::as_supported(h) ? ((nt::as_image_bytes(h) + 255) & ~size_t(255)) : 0;
+}
+
 extern "C" size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype) {
   (void)dtype;
   if (h <= 0) return 0;
-  return f32_image_bytes(h) + x6_part_bytes(h);
+  return f32_image_bytes(h) + x6_part_bytes(h) + as_part_bytes(h);
 }
 
 extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, int dtype, void* Wp,
@@ -541,6 +547,11 @@ extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, i
                             (char*)Wp + f32_image_bytes(h), stream);
     if (rc != NT_OK) return rc;
   }
+  if (as_supported(h)) {
+    int rc = pack_weight_as((const float*)W, nlayers, h, (int64_t)per_layer,
+                            (char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), stream);
+    if (rc != NT_OK) return rc;
+  }
   return NT_OK;
 }
 
@@ -562,13 +573,19 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                    (b == nullptr || aligned16(b));
   hipStream_t stream = as_stream(stream_);
   const char choice = update_kernel_choice();
+  if (vec && choice == 'a' && as_supported(h)) {
+    UpdateArgs a{(const float*)H, (const float*)S, src, rev,
+                 (const char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), (const float*)b, V, E, h,
+                 g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
+    return launch_update_as(a);
+  }
   if (vec && choice == 'p' && pc_supported(h)) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, (const char*)Wp + f32_image_bytes(h),
                  (const float*)b, V, E, h, g.KB, g.NT, residual, act, act_alpha, (float*)H_out,
                  stream};
     return launch_update_pc(a);
   }
-  if (vec && (choice == 'x' || choice == 'p') && x6_supported(h)) {
+  if (vec && (choice == 'x' || choice == 'p' || choice == 'a') && x6_supported(h)) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, (const char*)Wp + f32_image_bytes(h),
                  (const float*)b, V, E, h, g.KB, g.NT, residual, act, act_alpha, (float*)H_out,
                  stream};
@@ -579,7 +596,7 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
     return launch_update_ring(a);
   }
-  if (vec && (choice == 'g' || choice == 'x' || choice == 'p')) {
+  if (vec && (choice == 'g' || choice == 'x' || choice == 'p' || choice == 'a')) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
     return launch_update_glds(a);
@@ -592,4 +609,33 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
   return dispatch_cpw<32>((const float*)H, (const float*)S, src, rev, (const float4*)Wp,
                           (const float*)b, V, E, (int)h, g, residual, act, act_alpha,
                           (float*)H_out, vec, stream);
+}
+
+extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* src,
+                                     const int64_t* rev, const void* Wp, const void* b, int64_t V,
+                                     int64_t E, int64_t h, int residual, int act, float act_alpha,
+                                     const int32_t* tile_ptr, int64_t ntiles, const int32_t* perm,
+                                     const int32_t* dst_sorted, int reduce, int agg_act,
+                                     float agg_alpha, int dtype, void* H_out, void* S_out,
+                                     void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for update_fused");
+  NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
+  NT_REQUIRE(agg_act >= NT_ACT_IDENTITY && agg_act <= NT_ACT_SIGMOID, NT_EINVAL, "bad agg_act code");
+  NT_REQUIRE(reduce >= NT_SUM && reduce <= NT_MIN, NT_EINVAL, "bad reduce code");
+  NT_REQUIRE(V >= 0 && E >= 0 && E < (int64_t(1) << 31) && h > 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(ps_supported(h), NT_EUNSUPPORTED, "update_fused needs h % 4 == 0 and h <= 304");
+  if (E == 0) return NT_OK;
+  NT_REQUIRE(H && S && src && rev && Wp && H_out, NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(H != H_out && (S_out == nullptr || S_out != S), NT_EINVAL, "outputs alias inputs");
+  NT_REQUIRE(aligned16(H) && aligned16(S) && aligned16(H_out) && aligned16(Wp) &&
+                 (b == nullptr || aligned16(b)) && (S_out == nullptr || aligned16(S_out)),
+             NT_EINVAL, "feature pointers must be 16-byte aligned");
+  const UpdateGeom g = geom_for(h);
+  UpdateArgs a{(const float*)H, (const float*)S, src, rev,
+               (const char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), (const float*)b, V, E, h,
+               g.KB, g.NT, residual, act, act_alpha, (float*)H_out, as_stream(stream_)};
+  return launch_update_ps(a, tile_ptr, ntiles, perm, dst_sorted, reduce, agg_act, agg_alpha,
+                          (float*)S_out);
 }

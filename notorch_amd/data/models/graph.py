@@ -54,6 +54,9 @@ class DeviceLayout:
     edge_index: Optional[Tensor] = None
     batch_node_index: Optional[Tensor] = None
     validated: bool = False  # src/dst in [0,V), rev in [0,E) checked
+    # fused-update tile plan (tile_ptr, ntiles, dst_sorted, zero_fill), derived lazily on the device
+    # by notorch_amd.nn.gnn._engine.fused_plan; False = not available (in-degree > 32)
+    plan: object = None
 
     def to(self, device, edge_index: Tensor, batch_node_index: Optional[Tensor]) -> "DeviceLayout":
         mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731

@@ -19,6 +19,9 @@ __all__ = [
     "segment_reduce",
     "pack_weights",
     "dmpnn_update",
+    "tile_plan",
+    "fused_supported",
+    "dmpnn_update_fused",
     "act_code",
     "reduce_code",
 ]
@@ -253,3 +256,89 @@ def dmpnn_update(
         )
     )
     return out
+
+
+def fused_supported(V: int, E: int, h: int) -> bool:
+    """Shapes the fused persistent kernel (nt_dmpnn_update_fused) accepts."""
+    return h % 4 == 0 and 4 <= h <= 304 and E * h // 4 < 2**31 and V * h // 4 < 2**31 and E < 2**31
+
+
+def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int) -> tuple[Tensor, int, Tensor]:
+    """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) for nt_dmpnn_update_fused (max_in_degree <= 32)."""
+    dev = _require_device(dst_ptr)
+    if dst_ptr.dtype != torch.int32:
+        raise TypeError("dst_ptr must be int32")
+    V = dst_ptr.numel() - 1
+    lib = _lib.load()
+    ntiles = int(lib.nt_dmpnn_tile_count(E, max_in_degree))
+    tile_ptr = torch.empty(ntiles + 1, dtype=torch.int32, device=dev)
+    dsts = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
+    check(
+        lib.nt_dmpnn_tile_plan(
+            _ptr(dst_ptr), V, E, max_in_degree, _ptr(tile_ptr), ntiles, _ptr(dsts), _stream(dev)
+        )
+    )
+    return tile_ptr, ntiles, dsts
+
+
+def dmpnn_update_fused(
+    H: Tensor,
+    S: Tensor,
+    src: Tensor,
+    rev: Tensor,
+    Wp: Tensor,
+    bias: Tensor | None,
+    *,
+    residual: bool = True,
+    act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
+    plan: tuple[Tensor, int, Tensor] | None = None,
+    perm: Tensor | None = None,
+    reduce: str = "sum",
+    agg_act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
+    zero_fill: bool = False,
+    out: Tensor | None = None,
+    S_out: Tensor | None = None,
+) -> tuple[Tensor, Tensor | None]:
+    """H_out = (residual ? H : 0) + (S[src] - act(H[rev])) @ W^T + b and, with a tile plan,
+    S_out = scatter(agg_act(H_out), dst, reduce) in the same persistent launch.
+
+    ``zero_fill`` must be True when some node has no in-edge (its S_out row is then 0)."""
+    dev = _require_device(H, S, src, rev, Wp, bias, out, S_out, perm)
+    _require_f32("H", H)
+    _require_f32("S", S)
+    _require_i64("src", src)
+    _require_i64("rev_index", rev)
+    E, h = H.shape
+    V = S.shape[0]
+    if S.shape[1] != h or src.numel() != E or rev.numel() != E:
+        raise ValueError("shape mismatch between H, S, src and rev_index")
+    if Wp.numel() != packed_weight_numel(h):
+        raise ValueError("Wp is not a packed weight image for this hidden size")
+    if bias is not None:
+        _require_f32("bias", bias)
+        if bias.numel() != h:
+            raise ValueError("bias must have h entries")
+    if out is None:
+        out = torch.empty_like(H)
+    tile_ptr = dsts = None
+    ntiles = 0
+    if plan is not None:
+        tile_ptr, ntiles, dsts = plan
+        if perm is None or perm.dtype != torch.int32 or perm.numel() != E:
+            raise ValueError("fused aggregation needs the int32 dst CSR permutation")
+        if S_out is None:
+            S_out = (torch.zeros if zero_fill else torch.empty)(V, h, dtype=H.dtype, device=dev)
+        elif zero_fill:
+            S_out.zero_()
+    else:
+        perm = None
+        S_out = None
+    lib = _lib.load()
+    check(
+        lib.nt_dmpnn_update_fused(
+            _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
+            act[0], act[1], _ptr(tile_ptr), ntiles, _ptr(perm), _ptr(dsts), reduce_code(reduce),
+            agg_act[0], agg_act[1], NT_F32, _ptr(out), _ptr(S_out), _stream(dev),
+        )
+    )
+    return out, S_out

@@ -1,15 +1,18 @@
 """Device engine behind ChempropBlock / readouts: layout management, the fused layer loop and the
 autograd wrapper.
 
-Forward (per call, all on ``torch.cuda.current_stream()``, inputs already resident):
+Forward (per call, all on ``torch.cuda.current_stream()``, inputs already resident).  Fused path
+(every node's in-degree <= 32 and h % 4 == 0, h <= 304 — molecules):
 
-    nt_dmpnn_init       H0 = Xv[src] + Xe  fused with  S = scatter(act(H0), dst)   chemprop.py:82-83,37-39
+    nt_dmpnn_init         H0 = Xv[src] + Xe  fused with  S = scatter(act(H0), dst)  chemprop.py:82-83,37-39
     for l in 0..d-1:
-      nt_dmpnn_update   H_{l+1} = H_l + W_l (S[src] - act(H_l)[rev]) + b_l         chemprop.py:40-41, residual.py:28
-      nt_segment_reduce S = scatter(act(H_{l+1}), dst)        (skipped after the last layer)
-    nt_segment_reduce   node = scatter(H_d, dst)                                      chemprop.py:86
+      nt_dmpnn_update_fused  H_{l+1} = H_l + W_l (S[src] - act(H_l)[rev]) + b_l      chemprop.py:40-41, residual.py:28
+                             S = scatter(act(H_{l+1}), dst)   (last layer: node = scatter(H_d, dst),
+                                                               chemprop.py:86)
 
-plus one ``nt_dmpnn_pack_weight`` per distinct layer weight.  2 + 2d launches in all.
+d + 1 launches (+ one nt_dmpnn_pack_weight per distinct weight, cached).  Otherwise (hubs, other h):
+
+    nt_dmpnn_init; for l: nt_dmpnn_update, nt_segment_reduce; nt_segment_reduce (node)   2 + 2d launches
 
 Backward (training) is, for this round, a recompute of the same math in PyTorch device ops
 followed by autograd (``_torch_block``) — correct for every option, not yet a kernel (SURVEY §8(f)
@@ -100,6 +103,28 @@ def mol_layout(G) -> tuple[Tensor, Optional[Tensor]]:
     return mol_ptr, mol_perm
 
 
+def fused_plan(lay: DeviceLayout, V: int, E: int):
+    """Tile plan of the fused update for this layout (cached on it), or None when some node has more
+    than 32 in-edges (polymer hubs): those graphs take the unfused path.  One sync per layout."""
+    if lay.plan is None:
+        plan = False
+        if E > 0 and V > 0:
+            deg = lay.dst_ptr[1:] - lay.dst_ptr[:-1]
+            mm = torch.stack([deg.max(), deg.min()]).cpu()
+            maxdeg, mindeg = int(mm[0]), int(mm[1])
+            if maxdeg <= 32:
+                tile_ptr, ntiles, dsts = K.tile_plan(lay.dst_ptr, E, maxdeg)
+                plan = (tile_ptr, ntiles, dsts, mindeg == 0)
+        lay.plan = plan
+    return lay.plan or None
+
+
+def _fused_enabled() -> bool:
+    import os
+
+    return os.environ.get("NT_FUSED", "1") != "0"
+
+
 # ------------------------------------------------------------------------------------ forward
 # Packed-weight cache: the MFMA fragment image of a parameter is re-derived only when the
 # parameter changes (torch bumps Tensor._version on every in-place update, e.g. optimizer.step(),
@@ -147,6 +172,10 @@ def block_forward(
         return node, H, [H]
     Wps = pack_layer_weights(weights)
     H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
+    E, h = H.shape
+    plan = fused_plan(lay, V, E) if _fused_enabled() and K.fused_supported(V, E, h) else None
+    if plan is not None:
+        return _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual, keep_states)
     states = [H]
     spare: Optional[Tensor] = None  # ping-pong buffer when states are not kept
     timer = UPDATE_EVENTS
@@ -170,6 +199,36 @@ def block_forward(
         H = Hn
     node = K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=_IDENTITY)
     return node, H, states
+
+
+def _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual, keep_states):
+    tile_ptr, ntiles, dsts, zero_fill = plan
+    d = len(Wps)
+    states = [H]
+    spare_H: Optional[Tensor] = None
+    spare_S: Optional[Tensor] = None
+    timer = UPDATE_EVENTS
+    for l in range(d):
+        last = l == d - 1
+        if timer is not None:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
+        Hn, Sn = K.dmpnn_update_fused(
+            H, S, src, rev, Wps[l], None if biases[l] is None else biases[l].detach(),
+            residual=residual, act=act, plan=(tile_ptr, ntiles, dsts), perm=lay.dst_perm,
+            reduce=reduce, agg_act=_IDENTITY if last else act, zero_fill=zero_fill,
+            out=spare_H, S_out=None if last else spare_S,
+        )
+        if timer is not None:
+            ev[1].record()
+            timer.append(ev)
+        if keep_states:
+            states.append(Hn)
+        else:
+            spare_H = H
+        spare_S = S
+        H, S = Hn, Sn
+    return S, H, states
 
 
 # ------------------------------------------------------------------------------------ autograd

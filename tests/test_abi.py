@@ -20,7 +20,8 @@ def test_header_declares_the_boundary():
     assert set(names) == {
         "nt_abi_version", "nt_last_error", "nt_csr_workspace_bytes", "nt_csr_build",
         "nt_dmpnn_init", "nt_segment_reduce", "nt_dmpnn_packed_weight_bytes",
-        "nt_dmpnn_pack_weight", "nt_dmpnn_update",
+        "nt_dmpnn_pack_weight", "nt_dmpnn_update", "nt_dmpnn_tile_count", "nt_dmpnn_tile_plan",
+        "nt_dmpnn_update_fused",
     }
 
 

@@ -1,0 +1,210 @@
+"""GPU parity of the persistent fused layer kernel (nt_dmpnn_update_fused) and its tile plan.
+
+The kernel computes one layer (chemprop.py:36-43, residual.py:27-28) and, with a tile plan, the
+aggregation the next layer consumes (chemprop.py:37-39) or the final node scatter (chemprop.py:86).
+Reference: the fp64 restatement of the same ops; criterion FP32_NORM_TOL; the tile
+plan and the node sums' order are checked exactly.
+"""
+import pytest
+import torch
+import torch.nn as nn
+
+from helpers import FP32_NORM_TOL, assert_parity
+from oracle import dmpnn_ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _K():
+    from notorch_amd import kernels
+
+    return kernels
+
+
+def _graph(kind="qm9", n=40, seed=0, rev_offset="nodes"):
+    from notorch_amd.data.synth import make_batch
+
+    return make_batch(kind, n, seed=seed).collate(rev_offset)
+
+
+def _csr(G):
+    K = _K()
+    return K.csr_build(G.edge_index[1].contiguous().to(DEV), G.num_nodes)
+
+
+def _plan(G):
+    K = _K()
+    dst_ptr, perm = _csr(G)
+    deg = (dst_ptr[1:] - dst_ptr[:-1]).cpu()
+    tile_ptr, ntiles, dsts = K.tile_plan(dst_ptr, G.num_edges, int(deg.max()))
+    return dst_ptr, perm, (tile_ptr, ntiles, dsts), bool((deg == 0).any())
+
+
+def test_tile_plan_invariants():
+    G = _graph("qm9", 300, seed=5)
+    dst_ptr, perm, (tile_ptr, ntiles, dsts), _ = _plan(G)
+    tp = tile_ptr.cpu().long()
+    dp = dst_ptr.cpu().long()
+    E = G.num_edges
+    assert tp[0] == 0 and tp[-1] == E and len(tp) == ntiles + 1
+    sizes = tp[1:] - tp[:-1]
+    assert (sizes > 0).all() and (sizes <= 64).all()
+    # every cut is a node boundary of the dst CSR
+    assert torch.isin(tp, dp).all()
+    # dst_sorted[p] == dst of the edge at position p
+    dst = G.edge_index[1]
+    assert torch.equal(dsts.cpu().long(), dst[perm.cpu().long()])
+
+
+def _ref_layer(G, H, S, W, b, residual, act, reduce, agg_act):
+    src, dst, rev = G.edge_index[0], G.edge_index[1], G.rev_index
+    Hd, Sd = H.double(), S.double()
+    A = Sd[src] - act(Hd)[rev]
+    U = nn.functional.linear(A, W.double(), None if b is None else b.double())
+    Hn = Hd + U if residual else U
+    Sn = dmpnn_ref.scatter(agg_act(Hn), dst, G.num_nodes, reduce)
+    return Hn, Sn
+
+
+@pytest.mark.parametrize("h", [300, 296, 256, 100, 36])
+@pytest.mark.parametrize("rev_offset", ["nodes", "edges"])
+def test_fused_layer(h, rev_offset):
+    K = _K()
+    G = _graph("qm9", 45, seed=h, rev_offset=rev_offset)
+    E, V = G.num_edges, G.num_nodes
+    g = torch.Generator().manual_seed(h)
+    H, S = torch.randn(E, h, generator=g), torch.randn(V, h, generator=g)
+    lin = nn.Linear(h, h)
+    W, b = lin.weight.detach(), lin.bias.detach()
+    _, perm, plan, zf = _plan(G)
+    Wp = K.pack_weights(W.to(DEV))
+    relu = K.act_code(nn.ReLU())
+    Hn, Sn = K.dmpnn_update_fused(
+        H.to(DEV), S.to(DEV), G.edge_index[0].to(DEV), G.rev_index.to(DEV), Wp, b.to(DEV),
+        residual=True, act=relu, plan=plan, perm=perm, reduce="sum", agg_act=relu, zero_fill=zf,
+    )
+    rH, rS = _ref_layer(G, H, S, W, b, True, torch.relu, "sum", torch.relu)
+    assert_parity(Hn, rH, FP32_NORM_TOL, f"H h={h}")
+    assert_parity(Sn, rS, FP32_NORM_TOL, f"S h={h}")
+    # the node sums are exactly the CPU scatter_add_ of the kernel's own H_out (ascending edge id)
+    exact = dmpnn_ref.scatter(torch.relu(Hn.cpu()), G.edge_index[1], V, "sum")
+    assert torch.equal(Sn.cpu(), exact)
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
+@pytest.mark.parametrize("agg", ["relu", "identity"])
+def test_fused_reduce_and_final_scatter(reduce, agg):
+    K = _K()
+    h = 64
+    G = _graph("qm9", 30, seed=11)
+    E, V = G.num_edges, G.num_nodes
+    g = torch.Generator().manual_seed(3)
+    H, S = torch.randn(E, h, generator=g), torch.randn(V, h, generator=g)
+    W = torch.randn(h, h, generator=g) / 8
+    _, perm, plan, zf = _plan(G)
+    act_mod = nn.ReLU() if agg == "relu" else nn.Identity()
+    Hn, Sn = K.dmpnn_update_fused(
+        H.to(DEV), S.to(DEV), G.edge_index[0].to(DEV), G.rev_index.to(DEV), K.pack_weights(W.to(DEV)),
+        None, residual=False, act=K.act_code(nn.ReLU()), plan=plan, perm=perm, reduce=reduce,
+        agg_act=K.act_code(act_mod), zero_fill=zf,
+    )
+    rH, rS = _ref_layer(G, H, S, W, None, False, torch.relu, reduce, act_mod)
+    assert_parity(Hn, rH, FP32_NORM_TOL, "H")
+    exact = dmpnn_ref.scatter(act_mod(Hn.cpu()), G.edge_index[1], V, reduce)
+    assert torch.equal(Sn.cpu(), exact), reduce
+
+
+def test_fused_runtime_activation():
+    K = _K()
+    h = 100
+    G = _graph("qm9", 20, seed=2)
+    E, V = G.num_edges, G.num_nodes
+    g = torch.Generator().manual_seed(9)
+    H, S = torch.randn(E, h, generator=g), torch.randn(V, h, generator=g)
+    W = torch.randn(h, h, generator=g) / 10
+    _, perm, plan, zf = _plan(G)
+    for act in (nn.SiLU(), nn.Tanh(), nn.ELU()):
+        code = K.act_code(act)
+        Hn, Sn = K.dmpnn_update_fused(
+            H.to(DEV), S.to(DEV), G.edge_index[0].to(DEV), G.rev_index.to(DEV),
+            K.pack_weights(W.to(DEV)), None, residual=True, act=code, plan=plan, perm=perm,
+            agg_act=code, zero_fill=zf,
+        )
+        rH, rS = _ref_layer(G, H, S, W, None, True, act, "sum", act)
+        assert_parity(Hn, rH, FP32_NORM_TOL, type(act).__name__)
+        assert_parity(Sn, rS, FP32_NORM_TOL, type(act).__name__)
+
+
+def test_unfused_persistent_matches_update():
+    """plan=None: the persistent kernel computes exactly nt_dmpnn_update's H_out."""
+    K = _K()
+    h = 300
+    G = _graph("qm9", 70, seed=4)
+    E, V = G.num_edges, G.num_nodes
+    g = torch.Generator().manual_seed(1)
+    H, S = torch.randn(E, h, generator=g).to(DEV), torch.randn(V, h, generator=g).to(DEV)
+    lin = nn.Linear(h, h).to(DEV)
+    Wp = K.pack_weights(lin.weight.detach())
+    src, rev = G.edge_index[0].to(DEV), G.rev_index.to(DEV)
+    relu = K.act_code(nn.ReLU())
+    Hn, Sn = K.dmpnn_update_fused(H, S, src, rev, Wp, lin.bias.detach(), residual=True, act=relu)
+    assert Sn is None
+    with torch.no_grad():
+        ref = H.double() + nn.functional.linear(
+            S.double()[src] - torch.relu(H.double())[rev], lin.weight.double(), lin.bias.double()
+        )
+    assert_parity(Hn, ref, FP32_NORM_TOL, "unfused persistent")
+
+
+def test_fused_zero_in_degree_nodes():
+    """A node without in-edges gets S_out = 0 (torch_scatter's empty segment), via zero_fill."""
+    from notorch_amd.data.models.graph import BatchedGraph, Graph
+
+    K = _K()
+    h = 32
+    gs = [
+        Graph(torch.zeros(3, 7, dtype=torch.long), torch.zeros(4, 2, dtype=torch.long),
+              torch.tensor([[0, 1, 1, 2], [1, 0, 2, 1]]), torch.tensor([1, 0, 3, 2])),
+        Graph(torch.zeros(1, 7, dtype=torch.long), torch.zeros(0, 2, dtype=torch.long),
+              torch.zeros(2, 0, dtype=torch.long), torch.zeros(0, dtype=torch.long)),
+        Graph(torch.zeros(2, 7, dtype=torch.long), torch.zeros(2, 2, dtype=torch.long),
+              torch.tensor([[0, 1], [1, 0]]), torch.tensor([1, 0])),
+    ]
+    G = BatchedGraph.from_graphs(gs, rev_offset="edges")
+    E, V = G.num_edges, G.num_nodes
+    g = torch.Generator().manual_seed(0)
+    H, S = torch.randn(E, h, generator=g), torch.randn(V, h, generator=g)
+    W = torch.randn(h, h, generator=g) / 5
+    _, perm, plan, zf = _plan(G)
+    assert zf
+    relu = K.act_code(nn.ReLU())
+    Hn, Sn = K.dmpnn_update_fused(
+        H.to(DEV), S.to(DEV), G.edge_index[0].to(DEV), G.rev_index.to(DEV), K.pack_weights(W.to(DEV)),
+        None, residual=True, act=relu, plan=plan, perm=perm, agg_act=relu, zero_fill=zf,
+    )
+    rH, rS = _ref_layer(G, H, S, W, None, True, torch.relu, "sum", torch.relu)
+    assert_parity(Hn, rH, FP32_NORM_TOL, "H")
+    assert_parity(Sn, rS, FP32_NORM_TOL, "S")
+    assert (Sn[3] == 0).all()
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_block_paths_agree(fused, monkeypatch):
+    """ChempropBlock through the fused path and through the unfused path, against the oracle."""
+    from notorch_amd.nn import ChempropBlock
+
+    monkeypatch.setenv("NT_FUSED", fused)
+    h = 300
+    G = _graph("qm9", 64, seed=8)
+    torch.manual_seed(0)
+    Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
+    blk = ChempropBlock(hidden_dim=h, depth=3).eval()
+    Ws, bs = dmpnn_ref.block_params(blk)
+    ref_node, ref_edge = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, Ws, bs)
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
+    with torch.no_grad():
+        out = blk.to(DEV)(Gd)
+    assert_parity(out.edge_feats, ref_edge, FP32_NORM_TOL, f"edge fused={fused}")
+    assert_parity(out.node_feats, ref_node, FP32_NORM_TOL, f"node fused={fused}")

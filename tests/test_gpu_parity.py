@@ -117,6 +117,29 @@ def test_update_kernel(h, residual):
     assert_parity(out, ref, FP32_NORM_TOL, f"update h={h}")
 
 
+@pytest.mark.parametrize("variant", ["as", "x6", "pc", "glds"])
+@pytest.mark.parametrize("h", [300, 296, 256, 100, 36])
+def test_update_kernel_variants(variant, h, monkeypatch):
+    """Every selectable update kernel (NT_UPDATE_KERNEL) against the fp64 restatement."""
+    K = _K()
+    monkeypatch.setenv("NT_UPDATE_KERNEL", variant)
+    G = _graph_tensors("qm9", 37, seed=h + 1)
+    E, V = G.edge_index.shape[1], G.num_nodes
+    g = torch.Generator().manual_seed(h + 7)
+    H = torch.randn(E, h, generator=g)
+    S = torch.randn(V, h, generator=g)
+    lin = nn.Linear(h, h)
+    src, rev = G.edge_index[0], G.rev_index
+    out = K.dmpnn_update(
+        H.to(DEV), S.to(DEV), src.to(DEV), rev.to(DEV), K.pack_weights(lin.weight.detach().to(DEV)),
+        lin.bias.detach().to(DEV), residual=True, act=K.act_code(nn.ReLU()),
+    )
+    with torch.no_grad():
+        A = S.double()[src] - torch.relu(H.double())[rev]
+        ref = H.double() + nn.functional.linear(A, lin.weight.double(), lin.bias.double())
+    assert_parity(out, ref, FP32_NORM_TOL, f"update[{variant}] h={h}")
+
+
 def test_update_kernel_no_bias_and_acts():
     K = _K()
     G = _graph_tensors("qm9", 16, seed=3)

@@ -52,8 +52,56 @@ def main():
             K.dmpnn_update(H, S, src, rev, Wp, b, act=relu, out=out)
         return f
 
+    deg = (lay.dst_ptr[1:] - lay.dst_ptr[:-1]).max().item()
+    plan = K.tile_plan(lay.dst_ptr, E, int(deg))
+    S2 = torch.empty_like(S)
+
+    ident = torch.arange(E, dtype=torch.int32, device="cuda")
+    fake_d = (ident.long() * V // E).to(torch.int32)  # monotone, < V: timing stand-in only
+    eplan = (torch.arange(0, E + 64, 64, dtype=torch.int32, device="cuda").clamp_(max=E), (E + 63) // 64, fake_d)
+
+    def fused_edge_order():
+        os.environ["NT_PS_ABL"] = "0"
+        K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=eplan, perm=ident, agg_act=relu,
+                             out=out, S_out=S2)
+
+    def fused(kmid=None, with_plan=True, abl=0):
+        def f():
+            os.environ["NT_PS_ABL"] = str(abl)
+            if kmid is not None:
+                os.environ["NT_PS_KMID"] = str(kmid)
+            else:
+                os.environ.pop("NT_PS_KMID", None)
+            K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=plan if with_plan else None,
+                                 perm=lay.dst_perm, agg_act=relu, out=out,
+                                 S_out=S2 if with_plan else None)
+        return f
+
     fns = {
-        "update": upd("pc"),
+        "fused": fused(),
+        "fused_edgeorder": fused_edge_order,
+        "fused_k0": fused(0),
+        "fused_k3": fused(3),
+        "fused_k7": fused(7),
+        "ps": fused(with_plan=False),
+        "ps_noprod": fused(with_plan=False, abl=1),
+        "ps_nomfma": fused(with_plan=False, abl=2),
+        "ps_noW": fused(with_plan=False, abl=4),
+        "ps_nosplit": fused(with_plan=False, abl=8),
+        "ps_noprod_noW": fused(with_plan=False, abl=5),
+        "ps_noprod_nosplit": fused(with_plan=False, abl=9),
+        "ps_noprod_noW_nosplit": fused(with_plan=False, abl=13),
+        "ps_noprod_nomfma": fused(with_plan=False, abl=3),
+        "ps_nomfma_noW": fused(with_plan=False, abl=6),
+        "fused_noprod": fused(abl=1),
+        "fused_noHres": fused(abl=32),
+        "fused_nostore": fused(abl=64),
+        "fused_noHres_nostore": fused(abl=96),
+        "fused_nomfma_noHres": fused(abl=34),
+        "fused_nomfma_noHres_nostore": fused(abl=98),
+        "fused_nomfma": fused(abl=2),
+        "update": upd("as"),
+        "update_pc": upd("pc"),
         "pc_noW": upd("pc", mode="2"),
         "pc_oneW": upd("pc", mode="4"),
         "pc_noW_oneW": upd("pc", mode="6"),
@@ -93,7 +141,7 @@ def main():
         med = statistics.median(r[0] for r in res[name])
         mn = min(r[1] for r in res[name])
         extra = ""
-        if name.startswith(("update", "abl", "pc_")):
+        if name.startswith(("update", "abl", "pc_", "fused", "ps")):
             extra = f"  {2 * E * h * h / (med * 1e-6) / 1e12:.1f} TF/s"
         else:
             rows = {"aggregate": E + V, "init_fused": 3 * E + V, "node_scatter": E + V, "pack": 0}[name]

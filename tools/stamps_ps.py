@@ -1,0 +1,46 @@
+"""Per-phase cycles of the persistent producer/consumer update (diagnostic build NT_PS_ABL=16).
+Usage: python tools/stamps_ps.py [mols]"""
+import ctypes
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from notorch_amd import _lib, kernels as K  # noqa: E402
+from notorch_amd.data.synth import make_batch  # noqa: E402
+
+mols = int(sys.argv[1]) if len(sys.argv) > 1 else 4096
+lib = _lib.load()
+fn = lib.nt_debug_ps_stamps
+fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+G = make_batch("qm9", mols, seed=0).collate("nodes").to("cuda")
+lay = G._nt_layout
+V, E, h = G.num_nodes, G.num_edges, 300
+H = torch.randn(E, h, device="cuda"); S = torch.randn(V, h, device="cuda")
+W = torch.randn(h, h, device="cuda") / 17; b = torch.randn(h, device="cuda")
+Wp = K.pack_weights(W); src = G.edge_index[0].contiguous(); rev = G.rev_index
+relu = K.act_code(torch.nn.ReLU())
+deg = int((lay.dst_ptr[1:] - lay.dst_ptr[:-1]).max())
+plan = K.tile_plan(lay.dst_ptr, E, deg)
+out = torch.empty_like(H); S2 = torch.empty_like(S)
+names = ["P finish", "P wait B3", "P gather", "P wait B1+B2", "C steps<kmid", "C wait B3",
+         "C steps>=kmid", "C wait B1", "C stage+B2"]
+for mode in ("fused", "unfused"):
+    buf = (ctypes.c_ulonglong * 11)()
+    for diag in ("0", "16"):
+        os.environ["NT_PS_ABL"] = diag
+        fn(buf, 1)
+        ts = []
+        for _ in range(5):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu,
+                                 plan=plan if mode == "fused" else None, perm=lay.dst_perm,
+                                 agg_act=relu, out=out, S_out=S2 if mode == "fused" else None)
+            e1.record(); torch.cuda.synchronize(); ts.append(e0.elapsed_time(e1) * 1e3)
+        fn(buf, 0)
+        print(f"{mode} diag={diag} launch us: {sorted(ts)[2]:.1f}")
+    pw, cw = max(buf[9], 1), max(buf[10], 1)
+    for i, n in enumerate(names):
+        print(f"  {n:16s} {buf[i] / (pw if i < 4 else cw):10.0f} cycles/wave/launch-set")
