@@ -9,7 +9,8 @@ collate semantics (rev offset by nodes).  A "step" = one forward of ChempropBloc
 with the collated graph (incl. its CSR layout) and the embedded features already resident in HBM.
 value = sum over ranks of E_r * depth * K / max over ranks of the timed seconds.
 
-Also reported: ``roofline`` for the dominant kernel (nt_dmpnn_update; per-launch duration from
+Also reported: ``roofline`` for the dominant kernel (nt_dmpnn_update_fused, or nt_dmpnn_update on
+the unfused path; per-launch duration from
 torch.cuda events recorded on the launch stream around every launch inside the timed region) and
 ``cpu_baseline`` (the oracle restatement on the host CPU, rank 0, N=1, bounded sample).
 """
@@ -64,6 +65,12 @@ def forward_bytes_flops(V, E, B, h, d, b=4):
     idx = 4 * ((3 * d + 2) * E + (d + 1) * (V + 1) + (B + 1))
     wts = d * (h * h + h) * b
     return rows + idx + wts, 2 * d * E * h * h
+
+
+def fused_bytes(V, E, h, b=4):
+    """Algorithmic bytes of ONE nt_dmpnn_update_fused launch (SURVEY §8(d) minimal model of a
+    layer: read H, read S, write H', write S' = 2E + 2V rows; int32 src/rev/perm; weights once)."""
+    return b * h * (2 * E + 2 * V) + 4 * 3 * E + (h * h + h) * b
 
 
 def update_bytes(V, E, h, b=4):
@@ -195,6 +202,13 @@ def main():
         elapsed = time.perf_counter() - t0
         _engine.UPDATE_EVENTS = None
 
+    from notorch_amd import kernels as K
+
+    lay = getattr(Gd, "_nt_layout", None)
+    used_fused = bool(
+        lay is not None and _engine._fused_enabled() and K.fused_supported(V, E, h)
+        and _engine.fused_plan(lay, V, E) is not None
+    )
     upd_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
     units, secs, rate = aggregate_throughput(E * depth * args.steps, elapsed, device=dev)
     if env.rank != 0:
@@ -204,13 +218,22 @@ def main():
 
     flops_upd = 2 * E * h * h
     upd_bytes = update_bytes(V, E, h)
-    variant = os.environ.get("NT_UPDATE_KERNEL", "x6")
-    x6 = variant.startswith("x") and h % 4 == 0 and 97 <= h <= 512
+    variant = os.environ.get("NT_UPDATE_KERNEL", "as")
+    fused = used_fused
     traffic = read_pmc_traffic(args.pmc_csv) if args.pmc_csv else None
-    if x6:
-        # bf16x6 fp32 emulation: 6 bf16 MFMA products per fp32 product on 32x32x16 tiles
-        # (K padded to 16, N to 32).  Binding roof = max(HBM bytes / 8 TB/s, bf16 flops / 2.5 PF).
-        kp, np_ = 16 * ((h + 15) // 16), 32 * ((h + 31) // 32)
+    if fused or (h % 4 == 0 and 97 <= h <= 512 and variant[0] in "axp"):
+        # bf16x6 fp32 emulation: 6 bf16 MFMA products per fp32 product.  Fused / as16 kernels run
+        # v_mfma_f32_16x16x32_bf16 (K padded to 32, N to 16); x6 runs 32x32x16 (K to 16, N to 32).
+        if fused or variant[0] == "a":
+            kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
+        else:
+            kp, np_ = 16 * ((h + 15) // 16), 32 * ((h + 31) // 32)
+        if fused:
+            upd_bytes = fused_bytes(V, E, h)
+            kname = ("nt_dmpnn_update_fused (update_ps_kernel: persistent producer/consumer, "
+                     "bf16x6 16x16x32 MFMA, aggregation of the next layer fused)")
+        else:
+            kname = f"nt_dmpnn_update (bf16x6 variant {variant})"
         bf16_flops = 6 * 2 * E * kp * np_
         t_hbm = upd_bytes / (PEAK_HBM_GBPS * 1e9)
         t_mfma = bf16_flops / (PEAK_BF16_MFMA_TFLOPS * 1e12)
@@ -219,14 +242,16 @@ def main():
             achieved, peak, unit = upd_bytes / (upd_ms * 1e-3) / 1e9, PEAK_HBM_GBPS, "GB/s"
         else:
             achieved, peak, unit = bf16_flops / (upd_ms * 1e-3) / 1e12, PEAK_BF16_MFMA_TFLOPS, "TFLOP/s"
-        kname = "nt_dmpnn_update (update_x6_kernel: bf16x6 fp32-emulating 32x32x16 MFMA + LDS-DMA gathers)"
         extra = {
             "mfma_bf16_tflops": bf16_flops / (upd_ms * 1e-3) / 1e12,
             "mfma_bf16_frac": bf16_flops / (upd_ms * 1e-3) / 1e12 / PEAK_BF16_MFMA_TFLOPS,
+            "hbm_frac": upd_bytes / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
             "fp32_equiv_tflops": flops_upd / (upd_ms * 1e-3) / 1e12,
             "t_min_us": max(t_hbm, t_mfma) * 1e6,
         }
+        x6 = True
     else:
+        x6 = False
         bound = "mfma"
         achieved, peak, unit = flops_upd / (upd_ms * 1e-3) / 1e12, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
         kname = "nt_dmpnn_update (fp32 16x16x4 MFMA, variant %s)" % variant
