@@ -50,6 +50,11 @@ int launch_update_ps(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
                      const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
                      float* S_out);  // u.Wp points at the as16 image
 
+// Persistent K-slice-ring variant (update_pk.hip): same contract as launch_update_ps.
+int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntiles,
+                     const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
+                     float* S_out);
+
 // Deeper-ring variant (S/H 2 chunks ahead); requires additionally NT <= 24.
 int launch_update_ring(const UpdateArgs& a);
 

@@ -542,18 +542,9 @@ __global__ void dst_sorted_kernel(const int32_t* __restrict__ dst_ptr, int64_t V
     for (int p = dst_ptr[v]; p < dst_ptr[v + 1]; ++p) dsts[p] = (int32_t)v;
 }
 
-int cu_count() {
-  static int n[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (n[dev] == 0) {
-    int c = 0;
-    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
-      c = 256;
-    n[dev] = c;
-  }
-  return n[dev];
-}
+}  // namespace
+int cu_count();
+namespace {
 
 template <int KS, int ACT, int AACT, bool SUMONLY>
 int launch_ps(const Args& a, hipStream_t stream) {
@@ -593,6 +584,19 @@ int dispatch_ps(const Args& a, int ks, hipStream_t stream, std::integer_sequence
 }
 
 }  // namespace
+
+int cu_count() {
+  static int n[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (n[dev] == 0) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || c <= 0)
+      c = 256;
+    n[dev] = c;
+  }
+  return n[dev];
+}
 
 bool ps_supported(int64_t h) { return h % 4 == 0 && h >= 4 && h <= 304; }
 
@@ -638,6 +642,10 @@ int launch_update_ps(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
   const bool fused = tile_ptr != nullptr;
   NT_REQUIRE(fused == (S_out != nullptr), NT_EINVAL, "S_out must be given exactly with a tile plan");
   NT_REQUIRE(!fused || (perm && dsts), NT_EINVAL, "fused mode needs perm and dst_sorted");
+  // kernel choice (A/B): NT_FUSED_KERNEL = pk (default: K-slice ring of pre-split A) | ps
+  const char* fk = getenv("NT_FUSED_KERNEL");
+  if (!(fk && fk[0] == 'p' && fk[1] == 's'))
+    return launch_update_pk(u, tile_ptr, ntiles, perm, dsts, reduce, aact, aalpha, S_out);
   Args a;
   a.H4 = (const float4*)u.H;
   a.S4 = (const float4*)u.S;

@@ -208,3 +208,41 @@ def test_block_paths_agree(fused, monkeypatch):
         out = blk.to(DEV)(Gd)
     assert_parity(out.edge_feats, ref_edge, FP32_NORM_TOL, f"edge fused={fused}")
     assert_parity(out.node_feats, ref_node, FP32_NORM_TOL, f"node fused={fused}")
+
+
+@pytest.mark.parametrize("variant", ["pk", "ps"])
+def test_fused_kernel_variants_and_no_spin_timeouts(variant, monkeypatch):
+    """Both persistent kernels (NT_FUSED_KERNEL) agree with the oracle; the pk ring's bounded spins
+    never gave up (nt_debug_pk_timeouts)."""
+    import ctypes
+
+    from notorch_amd import _lib
+
+    K = _K()
+    monkeypatch.setenv("NT_FUSED_KERNEL", variant)
+    lib = _lib.load()
+    fn = lib.nt_debug_pk_timeouts
+    fn.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.c_int]
+    cnt = ctypes.c_uint(0)
+    assert fn(ctypes.byref(cnt), 1) == 0
+    for h, n, rev_offset in ((300, 300, "nodes"), (300, 7, "edges"), (100, 50, "nodes"), (32, 20, "nodes")):
+        G = _graph("qm9", n, seed=h + n, rev_offset=rev_offset)
+        E, V = G.num_edges, G.num_nodes
+        g = torch.Generator().manual_seed(n)
+        H, S = torch.randn(E, h, generator=g), torch.randn(V, h, generator=g)
+        lin = nn.Linear(h, h)
+        W, b = lin.weight.detach(), lin.bias.detach()
+        _, perm, plan, zf = _plan(G)
+        relu = K.act_code(nn.ReLU())
+        args = (H.to(DEV), S.to(DEV), G.edge_index[0].to(DEV), G.rev_index.to(DEV),
+                K.pack_weights(W.to(DEV)), b.to(DEV))
+        Hn, Sn = K.dmpnn_update_fused(*args, residual=True, act=relu, plan=plan, perm=perm,
+                                      agg_act=relu, zero_fill=zf)
+        rH, rS = _ref_layer(G, H, S, W, b, True, torch.relu, "sum", torch.relu)
+        assert_parity(Hn, rH, FP32_NORM_TOL, f"{variant} H h={h} n={n}")
+        assert_parity(Sn, rS, FP32_NORM_TOL, f"{variant} S h={h} n={n}")
+        Hu, _ = K.dmpnn_update_fused(*args, residual=True, act=relu)
+        assert_parity(Hu, rH, FP32_NORM_TOL, f"{variant} unfused H h={h} n={n}")
+    torch.cuda.synchronize()
+    assert fn(ctypes.byref(cnt), 1) == 0
+    assert cnt.value == 0, "a pk ring spin gave up"

@@ -65,9 +65,11 @@ def main():
         K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=eplan, perm=ident, agg_act=relu,
                              out=out, S_out=S2)
 
-    def fused(kmid=None, with_plan=True, abl=0):
+    def fused(kmid=None, with_plan=True, abl=0, kern="pk", pkabl=0):
         def f():
+            os.environ["NT_FUSED_KERNEL"] = kern
             os.environ["NT_PS_ABL"] = str(abl)
+            os.environ["NT_PK_ABL"] = str(pkabl)
             if kmid is not None:
                 os.environ["NT_PS_KMID"] = str(kmid)
             else:
@@ -79,27 +81,35 @@ def main():
 
     fns = {
         "fused": fused(),
+        "fused_ps": fused(kern="ps"),
+        "pk_unfused": fused(with_plan=False),
+        "pk_noprod": fused(pkabl=1),
+        "pk_noprod_noW": fused(pkabl=3),
+        "pk_noprod_nores": fused(pkabl=5),
+        "pk_noprod_noW_nores": fused(pkabl=7),
+        "pk_noprod_nomfma": fused(pkabl=9),
+        "pk_noprod_all": fused(pkabl=15),
         "fused_edgeorder": fused_edge_order,
-        "fused_k0": fused(0),
-        "fused_k3": fused(3),
-        "fused_k7": fused(7),
-        "ps": fused(with_plan=False),
-        "ps_noprod": fused(with_plan=False, abl=1),
-        "ps_nomfma": fused(with_plan=False, abl=2),
-        "ps_noW": fused(with_plan=False, abl=4),
-        "ps_nosplit": fused(with_plan=False, abl=8),
-        "ps_noprod_noW": fused(with_plan=False, abl=5),
-        "ps_noprod_nosplit": fused(with_plan=False, abl=9),
-        "ps_noprod_noW_nosplit": fused(with_plan=False, abl=13),
-        "ps_noprod_nomfma": fused(with_plan=False, abl=3),
-        "ps_nomfma_noW": fused(with_plan=False, abl=6),
-        "fused_noprod": fused(abl=1),
-        "fused_noHres": fused(abl=32),
-        "fused_nostore": fused(abl=64),
-        "fused_noHres_nostore": fused(abl=96),
-        "fused_nomfma_noHres": fused(abl=34),
-        "fused_nomfma_noHres_nostore": fused(abl=98),
-        "fused_nomfma": fused(abl=2),
+        "fused_k0": fused(0, kern="ps"),
+        "fused_k3": fused(3, kern="ps"),
+        "fused_k7": fused(7, kern="ps"),
+        "ps": fused(with_plan=False, kern="ps"),
+        "ps_noprod": fused(with_plan=False, abl=1, kern="ps"),
+        "ps_nomfma": fused(with_plan=False, abl=2, kern="ps"),
+        "ps_noW": fused(with_plan=False, abl=4, kern="ps"),
+        "ps_nosplit": fused(with_plan=False, abl=8, kern="ps"),
+        "ps_noprod_noW": fused(with_plan=False, abl=5, kern="ps"),
+        "ps_noprod_nosplit": fused(with_plan=False, abl=9, kern="ps"),
+        "ps_noprod_noW_nosplit": fused(with_plan=False, abl=13, kern="ps"),
+        "ps_noprod_nomfma": fused(with_plan=False, abl=3, kern="ps"),
+        "ps_nomfma_noW": fused(with_plan=False, abl=6, kern="ps"),
+        "fused_noprod": fused(abl=1, kern="ps"),
+        "fused_noHres": fused(abl=32, kern="ps"),
+        "fused_nostore": fused(abl=64, kern="ps"),
+        "fused_noHres_nostore": fused(abl=96, kern="ps"),
+        "fused_nomfma_noHres": fused(abl=34, kern="ps"),
+        "fused_nomfma_noHres_nostore": fused(abl=98, kern="ps"),
+        "fused_nomfma": fused(abl=2, kern="ps"),
         "update": upd("as"),
         "update_pc": upd("pc"),
         "pc_noW": upd("pc", mode="2"),
@@ -141,7 +151,7 @@ def main():
         med = statistics.median(r[0] for r in res[name])
         mn = min(r[1] for r in res[name])
         extra = ""
-        if name.startswith(("update", "abl", "pc_", "fused", "ps")):
+        if name.startswith(("update", "abl", "pc_", "fused", "ps", "pk")):
             extra = f"  {2 * E * h * h / (med * 1e-6) / 1e12:.1f} TF/s"
         else:
             rows = {"aggregate": E + V, "init_fused": 3 * E + V, "node_scatter": E + V, "pack": 0}[name]
