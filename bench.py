@@ -230,8 +230,9 @@ def main():
             kp, np_ = 16 * ((h + 15) // 16), 32 * ((h + 31) // 32)
         if fused:
             upd_bytes = fused_bytes(V, E, h)
-            kname = ("nt_dmpnn_update_fused (update_ps_kernel: persistent producer/consumer, "
-                     "bf16x6 16x16x32 MFMA, aggregation of the next layer fused)")
+            fk = os.environ.get("NT_FUSED_KERNEL", "pk")
+            kname = ("nt_dmpnn_update_fused (update_%s_kernel: persistent producer/consumer, "
+                     "bf16x6 16x16x32 MFMA, aggregation of the next layer fused)" % ("ps" if fk == "ps" else "pk"))
         else:
             kname = f"nt_dmpnn_update (bf16x6 variant {variant})"
         bf16_flops = 6 * 2 * E * kp * np_
