@@ -153,6 +153,44 @@ NT_API int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* sr
                                  int reduce, int agg_act, float agg_alpha, int dtype, void* H_out,
                                  void* S_out, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Backward (training through ChempropBlock, lightning_models/model.py:224-241).  The reference's
+ * backward is ATen autograd of chemprop.py:28-43,81-88 (index_backward = index_add, scatter_add
+ * backward = gather, addmm backward = two mm).  These replace the gather/scatter/element-wise parts;
+ * the two dense products per layer (dA = G W, dW = G^T A) are library GEMMs on the same stream.
+ * --------------------------------------------------------------------------------------------- */
+
+/*
+ * Layer message, recomputed for the weight gradient (chemprop.py:40):
+ *   A[e] = S[src[e]] - act(H[rev[e]])
+ */
+NT_API int nt_dmpnn_message(const void* H, const void* S, const int64_t* src, const int64_t* rev,
+                            int64_t V, int64_t E, int64_t h, int act, float act_alpha, int dtype,
+                            void* A_out, void* stream);
+
+/*
+ * Gradient of one layer's input hidden state (backward of chemprop.py:37-40 and residual.py:28):
+ *   G_out[e] = (residual ? G[e] : 0)
+ *            + act'(H[e]) * (dS[dst[e]] / c(dst[e]) - sum_{j in [rev_ptr[e], rev_ptr[e+1])} dA[rev_perm[j]])
+ * G = dL/dH_{l+1}; H = H_l; dA = G W; dS = nt_segment_reduce(dA, src CSR, sum);
+ * (rev_ptr, rev_perm) = nt_csr_build(rev_index, E, E); c(v) = max(in-degree, 1) for
+ * reduce = NT_MEAN (dst_ptr required), 1 for NT_SUM.  max/min are not covered (NT_EUNSUPPORTED).
+ */
+NT_API int nt_dmpnn_edge_backward(const void* G, const void* H, const void* dA, const void* dS,
+                                  const int64_t* dst, const int32_t* rev_ptr, const int32_t* rev_perm,
+                                  const int32_t* dst_ptr, int64_t V, int64_t E, int64_t h,
+                                  int residual, int act, float act_alpha, int reduce, int dtype,
+                                  void* G_out, void* stream);
+
+/*
+ * Row gather with optional base and mean scaling (backward of a sum/mean scatter):
+ *   out[i] = (base ? base[i] : 0) + X[idx[i]] / (seg_ptr ? max(seg_ptr[idx+1] - seg_ptr[idx], 1) : 1)
+ * Used for dL/dH_d += dnode[dst] (chemprop.py:86) and the Sum/Mean readout backward
+ * (agg.py:23-38, idx = batch_node_index, seg_ptr = molecule CSR for mean).
+ */
+NT_API int nt_gather_rows(const void* base, const void* X, const int64_t* idx, const int32_t* seg_ptr,
+                          int64_t n, int64_t nseg, int64_t h, int dtype, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,247 @@
+// Backward of the D-MPNN block: the gather/scatter/element-wise parts as HIP
+// kernels; the two dense products per layer (dA = G W, dW = G^T A) are plain library GEMMs issued by
+// the host on the same stream.
+//
+// Forward of layer l (chemprop.py:28-43, residual.py:27-28), per directed edge e:
+//   M = act(H_l);  S_l[v] = R_{e->v} M[e];  A_l[e] = S_l[src e] - M[rev e];  H_{l+1} = H_l + A_l W^T + b
+// Backward with G = dL/dH_{l+1} (R = sum or mean; c_v = max(in-degree v, 1) for mean, 1 for sum):
+//   dA = G W;  dS[v] = sum_{e: src e = v} dA[e]                         (nt_segment_reduce, src CSR)
+//   dL/dH_l[e] = (residual ? G[e] : 0)
+//              + act'(H_l[e]) * (dS[dst e] / c_{dst e} - sum_{e': rev e' = e} dA[e'])   (this file)
+// The rev term is a scatter by rev_index; the reference collate's rev_index is not a permutation
+// (graph.py:200 offsets it by nodes), so it is read through the rev CSR (ascending e').
+//
+// Kernels (all HBM-bound streaming gathers, one lane per (row, 16-B column chunk) so every row is
+// read as whole contiguous pieces):
+//   nt_dmpnn_message        A[e] = S[src e] - act(H[rev e])                3 rows / edge
+//   nt_dmpnn_edge_backward  the dL/dH_l line above                         5 rows / edge
+//   nt_gather_rows          out[i] = base[i] + X[idx i] / c_{idx i}        3 rows / row
+//                           (dnode[dst] into dL/dH_d, chemprop.py:86; readout backward, agg.py:23-38)
+#include "common.hpp"
+
+namespace nt {
+
+__device__ __forceinline__ float act_grad(float x, int act, float alpha) {
+  switch (act) {
+    case NT_ACT_RELU: return x > 0.f ? 1.f : 0.f;
+    case NT_ACT_LEAKY_RELU: return x > 0.f ? 1.f : alpha;
+    case NT_ACT_ELU: return x > 0.f ? 1.f : alpha * expf(x);
+    case NT_ACT_GELU: {
+      const float cdf = 0.5f * (1.f + erff(x * 0.70710678118654752f));
+      const float pdf = 0.39894228040143268f * expf(-0.5f * x * x);
+      return cdf + x * pdf;
+    }
+    case NT_ACT_SILU: {
+      const float s = 1.f / (1.f + expf(-x));
+      return s * (1.f + x * (1.f - s));
+    }
+    case NT_ACT_TANH: {
+      const float t = tanhf(x);
+      return 1.f - t * t;
+    }
+    case NT_ACT_SIGMOID: {
+      const float s = 1.f / (1.f + expf(-x));
+      return s * (1.f - s);
+    }
+    default: return 1.f;
+  }
+}
+
+template <int ACT>
+__device__ __forceinline__ float act_grad_t(float x, int act, float alpha) {
+  if constexpr (ACT == NT_ACT_IDENTITY) return 1.f;
+  else if constexpr (ACT == NT_ACT_RELU) return x > 0.f ? 1.f : 0.f;
+  else return act_grad(x, act, alpha);
+}
+
+// ---- element-type helpers: the same kernel body runs on float4 (h % 4 == 0) or float ----
+__device__ __forceinline__ float4 vfill(float4, float s) { return make_float4(s, s, s, s); }
+__device__ __forceinline__ float vfill(float, float s) { return s; }
+__device__ __forceinline__ float4 vmul(float4 a, float4 b) {
+  return make_float4(a.x * b.x, a.y * b.y, a.z * b.z, a.w * b.w);
+}
+__device__ __forceinline__ float vmul(float a, float b) { return a * b; }
+template <int ACT>
+__device__ __forceinline__ float4 vact(float4 v, int act, float alpha) { return act4_t<ACT>(v, act, alpha); }
+template <int ACT>
+__device__ __forceinline__ float vact(float v, int act, float alpha) { return act_t<ACT>(v, act, alpha); }
+template <int ACT>
+__device__ __forceinline__ float4 vgrad(float4 v, int act, float alpha) {
+  return make_float4(act_grad_t<ACT>(v.x, act, alpha), act_grad_t<ACT>(v.y, act, alpha),
+                     act_grad_t<ACT>(v.z, act, alpha), act_grad_t<ACT>(v.w, act, alpha));
+}
+template <int ACT>
+__device__ __forceinline__ float vgrad(float v, int act, float alpha) { return act_grad_t<ACT>(v, act, alpha); }
+
+// ------------------------------------------------------------------------------ message
+template <typename T, int ACT>
+__global__ void __launch_bounds__(256) message_kernel(const T* __restrict__ H, const T* __restrict__ S,
+                                                      const int64_t* __restrict__ src,
+                                                      const int64_t* __restrict__ rev, int64_t E,
+                                                      int64_t hw, int act, float alpha,
+                                                      T* __restrict__ A) {
+  const int64_t total = E * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / hw, c = t - e * hw;
+    A[t] = S[src[e] * hw + c] - vact<ACT>(H[rev[e] * hw + c], act, alpha);
+  }
+}
+
+// ------------------------------------------------------------------------------ edge backward
+template <typename T, int ACT, bool MEAN>
+__global__ void __launch_bounds__(256) edge_backward_kernel(
+    const T* __restrict__ G, const T* __restrict__ H, const T* __restrict__ dA,
+    const T* __restrict__ dS, const int64_t* __restrict__ dst, const int32_t* __restrict__ rev_ptr,
+    const int32_t* __restrict__ rev_perm, const int32_t* __restrict__ dst_ptr, int64_t E,
+    int64_t hw, int residual, int act, float alpha, T* __restrict__ Gout) {
+  const int64_t total = E * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / hw, c = t - e * hw;
+    const int64_t v = dst[e];
+    T dm = dS[v * hw + c];
+    if constexpr (MEAN) {
+      const int cnt = dst_ptr[v + 1] - dst_ptr[v];
+      dm = vmul(dm, vfill(dm, 1.f / (float)(cnt > 1 ? cnt : 1)));
+    }
+    const int32_t b = rev_ptr[e], en = rev_ptr[e + 1];
+    for (int32_t j = b; j < en; ++j) dm = dm - dA[(int64_t)rev_perm[j] * hw + c];
+    T g = vmul(vgrad<ACT>(H[t], act, alpha), dm);
+    if (residual) g = g + G[t];
+    Gout[t] = g;
+  }
+}
+
+// ------------------------------------------------------------------------------ gather rows
+template <typename T, bool MEAN>
+__global__ void __launch_bounds__(256) gather_rows_kernel(const T* __restrict__ base,
+                                                          const T* __restrict__ X,
+                                                          const int64_t* __restrict__ idx,
+                                                          const int32_t* __restrict__ seg_ptr,
+                                                          int64_t n, int64_t hw, T* __restrict__ out) {
+  const int64_t total = n * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / hw, c = t - i * hw;
+    const int64_t s = idx[i];
+    T x = X[s * hw + c];
+    if constexpr (MEAN) {
+      const int cnt = seg_ptr[s + 1] - seg_ptr[s];
+      x = vmul(x, vfill(x, 1.f / (float)(cnt > 1 ? cnt : 1)));
+    }
+    out[t] = base ? base[t] + x : x;
+  }
+}
+
+static bool valid_act(int a) { return a >= NT_ACT_IDENTITY && a <= NT_ACT_SIGMOID; }
+
+#define NT_BW_DISPATCH_ACT(ACT, LAUNCH)                                          \
+  do {                                                                           \
+    if ((ACT) == NT_ACT_IDENTITY) { constexpr int A_ = NT_ACT_IDENTITY; LAUNCH; } \
+    else if ((ACT) == NT_ACT_RELU) { constexpr int A_ = NT_ACT_RELU; LAUNCH; }    \
+    else { constexpr int A_ = -1; LAUNCH; }                                      \
+  } while (0)
+
+}  // namespace nt
+
+extern "C" int nt_dmpnn_message(const void* H, const void* S, const int64_t* src, const int64_t* rev,
+                                int64_t V, int64_t E, int64_t h, int act, float act_alpha, int dtype,
+                                void* A_out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented");
+  NT_REQUIRE(valid_act(act), NT_EINVAL, "bad act code");
+  NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  if (E == 0) return NT_OK;
+  NT_REQUIRE(H && S && src && rev && A_out, NT_EINVAL, "NULL pointer");
+  hipStream_t stream = as_stream(stream_);
+  if (h % 4 == 0 && aligned16(H) && aligned16(S) && aligned16(A_out)) {
+    const int64_t hw = h / 4;
+    NT_BW_DISPATCH_ACT(act, (message_kernel<float4, A_><<<grid_for(E * hw, 256, 256 * 32), 256, 0, stream>>>(
+                                (const float4*)H, (const float4*)S, src, rev, E, hw, act, act_alpha,
+                                (float4*)A_out)));
+  } else {
+    NT_BW_DISPATCH_ACT(act, (message_kernel<float, A_><<<grid_for(E * h, 256, 256 * 32), 256, 0, stream>>>(
+                                (const float*)H, (const float*)S, src, rev, E, h, act, act_alpha,
+                                (float*)A_out)));
+  }
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+extern "C" int nt_dmpnn_edge_backward(const void* G, const void* H, const void* dA, const void* dS,
+                                      const int64_t* dst, const int32_t* rev_ptr,
+                                      const int32_t* rev_perm, const int32_t* dst_ptr, int64_t V,
+                                      int64_t E, int64_t h, int residual, int act, float act_alpha,
+                                      int reduce, int dtype, void* G_out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented");
+  NT_REQUIRE(valid_act(act), NT_EINVAL, "bad act code");
+  NT_REQUIRE(reduce == NT_SUM || reduce == NT_MEAN, NT_EUNSUPPORTED,
+             "edge backward covers reduce = sum | mean");
+  NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  if (E == 0) return NT_OK;
+  NT_REQUIRE(H && dA && dS && dst && rev_ptr && rev_perm && G_out, NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(!residual || G, NT_EINVAL, "residual needs G");
+  NT_REQUIRE(reduce != NT_MEAN || dst_ptr, NT_EINVAL, "mean needs the dst CSR");
+  hipStream_t stream = as_stream(stream_);
+  const bool mean = reduce == NT_MEAN;
+  if (h % 4 == 0 && aligned16(H) && aligned16(dA) && aligned16(dS) && aligned16(G_out) &&
+      (!residual || aligned16(G))) {
+    const int64_t hw = h / 4;
+    const int grid = grid_for(E * hw, 256, 256 * 32);
+#define NT_EB_LAUNCH(MEAN_)                                                                       \
+  NT_BW_DISPATCH_ACT(act, (edge_backward_kernel<float4, A_, MEAN_><<<grid, 256, 0, stream>>>(     \
+                              (const float4*)G, (const float4*)H, (const float4*)dA,              \
+                              (const float4*)dS, dst, rev_ptr, rev_perm, dst_ptr, E, hw, residual, \
+                              act, act_alpha, (float4*)G_out)))
+    if (mean) NT_EB_LAUNCH(true); else NT_EB_LAUNCH(false);
+#undef NT_EB_LAUNCH
+  } else {
+    const int grid = grid_for(E * h, 256, 256 * 32);
+#define NT_EB_LAUNCH(MEAN_)                                                                     \
+  NT_BW_DISPATCH_ACT(act, (edge_backward_kernel<float, A_, MEAN_><<<grid, 256, 0, stream>>>(    \
+                              (const float*)G, (const float*)H, (const float*)dA, (const float*)dS, \
+                              dst, rev_ptr, rev_perm, dst_ptr, E, h, residual, act, act_alpha,   \
+                              (float*)G_out)))
+    if (mean) NT_EB_LAUNCH(true); else NT_EB_LAUNCH(false);
+#undef NT_EB_LAUNCH
+  }
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+extern "C" int nt_gather_rows(const void* base, const void* X, const int64_t* idx,
+                              const int32_t* seg_ptr, int64_t n, int64_t nseg, int64_t h, int dtype,
+                              void* out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented");
+  NT_REQUIRE(n >= 0 && nseg >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  if (n == 0) return NT_OK;
+  NT_REQUIRE(X && idx && out, NT_EINVAL, "NULL pointer");
+  hipStream_t stream = as_stream(stream_);
+  const bool mean = seg_ptr != nullptr;
+  if (h % 4 == 0 && aligned16(X) && aligned16(out) && (!base || aligned16(base))) {
+    const int64_t hw = h / 4;
+    const int grid = grid_for(n * hw, 256, 256 * 32);
+    if (mean)
+      gather_rows_kernel<float4, true><<<grid, 256, 0, stream>>>(
+          (const float4*)base, (const float4*)X, idx, seg_ptr, n, hw, (float4*)out);
+    else
+      gather_rows_kernel<float4, false><<<grid, 256, 0, stream>>>(
+          (const float4*)base, (const float4*)X, idx, seg_ptr, n, hw, (float4*)out);
+  } else {
+    const int grid = grid_for(n * h, 256, 256 * 32);
+    if (mean)
+      gather_rows_kernel<float, true><<<grid, 256, 0, stream>>>(
+          (const float*)base, (const float*)X, idx, seg_ptr, n, h, (float*)out);
+    else
+      gather_rows_kernel<float, false><<<grid, 256, 0, stream>>>(
+          (const float*)base, (const float*)X, idx, seg_ptr, n, h, (float*)out);
+  }
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}

@@ -57,6 +57,8 @@ class DeviceLayout:
     # fused-update tile plan (tile_ptr, ntiles, dst_sorted, zero_fill), derived lazily on the device
     # by notorch_amd.nn.gnn._engine.fused_plan; False = not available (in-degree > 32)
     plan: object = None
+    # backward CSRs (src -> nodes, rev_index -> edges), built lazily by _engine.backward_layout
+    bwd: object = None
 
     def to(self, device, edge_index: Tensor, batch_node_index: Optional[Tensor]) -> "DeviceLayout":
         mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731

@@ -14,12 +14,20 @@ d + 1 launches (+ one nt_dmpnn_pack_weight per distinct weight, cached).  Otherw
 
     nt_dmpnn_init; for l: nt_dmpnn_update, nt_segment_reduce; nt_segment_reduce (node)   2 + 2d launches
 
-Backward (training) is, for this round, a recompute of the same math in PyTorch device ops
-followed by autograd (``_torch_block``) — correct for every option, not yet a kernel (SURVEY §8(f)
-row 1).  The forward of a training step still runs the HIP kernels.
+Backward (training), reduce in {sum, mean}: the forward keeps (H_l, S_l) of
+every layer; per layer, last to first (csrc/backward.hip):
+
+    nt_dmpnn_message        A_l = S_l[src] - act(H_l)[rev]                   (recomputed, for dW)
+    GEMM (library)          dW_l = G^T A_l,  db_l = colsum(G),  dA = G W_l
+    nt_segment_reduce       dS = scatter_sum(dA, src)            (src CSR, cached on the layout)
+    nt_dmpnn_edge_backward  G <- G + act'(H_l) * (dS[dst] / c - scatter_sum(dA, rev))  (rev CSR)
+
+then dXe = G, dXv = scatter_sum(G, src).  max/min reductions recompute the block in PyTorch device
+ops and run autograd (``_torch_block``).
 """
 from __future__ import annotations
 
+import os
 import weakref
 from typing import Optional, Sequence
 
@@ -120,8 +128,6 @@ def fused_plan(lay: DeviceLayout, V: int, E: int):
 
 
 def _fused_enabled() -> bool:
-    import os
-
     return os.environ.get("NT_FUSED", "1") != "0"
 
 
@@ -162,24 +168,27 @@ def block_forward(
     reduce: str,
     residual: bool,
     keep_states: bool = False,
-) -> tuple[Tensor, Tensor, list[Tensor]]:
-    """Run the fused kernel sequence; returns (node, H_d, [H_0..H_d] if keep_states)."""
+) -> tuple[Tensor, Tensor, list[tuple[Tensor, Tensor]]]:
+    """Run the kernel sequence; returns (node, H_d, states) with states = [(H_l, S_l)] for
+    l = 0..d-1 (each layer's input hidden state and its aggregation) if keep_states, else []."""
     V = Xv.shape[0]
     d = len(weights)
     if d == 0:
         H, _ = K.dmpnn_init(Xv, Xe, src)
         node = K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=_IDENTITY)
-        return node, H, [H]
+        return node, H, []
     Wps = pack_layer_weights(weights)
     H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
     E, h = H.shape
     plan = fused_plan(lay, V, E) if _fused_enabled() and K.fused_supported(V, E, h) else None
     if plan is not None:
         return _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual, keep_states)
-    states = [H]
+    states = []
     spare: Optional[Tensor] = None  # ping-pong buffer when states are not kept
     timer = UPDATE_EVENTS
     for l in range(d):
+        if keep_states:
+            states.append((H, S))
         if timer is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
@@ -191,10 +200,9 @@ def block_forward(
             ev[1].record()
             timer.append(ev)
         if l < d - 1:
-            K.segment_reduce(Hn, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=act, out=S)
-        if keep_states:
-            states.append(Hn)
-        else:
+            S = K.segment_reduce(Hn, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=act,
+                                 out=None if keep_states else S)
+        if not keep_states:
             spare = H  # H_l is dead once H_{l+1} exists: reuse its buffer for H_{l+2}
         H = Hn
     node = K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=_IDENTITY)
@@ -204,12 +212,14 @@ def block_forward(
 def _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual, keep_states):
     tile_ptr, ntiles, dsts, zero_fill = plan
     d = len(Wps)
-    states = [H]
+    states = []
     spare_H: Optional[Tensor] = None
     spare_S: Optional[Tensor] = None
     timer = UPDATE_EVENTS
     for l in range(d):
         last = l == d - 1
+        if keep_states:
+            states.append((H, S))
         if timer is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
@@ -222,11 +232,9 @@ def _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual
         if timer is not None:
             ev[1].record()
             timer.append(ev)
-        if keep_states:
-            states.append(Hn)
-        else:
+        if not keep_states:
             spare_H = H
-        spare_S = S
+            spare_S = S
         H, S = Hn, Sn
     return S, H, states
 
@@ -254,27 +262,105 @@ def _torch_block(Xv, Xe, edge_index, rev, weights, biases, act_mod, reduce, resi
     return _torch_scatter(H, dst, V, reduce), H
 
 
+def backward_layout(lay: DeviceLayout, src: Tensor, rev: Tensor, V: int, E: int) -> tuple:
+    """(src_ptr, src_perm, rev_ptr, rev_perm): the CSRs of the two gathers' transposes (scatter by
+    src into nodes, scatter by rev_index into edges), built once per graph and cached on its layout."""
+    bwd = getattr(lay, "bwd", None)
+    # keyed on the storage (src is a fresh view of edge_index[0] on every call) and the rev tensor
+    key = (src.data_ptr(), src.numel(), rev.data_ptr(), rev.numel(), V)
+    if bwd is None or bwd[0] != key or bwd[1] is not rev:
+        src_ptr, src_perm = K.csr_build(src, V, check_bounds=False)
+        rev_ptr, rev_perm = K.csr_build(rev, E, check_bounds=False)
+        bwd = (key, rev, src_ptr, src_perm, rev_ptr, rev_perm)
+        lay.bwd = bwd
+    return bwd[2:]
+
+
+def _weight_grad(G: Tensor, A: Tensor) -> Tensor:
+    """dW = G^T A (h x h, reduction over all E edges).  A single GEMM has only (h/32)(h/64) output
+    tiles, far too few for 256 CUs, so the edge dimension is split k ways into a batched GEMM
+    whose k partial products are then summed (split-K)."""
+    E, h = G.shape
+    k = min(64, E // 2048)
+    if k < 2:
+        return torch.mm(G.t(), A)
+    rows = E // k
+    Eb = rows * k
+    dW = torch.bmm(G[:Eb].view(k, rows, h).transpose(1, 2), A[:Eb].view(k, rows, h)).sum(0)
+    if Eb < E:
+        dW.addmm_(G[Eb:].t(), A[Eb:])
+    return dW
+
+
+def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, residual, V, need_x):
+    """Kernel backward of block_forward for reduce in {sum, mean} (see csrc/backward.hip).
+    Returns (dXv, dXe, [dW_l], [db_l])."""
+    E, h = states[0][0].shape if states else dH.shape
+    src_ptr, src_perm, rev_ptr, rev_perm = backward_layout(lay, src, rev, V, E)
+    mean_ptr = lay.dst_ptr if reduce == "mean" else None
+    if dH is None:
+        G = torch.zeros(E, h, dtype=torch.float32, device=src.device)
+    else:
+        G = dH.contiguous()
+    if dnode is not None:
+        G = K.gather_rows(dnode.contiguous(), dst, base=G, seg_ptr=mean_ptr)
+    d = len(weights)
+    dWs: list = [None] * d
+    dbs: list = [None] * d
+    for l in range(d - 1, -1, -1):
+        H_l, S_l = states[l]
+        W = weights[l].detach()
+        A = K.dmpnn_message(H_l, S_l, src, rev, act=act)
+        dWs[l] = _weight_grad(G, A)
+        dbs[l] = G.sum(0)
+        del A
+        dA = torch.mm(G, W)
+        dS = K.segment_reduce(dA, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY)
+        G = K.dmpnn_edge_backward(G, H_l, dA, dS, dst, rev_ptr, rev_perm, lay.dst_ptr,
+                                  residual=residual, act=act, reduce=reduce)
+    dXv = K.segment_reduce(G, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY) if need_x[0] else None
+    return dXv, G if need_x[1] else None, dWs, dbs
+
+
 class ChempropBlockFunction(torch.autograd.Function):
-    """Kernel forward, recompute-in-torch backward (interim; see module docstring)."""
+    """Kernel forward; kernel backward for reduce in {sum, mean} (gather/scatter/element-wise HIP
+    kernels + two library GEMMs per layer), recompute-in-torch-device-ops backward for max/min."""
 
     @staticmethod
     def forward(ctx, Xv, Xe, edge_index, rev, lay, act_mod, act, reduce, residual, nlayers, *params):
         weights = list(params[:nlayers])
         biases = list(params[nlayers:])
         src = edge_index[0].contiguous()
-        node, H, _ = block_forward(Xv, Xe, src, rev, lay, weights, biases, act, reduce, residual)
-        ctx.save_for_backward(Xv, Xe, edge_index, rev, *[p if p is not None else torch.empty(0) for p in params])
-        ctx.cfg = (act_mod, reduce, residual, nlayers, [p is None for p in params])
+        kernel_bwd = reduce in ("sum", "mean") and os.environ.get("NT_BWD", "kernel") != "torch"
+        node, H, states = block_forward(Xv, Xe, src, rev, lay, weights, biases, act, reduce, residual,
+                                        keep_states=kernel_bwd)
+        flat = [t for hs in states for t in hs]
+        ctx.save_for_backward(Xv, Xe, edge_index, rev,
+                              *[p if p is not None else torch.empty(0) for p in params], *flat)
+        ctx.cfg = (act_mod, act, reduce, residual, nlayers, [p is None for p in params], lay, kernel_bwd)
         return node, H
 
     @staticmethod
     def backward(ctx, dnode, dH):
-        act_mod, reduce, residual, nlayers, is_none = ctx.cfg
-        Xv, Xe, edge_index, rev, *params = ctx.saved_tensors
-        params = [None if n else p for p, n in zip(params, is_none)]
+        act_mod, act, reduce, residual, nlayers, is_none, lay, kernel_bwd = ctx.cfg
+        Xv, Xe, edge_index, rev, *rest = ctx.saved_tensors
+        nparams = len(is_none)
+        params = [None if n else p for p, n in zip(rest[:nparams], is_none)]
         need = ctx.needs_input_grad
+        if kernel_bwd:
+            flat = rest[nparams:]
+            states = [(flat[2 * i], flat[2 * i + 1]) for i in range(nlayers)]
+            src = edge_index[0].contiguous()
+            dst = edge_index[1].contiguous()
+            dXv, dXe, dWs, dbs = block_backward(
+                dnode, dH, states, params[:nlayers], src, dst, rev, lay, act, reduce, residual,
+                Xv.shape[0], (need[0], need[1]),
+            )
+            res_params = [dW if need[10 + i] else None for i, dW in enumerate(dWs)]
+            res_params += [None if p is None or not need[10 + nlayers + i] else dbs[i]
+                           for i, p in enumerate(params[nlayers:])]
+            return (dXv, dXe, None, None, None, None, None, None, None, None, *res_params)
         with torch.enable_grad():
-            leaves = []
             Xv_ = Xv.detach().requires_grad_(need[0])
             Xe_ = Xe.detach().requires_grad_(need[1])
             ps = [None if p is None else p.detach().requires_grad_(True) for p in params]
@@ -303,13 +389,16 @@ class ReadoutFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, X, mol_ptr, mol_perm, B, reduce, batch_node_index):
         ctx.save_for_backward(X, batch_node_index)
-        ctx.cfg = (B, reduce)
+        ctx.cfg = (B, reduce, mol_ptr)
         return K.segment_reduce(X, mol_ptr, mol_perm, B, reduce=reduce, act=_IDENTITY)
 
     @staticmethod
     def backward(ctx, dout):
         X, bni = ctx.saved_tensors
-        B, reduce = ctx.cfg
+        B, reduce, mol_ptr = ctx.cfg
+        if reduce in ("sum", "mean"):  # dX[v] = dout[batch v] (/ count for mean): one gather kernel
+            dX = K.gather_rows(dout.contiguous(), bni, seg_ptr=mol_ptr if reduce == "mean" else None)
+            return dX, None, None, None, None, None
         with torch.enable_grad():
             X_ = X.detach().requires_grad_(True)
             out = _torch_scatter(X_, bni, B, reduce)

@@ -21,7 +21,7 @@ def test_header_declares_the_boundary():
         "nt_abi_version", "nt_last_error", "nt_csr_workspace_bytes", "nt_csr_build",
         "nt_dmpnn_init", "nt_segment_reduce", "nt_dmpnn_packed_weight_bytes",
         "nt_dmpnn_pack_weight", "nt_dmpnn_update", "nt_dmpnn_tile_count", "nt_dmpnn_tile_plan",
-        "nt_dmpnn_update_fused",
+        "nt_dmpnn_update_fused", "nt_dmpnn_message", "nt_dmpnn_edge_backward", "nt_gather_rows",
     }
 
 
@@ -52,6 +52,14 @@ def test_abi_version_and_errors_without_gpu():
     rc = lib.nt_segment_reduce(None, None, None, 4, 8, 0, 0, 0.0, 1, None, None)
     assert rc == 3  # NT_EUNSUPPORTED: bf16 segment reduce not implemented
     rc = lib.nt_csr_build(None, -1, 3, None, None, None, 0, None, None)
+    assert rc == 1
+    # backward entry points validate before touching the device
+    rc = lib.nt_dmpnn_edge_backward(None, None, None, None, None, None, None, None, 4, 8, 16, 1, 1,
+                                    0.0, 2, 0, None, None)
+    assert rc == 3 and b"sum | mean" in lib.nt_last_error()  # max/min backward: not a kernel
+    rc = lib.nt_dmpnn_message(None, None, None, None, 4, 8, 16, 99, 0.0, 0, None, None)
+    assert rc == 1
+    rc = lib.nt_gather_rows(None, None, None, None, -1, 4, 8, 0, None, None)
     assert rc == 1
 
 

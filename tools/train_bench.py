@@ -1,0 +1,69 @@
+"""Training-step timing of ChempropBlock + Sum readout (forward + backward) at config 2:
+kernel backward (default) vs the recompute-in-torch backward (NT_BWD=torch).
+Usage: python tools/train_bench.py [--mols 4096] [--h 300] [--depth 3] [--steps 20]"""
+import argparse
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from notorch_amd.data.synth import make_batch  # noqa: E402
+from notorch_amd.nn import ChempropBlock, Sum  # noqa: E402
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--mols", type=int, default=4096)
+    p.add_argument("--h", type=int, default=300)
+    p.add_argument("--depth", type=int, default=3)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--modes", default="kernel,torch")
+    a = p.parse_args()
+    G = make_batch("qm9", a.mols, seed=0).collate("nodes")
+    torch.manual_seed(0)
+    ev = torch.nn.EmbeddingBag(42, a.h, mode="sum")
+    ee = torch.nn.EmbeddingBag(13, a.h, mode="sum")
+    with torch.no_grad():
+        Xv, Xe = ev(G.node_feats), ee(G.edge_feats)
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to("cuda")
+    blk = ChempropBlock(a.h, depth=a.depth).cuda().train()
+    ro = Sum()
+    Xv_d = Gd.node_feats.requires_grad_(True)
+    Xe_d = Gd.edge_feats.requires_grad_(True)
+    E = G.num_edges
+
+    def step():
+        blk.zero_grad(set_to_none=True)
+        Xv_d.grad = Xe_d.grad = None
+        out = blk(Gd.update(node_feats=Xv_d, edge_feats=Xe_d))
+        ro(out).pow(2).sum().backward()
+
+    def fwd():
+        with torch.no_grad():
+            ro(blk(Gd))
+
+    res = {}
+    for mode in a.modes.split(","):
+        os.environ["NT_BWD"] = mode
+        for name, fn in (("fwd", fwd), (f"train[{mode}]", step)):
+            for _ in range(3):
+                fn()
+            torch.cuda.synchronize()
+            ts = []
+            for _ in range(a.steps):
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                fn()
+                e.record()
+                e.synchronize()
+                ts.append(s.elapsed_time(e))
+            res[name] = statistics.median(ts)
+    print(f"V={G.num_nodes} E={E} h={a.h} depth={a.depth}")
+    for k, v in res.items():
+        print(f"{k:14s} {v:8.3f} ms/step  {E * a.depth / (v * 1e-3):.3e} edge-msg/s")
+
+
+if __name__ == "__main__":
+    main()
