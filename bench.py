@@ -37,11 +37,13 @@ PEAK_HBM_GBPS = 8000.0
 PEAK_BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
 
 WORKLOADS = {
-    # name: (generator, molecules per GPU, hidden, depth)
-    "qm9-4096": ("qm9", 4096, 300, 3),  # BASELINE config 2 (the metric's configuration)
-    "qm9-32k": ("qm9", 32768, 300, 3),  # HBM-scale batch (working set >> Infinity Cache)
-    "zinc-4096": ("zinc", 4096, 512, 5),  # config 3 shape, run in fp32
-    "polymer-16": ("polymer", 16, 300, 3),  # config 5 shape
+    # name: (generator, molecules per GPU, hidden, depth, storage dtype)
+    "qm9-4096": ("qm9", 4096, 300, 3, "f32"),  # BASELINE config 2 (the metric's configuration)
+    "qm9-32k": ("qm9", 32768, 300, 3, "f32"),  # HBM-scale batch (working set >> Infinity Cache)
+    "qm9-125k": ("qm9", 125000, 300, 3, "f32"),  # config 4: one GPU's whole 1M/8 shard in one batch
+    "zinc-4096-bf16": ("zinc", 4096, 512, 5, "bf16"),  # BASELINE config 3 (bf16)
+    "zinc-4096": ("zinc", 4096, 512, 5, "f32"),  # config 3 shape, fp32
+    "polymer-16": ("polymer", 16, 300, 3, "f32"),  # config 5 shape
 }
 
 
@@ -164,7 +166,8 @@ def main():
     from notorch_amd.nn.gnn import _engine
 
     _lib.load()  # fail loudly if the HIP extension is missing
-    kind, n_mols, h, depth = WORKLOADS[args.workload]
+    kind, n_mols, h, depth, sdtype = WORKLOADS[args.workload]
+    bf16 = sdtype == "bf16"
     torch.manual_seed(0)
     batch = make_batch(kind, n_mols, seed=1000 + env.rank)
     G = batch.collate("nodes")
@@ -174,10 +177,14 @@ def main():
         Xv, Xe = emb_v(G.node_feats), emb_e(G.edge_feats)
     block = ChempropBlock(hidden_dim=h, depth=depth).eval()
     readout = Sum()
-    Ws = [l.linear.weight.detach().clone() for l in block._chemprop_layers()]
-    bs = [l.linear.bias.detach().clone() for l in block._chemprop_layers()]
+    if bf16:  # bf16 storage: the CPU baseline runs the fp32 oracle on the same bf16-rounded values
+        block = block.to(torch.bfloat16)
+        Xv, Xe = Xv.to(torch.bfloat16), Xe.to(torch.bfloat16)
+    Ws = [l.linear.weight.detach().float().clone() for l in block._chemprop_layers()]
+    bs = [l.linear.bias.detach().float().clone() for l in block._chemprop_layers()]
     block = block.to(dev)
     Gd = G.update(node_feats=Xv, edge_feats=Xe).to(dev)
+    Xv, Xe = Xv.float(), Xe.float()
     V, E, B = G.num_nodes, G.num_edges, len(G)
     torch.cuda.synchronize(dev)
 
@@ -206,7 +213,7 @@ def main():
 
     lay = getattr(Gd, "_nt_layout", None)
     used_fused = bool(
-        lay is not None and _engine._fused_enabled() and K.fused_supported(V, E, h)
+        lay is not None and _engine._fused_enabled() and K.fused_supported(V, E, h, Gd.edge_feats.dtype)
         and _engine.fused_plan(lay, V, E) is not None
     )
     upd_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
@@ -221,7 +228,27 @@ def main():
     variant = os.environ.get("NT_UPDATE_KERNEL", "as")
     fused = used_fused
     traffic = read_pmc_traffic(args.pmc_csv) if args.pmc_csv else None
-    if fused or (h % 4 == 0 and 97 <= h <= 512 and variant[0] in "axp"):
+    if bf16:
+        # native bf16 MFMA (16x16x32, K padded to 32, N to 16); HBM bytes at 2 B per element
+        kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
+        upd_bytes = update_bytes(V, E, h, b=2)
+        bf16_flops = 2 * E * kp * np_
+        t_hbm = upd_bytes / (PEAK_HBM_GBPS * 1e9)
+        t_mfma = bf16_flops / (PEAK_BF16_MFMA_TFLOPS * 1e12)
+        bound = "hbm" if t_hbm >= t_mfma else "mfma"
+        if bound == "hbm":
+            achieved, peak, unit = upd_bytes / (upd_ms * 1e-3) / 1e9, PEAK_HBM_GBPS, "GB/s"
+        else:
+            achieved, peak, unit = bf16_flops / (upd_ms * 1e-3) / 1e12, PEAK_BF16_MFMA_TFLOPS, "TFLOP/s"
+        kname = "nt_dmpnn_update (update_bf16_kernel: 64-edge tiles, bf16 16x16x32 MFMA, fp32 accumulate)"
+        extra = {
+            "mfma_bf16_tflops": bf16_flops / (upd_ms * 1e-3) / 1e12,
+            "mfma_bf16_frac": bf16_flops / (upd_ms * 1e-3) / 1e12 / PEAK_BF16_MFMA_TFLOPS,
+            "hbm_frac": upd_bytes / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
+            "t_min_us": max(t_hbm, t_mfma) * 1e6,
+        }
+        x6 = False
+    elif fused or (h % 4 == 0 and 97 <= h <= 512 and variant[0] in "axp"):
         # bf16x6 fp32 emulation: 6 bf16 MFMA products per fp32 product.  Fused / as16 kernels run
         # v_mfma_f32_16x16x32_bf16 (K padded to 32, N to 16); x6 runs 32x32x16 (K to 16, N to 32).
         if fused or variant[0] == "a":
@@ -257,9 +284,10 @@ def main():
         achieved, peak, unit = flops_upd / (upd_ms * 1e-3) / 1e12, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
         kname = "nt_dmpnn_update (fp32 16x16x4 MFMA, variant %s)" % variant
         extra = {"alg_hbm_gbps": upd_bytes / (upd_ms * 1e-3) / 1e9}
-    fwd_bytes, fwd_flops = forward_bytes_flops(V, E, B, h, depth)
+    fwd_bytes, fwd_flops = forward_bytes_flops(V, E, B, h, depth, b=2 if bf16 else 4)
     t_step = secs / args.steps
-    t_min = max(fwd_bytes / (PEAK_HBM_GBPS * 1e9), fwd_flops / (PEAK_FP32_MFMA_TFLOPS * 1e12))
+    mfma_peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
+    t_min = max(fwd_bytes / (PEAK_HBM_GBPS * 1e9), fwd_flops / (mfma_peak * 1e12))
     line = {
         "metric": METRIC,
         "value": rate,
@@ -271,9 +299,10 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "mfma_numerics": "bf16x6 split (fp32-accurate)" if x6 else "fp32 MFMA",
-        "data": "synthetic (seeded QM9-shaped molecules per rank, random-init EmbeddingBag + weights)",
+        "dtype": "bf16" if bf16 else "f32",
+        "mfma_numerics": ("bf16 MFMA, fp32 accumulate" if bf16 else
+                          "bf16x6 split (fp32-accurate)" if x6 else "fp32 MFMA"),
+        "data": f"synthetic (seeded {kind}-shaped molecules per rank, random-init EmbeddingBag + weights)",
         "config": {
             "workload": f"{args.workload}: {n_mols} {kind}-shaped molecules per GPU, D-MPNN depth={depth} "
             f"hidden={h}, ChempropBlock + Sum readout, reference collate (rev offset by nodes)",
@@ -303,7 +332,7 @@ def main():
             "alg_bytes": fwd_bytes,
             "flops": fwd_flops,
             "hbm_frac": fwd_bytes / t_step / (PEAK_HBM_GBPS * 1e9),
-            "mfma_frac": fwd_flops / t_step / (PEAK_FP32_MFMA_TFLOPS * 1e12),
+            "mfma_frac": fwd_flops / t_step / (mfma_peak * 1e12),
             "binding_frac": t_min / t_step,
         },
     }

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <float.h>
+
 #include <string>
 
 #include "../../include/notorch_amd.h"
@@ -77,6 +79,40 @@ __device__ __forceinline__ float4 operator+(float4 a, float4 b) {
 __device__ __forceinline__ float4 operator-(float4 a, float4 b) {
   return make_float4(a.x - b.x, a.y - b.y, a.z - b.z, a.w - b.w);
 }
+
+// ---- torch_scatter reduce semantics in fp32 (sum; mean = sum / max(n,1); max/min, empty -> 0) ----
+template <int R>
+struct Reducer {
+  float acc;
+  int n;
+  __device__ __forceinline__ void init() {
+    n = 0;
+    if constexpr (R == NT_MAX) acc = -FLT_MAX;
+    else if constexpr (R == NT_MIN) acc = FLT_MAX;
+    else acc = 0.f;
+  }
+  __device__ __forceinline__ void push(float x) {
+    ++n;
+    if constexpr (R == NT_MAX) acc = (n == 1 || x > acc) ? x : acc;
+    else if constexpr (R == NT_MIN) acc = (n == 1 || x < acc) ? x : acc;
+    else acc += x;
+  }
+  __device__ __forceinline__ float result() const {
+    if constexpr (R == NT_MEAN) return acc / (float)(n > 1 ? n : 1);
+    else if constexpr (R == NT_MAX || R == NT_MIN) return n == 0 ? 0.f : acc;
+    else return acc;
+  }
+};
+
+template <int R>
+struct Reducer4 {
+  Reducer<R> x, y, z, w;
+  __device__ __forceinline__ void init() { x.init(); y.init(); z.init(); w.init(); }
+  __device__ __forceinline__ void push(float4 v) { x.push(v.x); y.push(v.y); z.push(v.z); w.push(v.w); }
+  __device__ __forceinline__ float4 result() const {
+    return make_float4(x.result(), y.result(), z.result(), w.result());
+  }
+};
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 

@@ -12,42 +12,10 @@
 // These kernels are HBM-bound: bytes per segment = (rows read + 1 row written) * h * 4.
 #include <float.h>
 
+#include "bf16.hpp"
 #include "common.hpp"
 
 namespace nt {
-
-template <int R>
-struct Reducer {
-  float acc;
-  int n;
-  __device__ __forceinline__ void init() {
-    n = 0;
-    if constexpr (R == NT_MAX) acc = -FLT_MAX;
-    else if constexpr (R == NT_MIN) acc = FLT_MAX;
-    else acc = 0.f;
-  }
-  __device__ __forceinline__ void push(float x) {
-    ++n;
-    if constexpr (R == NT_MAX) acc = (n == 1 || x > acc) ? x : acc;
-    else if constexpr (R == NT_MIN) acc = (n == 1 || x < acc) ? x : acc;
-    else acc += x;
-  }
-  __device__ __forceinline__ float result() const {
-    if constexpr (R == NT_MEAN) return acc / (float)(n > 1 ? n : 1);
-    else if constexpr (R == NT_MAX || R == NT_MIN) return n == 0 ? 0.f : acc;
-    else return acc;
-  }
-};
-
-template <int R>
-struct Reducer4 {
-  Reducer<R> x, y, z, w;
-  __device__ __forceinline__ void init() { x.init(); y.init(); z.init(); w.init(); }
-  __device__ __forceinline__ void push(float4 v) { x.push(v.x); y.push(v.y); z.push(v.z); w.push(v.w); }
-  __device__ __forceinline__ float4 result() const {
-    return make_float4(x.result(), y.result(), z.result(), w.result());
-  }
-};
 
 // ---------------- segment reduce ----------------
 template <int R, int ACT>
@@ -186,12 +154,14 @@ extern "C" int nt_segment_reduce(const void* X, const int32_t* seg_ptr, const in
                                  int dtype, void* out, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for segment_reduce");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
   NT_REQUIRE(nseg >= 0 && h > 0, NT_EINVAL, "bad sizes");
   if (nseg == 0) return NT_OK;
   NT_REQUIRE(X && seg_ptr && out, NT_EINVAL, "NULL pointer");
   hipStream_t stream = as_stream(stream_);
+  if (dtype == NT_BF16)
+    return launch_segment_reduce_bf16(X, seg_ptr, perm, nseg, h, reduce, act, act_alpha, out, stream);
   const bool vec = (h % 4 == 0) && aligned16(X) && aligned16(out);
   if (vec) {
     const int64_t hv = h / 4;
@@ -215,10 +185,12 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
                              void* S, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for dmpnn_init");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
   NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
   hipStream_t stream = as_stream(stream_);
+  if (dtype == NT_BF16)
+    return launch_init_bf16(Xv, Xe, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S, stream);
   const bool vec = (h % 4 == 0) && aligned16(Xv) && aligned16(Xe) && aligned16(H0) &&
                    (S == nullptr || aligned16(S));
   if (S != nullptr) {

@@ -27,6 +27,7 @@
 #include <type_traits>
 
 #include "common.hpp"
+#include "bf16.hpp"
 #include "update.hpp"
 
 namespace nt {
@@ -517,8 +518,8 @@ static size_t as_part_bytes(int64_t h) {
 }
 
 extern "C" size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype) {
-  (void)dtype;
   if (h <= 0) return 0;
+  if (dtype == NT_BF16) return (nt::bf16_image_bytes(h) + 255) & ~size_t(255);
   return f32_image_bytes(h) + x6_part_bytes(h) + as_part_bytes(h);
 }
 
@@ -526,10 +527,13 @@ extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, i
                                     void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for pack_weight");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(nlayers >= 0 && h > 0 && h <= 512, NT_EINVAL, "bad sizes (1 <= h <= 512)");
   if (nlayers == 0) return NT_OK;
   NT_REQUIRE(W && Wp && aligned16(Wp), NT_EINVAL, "NULL or misaligned pointer");
+  if (dtype == NT_BF16)
+    return pack_weight_bf16(W, nlayers, h, (int64_t)nt_dmpnn_packed_weight_bytes(h, dtype), Wp,
+                            as_stream(stream_));
   const UpdateGeom g = geom_for(h);
   const size_t per_layer = nt_dmpnn_packed_weight_bytes(h, dtype);
   NT_REQUIRE(per_layer % 16 == 0, NT_EINVAL, "internal: packed layer size");
@@ -561,13 +565,16 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                                int dtype, void* H_out, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for dmpnn_update");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
   NT_REQUIRE(V >= 0 && E >= 0 && h > 0 && h <= 512, NT_EINVAL, "bad sizes (1 <= h <= 512)");
   if (E == 0) return NT_OK;
   NT_REQUIRE(H && S && src && rev && Wp && H_out, NT_EINVAL, "NULL pointer");
   NT_REQUIRE(H != H_out, NT_EINVAL, "H_out must not alias H");
   NT_REQUIRE(aligned16(Wp), NT_EINVAL, "Wp must be 16-byte aligned");
+  if (dtype == NT_BF16)
+    return launch_update_bf16(H, S, src, rev, Wp, b, V, E, h, residual, act, act_alpha, H_out,
+                              as_stream(stream_));
   const UpdateGeom g = geom_for(h);
   const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(S) && aligned16(H_out) &&
                    (b == nullptr || aligned16(b));

@@ -11,7 +11,7 @@ import torch
 from torch import Tensor
 
 from notorch_amd import _lib
-from notorch_amd._lib import NT_F32, REDUCE_CODES, check
+from notorch_amd._lib import NT_BF16, NT_F32, REDUCE_CODES, check
 
 __all__ = [
     "csr_build",
@@ -61,6 +61,21 @@ def _require_f32(name: str, t: Tensor) -> None:
         raise TypeError(f"{name} must be float32 on the fp32 kernel path, got {t.dtype}")
     if not t.is_contiguous():
         raise ValueError(f"{name} must be contiguous")
+
+
+_DTYPE_CODES = {torch.float32: NT_F32, torch.bfloat16: NT_BF16}
+
+
+def _require_feat(name: str, t: Tensor, dtype: torch.dtype | None = None) -> int:
+    """Feature tensor on the kernel path: fp32 or bf16 (all operands of one call share it), contiguous.
+    Returns the C-ABI dtype code."""
+    if t.dtype not in _DTYPE_CODES:
+        raise TypeError(f"{name} must be float32 or bfloat16, got {t.dtype}")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} is {t.dtype} but the other operands are {dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    return _DTYPE_CODES[t.dtype]
 
 
 def _require_i64(name: str, t: Tensor) -> None:
@@ -145,8 +160,8 @@ def dmpnn_init(
 ) -> tuple[Tensor, Tensor | None]:
     """H0 = Xv[src] + Xe, optionally fused with S = scatter(act(H0), dst) (needs the dst CSR)."""
     dev = _require_device(Xv, Xe, src, seg_ptr, perm)
-    _require_f32("node_feats", Xv)
-    _require_f32("edge_feats", Xe)
+    code = _require_feat("node_feats", Xv)
+    _require_feat("edge_feats", Xe, Xv.dtype)
     _require_i64("src", src)
     if Xv.dim() != 2 or Xe.dim() != 2 or Xv.shape[1] != Xe.shape[1]:
         raise RuntimeError(
@@ -164,7 +179,7 @@ def dmpnn_init(
     check(
         lib.nt_dmpnn_init(
             _ptr(Xv), _ptr(Xe), _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h, act[0], act[1],
-            reduce_code(reduce), NT_F32, _ptr(H0), _ptr(S), _stream(dev),
+            reduce_code(reduce), code, _ptr(H0), _ptr(S), _stream(dev),
         )
     )
     return H0, S
@@ -182,7 +197,9 @@ def segment_reduce(
 ) -> Tensor:
     """out[s] = reduce over rows X[perm[j]] (j in segment s) of act(row); empty segment -> 0."""
     dev = _require_device(X, seg_ptr, perm)
-    _require_f32("X", X)
+    code = _require_feat("X", X)
+    if out is not None:
+        _require_feat("out", out, X.dtype)
     if X.dim() != 2:
         raise ValueError("X must be 2-D")
     if seg_ptr.dtype != torch.int32 or seg_ptr.numel() != nseg + 1:
@@ -193,21 +210,24 @@ def segment_reduce(
     lib = _lib.load()
     check(
         lib.nt_segment_reduce(
-            _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce), act[0], act[1], NT_F32,
+            _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce), act[0], act[1], code,
             _ptr(out), _stream(dev),
         )
     )
     return out
 
 
-def packed_weight_numel(h: int) -> int:
-    return _lib.load().nt_dmpnn_packed_weight_bytes(h, NT_F32) // 4
+def packed_weight_numel(h: int, dtype: torch.dtype = torch.float32) -> int:
+    """Size (in 4-byte words) of one layer's packed weight image for feature dtype ``dtype``."""
+    return _lib.load().nt_dmpnn_packed_weight_bytes(h, _DTYPE_CODES[dtype]) // 4
 
 
 def pack_weights(W: Tensor) -> Tensor:
-    """Pack one nn.Linear weight [h, h] (or a stack [L, h, h]) into the MFMA fragment image."""
+    """Pack one nn.Linear weight [h, h] (or a stack [L, h, h]) into the MFMA fragment image of its
+    dtype (fp32: bf16x3-split images; bf16: one bf16 fragment image).  The image is an opaque
+    float32-typed buffer; its dtype is recorded as ``Wp.nt_dtype``."""
     dev = _require_device(W)
-    _require_f32("weight", W)
+    code = _require_feat("weight", W)
     if W.dim() == 2:
         W3 = W.unsqueeze(0)
     else:
@@ -215,9 +235,9 @@ def pack_weights(W: Tensor) -> Tensor:
     L, h, h2 = W3.shape
     if h != h2:
         raise ValueError(f"ChempropLayer weight must be square, got {tuple(W.shape)}")
-    Wp = torch.empty(L, packed_weight_numel(h), dtype=torch.float32, device=dev)
+    Wp = torch.empty(L, packed_weight_numel(h, W.dtype), dtype=torch.float32, device=dev)
     lib = _lib.load()
-    check(lib.nt_dmpnn_pack_weight(_ptr(W3), L, h, NT_F32, _ptr(Wp), _stream(dev)))
+    check(lib.nt_dmpnn_pack_weight(_ptr(W3), L, h, code, _ptr(Wp), _stream(dev)))
     return Wp[0] if W.dim() == 2 else Wp
 
 
@@ -235,35 +255,38 @@ def dmpnn_update(
 ) -> Tensor:
     """H_out = (residual ? H : 0) + (S[src] - act(H[rev])) @ W^T + b   (one fused launch)."""
     dev = _require_device(H, S, src, rev, Wp, bias, out)
-    _require_f32("H", H)
-    _require_f32("S", S)
+    code = _require_feat("H", H)
+    _require_feat("S", S, H.dtype)
     _require_i64("src", src)
     _require_i64("rev_index", rev)
     E, h = H.shape
     V = S.shape[0]
     if S.shape[1] != h or src.numel() != E or rev.numel() != E:
         raise ValueError("shape mismatch between H, S, src and rev_index")
-    if Wp.numel() != packed_weight_numel(h):
-        raise ValueError("Wp is not a packed weight image for this hidden size")
+    if Wp.numel() != packed_weight_numel(h, H.dtype):
+        raise ValueError(f"Wp is not a packed {H.dtype} weight image for this hidden size")
     if bias is not None:
-        _require_f32("bias", bias)
+        _require_feat("bias", bias, H.dtype)
         if bias.numel() != h:
             raise ValueError("bias must have h entries")
     if out is None:
         out = torch.empty_like(H)
+    else:
+        _require_feat("out", out, H.dtype)
     lib = _lib.load()
     check(
         lib.nt_dmpnn_update(
             _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
-            act[0], act[1], NT_F32, _ptr(out), _stream(dev),
+            act[0], act[1], code, _ptr(out), _stream(dev),
         )
     )
     return out
 
 
-def fused_supported(V: int, E: int, h: int) -> bool:
-    """Shapes the fused persistent kernel (nt_dmpnn_update_fused) accepts."""
-    return h % 4 == 0 and 4 <= h <= 304 and E * h // 4 < 2**31 and V * h // 4 < 2**31 and E < 2**31
+def fused_supported(V: int, E: int, h: int, dtype: torch.dtype = torch.float32) -> bool:
+    """Shapes the fused persistent kernel (nt_dmpnn_update_fused, fp32 only) accepts."""
+    return (dtype == torch.float32 and h % 4 == 0 and 4 <= h <= 304 and E * h // 4 < 2**31
+            and V * h // 4 < 2**31 and E < 2**31)
 
 
 def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int) -> tuple[Tensor, int, Tensor]:

@@ -14,7 +14,9 @@ d + 1 launches (+ one nt_dmpnn_pack_weight per distinct weight, cached).  Otherw
 
     nt_dmpnn_init; for l: nt_dmpnn_update, nt_segment_reduce; nt_segment_reduce (node)   2 + 2d launches
 
-Backward (training), reduce in {sum, mean}: the forward keeps (H_l, S_l) of
+bf16 features (BASELINE config 3) run the unfused sequence on the bf16 kernels (csrc/bf16.hip).
+
+Backward (training), reduce in {sum, mean}, fp32: the forward keeps (H_l, S_l) of
 every layer; per layer, last to first (csrc/backward.hip):
 
     nt_dmpnn_message        A_l = S_l[src] - act(H_l)[rev]                   (recomputed, for dW)
@@ -22,8 +24,8 @@ every layer; per layer, last to first (csrc/backward.hip):
     nt_segment_reduce       dS = scatter_sum(dA, src)            (src CSR, cached on the layout)
     nt_dmpnn_edge_backward  G <- G + act'(H_l) * (dS[dst] / c - scatter_sum(dA, rev))  (rev CSR)
 
-then dXe = G, dXv = scatter_sum(G, src).  max/min reductions recompute the block in PyTorch device
-ops and run autograd (``_torch_block``).
+then dXe = G, dXv = scatter_sum(G, src).  max/min reductions and bf16 recompute the block in
+PyTorch device ops and run autograd (``_torch_block``).
 """
 from __future__ import annotations
 
@@ -180,7 +182,7 @@ def block_forward(
     Wps = pack_layer_weights(weights)
     H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
     E, h = H.shape
-    plan = fused_plan(lay, V, E) if _fused_enabled() and K.fused_supported(V, E, h) else None
+    plan = fused_plan(lay, V, E) if _fused_enabled() and K.fused_supported(V, E, h, H.dtype) else None
     if plan is not None:
         return _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual, keep_states)
     states = []
@@ -331,7 +333,8 @@ class ChempropBlockFunction(torch.autograd.Function):
         weights = list(params[:nlayers])
         biases = list(params[nlayers:])
         src = edge_index[0].contiguous()
-        kernel_bwd = reduce in ("sum", "mean") and os.environ.get("NT_BWD", "kernel") != "torch"
+        kernel_bwd = (reduce in ("sum", "mean") and Xv.dtype == torch.float32
+                      and os.environ.get("NT_BWD", "kernel") != "torch")
         node, H, states = block_forward(Xv, Xe, src, rev, lay, weights, biases, act, reduce, residual,
                                         keep_states=kernel_bwd)
         flat = [t for hs in states for t in hs]
@@ -396,7 +399,8 @@ class ReadoutFunction(torch.autograd.Function):
     def backward(ctx, dout):
         X, bni = ctx.saved_tensors
         B, reduce, mol_ptr = ctx.cfg
-        if reduce in ("sum", "mean"):  # dX[v] = dout[batch v] (/ count for mean): one gather kernel
+        if reduce in ("sum", "mean") and dout.dtype == torch.float32:
+            # dX[v] = dout[batch v] (/ count for mean): one gather kernel
             dX = K.gather_rows(dout.contiguous(), bni, seg_ptr=mol_ptr if reduce == "mean" else None)
             return dX, None, None, None, None, None
         with torch.enable_grad():

@@ -87,7 +87,7 @@ class ChempropLayer(nn.Module):
             # training through a standalone layer: route through the block function with depth 1
             # and no residual, then subtract nothing (the block function returns H_1 = U).
             lay = _engine.DeviceLayout(*self._csr(edge_index, rev_index, V), edge_index=edge_index, validated=True)
-            Xv = torch.zeros(V, edge_feats.shape[1], device=edge_feats.device)
+            Xv = torch.zeros(V, edge_feats.shape[1], device=edge_feats.device, dtype=edge_feats.dtype)
             # H0 = Xv[src] + Xe = edge_feats exactly (adding +0.0)
             _, H = _engine.ChempropBlockFunction.apply(
                 Xv, edge_feats, edge_index, rev_index.contiguous(), lay, self.act, act, self.reduce,
@@ -153,6 +153,12 @@ class ChempropBlock(nn.Module):
                 "hidden dimension (chemprop.py:83)"
             )
         layers = self._chemprop_layers()
+        if Xv.dtype != Xe.dtype or any(l.linear.weight.dtype != Xv.dtype for l in layers):
+            # what nn.Linear / the Xv[src] + Xe add would raise on mixed dtypes in the reference
+            raise RuntimeError(
+                f"node_feats ({Xv.dtype}), edge_feats ({Xe.dtype}) and the layer weights must share "
+                "one dtype (float32, or bfloat16 after block.to(torch.bfloat16))"
+            )
         for layer in layers:
             _check_dropout(layer)
         acts = {K.act_code(layer.act) for layer in layers}

@@ -186,21 +186,43 @@ def test_block_grads_polymer_hubs_unfused_forward():
     _check(_graph("polymer", 2, seed=11), 32, depth=2, reduce="mean", readout="mean", fp32_floor=True)
 
 
-def test_block_grads_config2_fp32():
-    """Config-2 shape (4096 QM9 molecules, h=300, depth 3) against the fp32 oracle's autograd."""
+def _rel_l2(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+
+@pytest.mark.parametrize("act", ["ReLU", "SiLU"])
+def test_block_grads_config2_fp32(act):
+    """Config-2 shape (4096 QM9 molecules, h=300, depth 3), fp64 oracle autograd as the truth.
+
+    SiLU (smooth): every gradient within the fp32 contract of fp64, normalised max <= 1e-5.
+    ReLU: at 23M edge-state elements some H_l entries sit within fp32 rounding of 0, so ANY two
+    fp32 evaluations disagree on relu'(H) there and the gradient of that element (and, through the
+    earlier layers, of its molecule) jumps by a whole dm.  Measured on MI355X: the fp32 CPU oracle
+    itself is 1.2e-2 (max) / 1.4e-4 (L2) off fp64 on dXv, the kernels 1.2e-2 / 1.3e-4 (and
+    3e-7 / 3e-7 with SiLU).  So for ReLU the kernels must be no further from fp64 than 2x the fp32
+    CPU oracle, on both the normalised max and the relative L2 error (tools/diag_grad.py)."""
     from notorch_amd.nn import ChempropBlock
 
     G = _graph("qm9", 4096, seed=0)
     h = 300
     Xv, Xe = _embed(G, h)
     torch.manual_seed(1)
-    blk = ChempropBlock(h, depth=3)
-    truth = _oracle_grads(G, Xv, Xe, blk, torch.relu, True, "sum", "sum", torch.float32)
+    blk = ChempropBlock(h, depth=3, act=_ACTS[act][0])
+    fn = _ACTS[act][1]
+    truth = _oracle_grads(G, Xv, Xe, blk, fn, True, "sum", "sum", torch.float64)
+    o32 = _oracle_grads(G, Xv, Xe, blk, fn, True, "sum", "sum", torch.float32)
     got = _device_grads(G, Xv, Xe, blk, "sum")
-    for name, a, b in (("dXv", got[1], truth[1]), ("dXe", got[2], truth[2])):
-        assert_parity(a, b, 2e-5, name)
-    for l, (a, b) in enumerate(zip(got[3], truth[3])):
-        assert_parity(a, b, 2e-5, f"dW[{l}]")
+    pairs = [("dXv", got[1], o32[1], truth[1]), ("dXe", got[2], o32[2], truth[2])]
+    pairs += [(f"dW[{l}]", a, c, b) for l, (a, c, b) in enumerate(zip(got[3], o32[3], truth[3]))]
+    pairs += [(f"db[{l}]", a, c, b) for l, (a, c, b) in enumerate(zip(got[4], o32[4], truth[4]))]
+    for name, a, c, b in pairs:
+        if act == "SiLU":
+            assert_parity(a, b, GRAD_TOL, name)
+            continue
+        l2, l2_cpu = _rel_l2(a, b), _rel_l2(c, b)
+        assert l2 <= max(1e-5, 2 * l2_cpu), f"{name}: relative L2 {l2:.3e} (fp32 CPU oracle {l2_cpu:.3e})"
+        assert_parity(a, b, max(2e-5, 2 * norm_err(c, b)), name)
 
 
 def test_max_reduce_takes_recompute_backward():

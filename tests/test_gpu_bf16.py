@@ -1,0 +1,197 @@
+"""GPU parity of the bf16 storage path (BASELINE config 3: ZINC-shaped, depth 5, hidden 512, bf16).
+
+The kernels store bf16 and compute in fp32 (csrc/bf16.hip).  Oracle: the fp32 CPU restatement
+(oracle/dmpnn_ref.py) fed the bf16-rounded inputs and weights.
+* element kernels (init, segment reduce): the oracle's fp32 result rounded to bf16 once — bit-exact,
+  because the kernels sum in the CPU scatter_add_ order and round once;
+* one update launch: within 1 bf16 ulp of the max element (normalised max error <= 2^-8), the only
+  differences being the fp32 accumulation order of the GEMM and that final rounding;
+* the whole block + readout: normalised max error <= 2e-2 (SURVEY §8(c) bf16 criterion): the kernels
+  round H_l and S_l to bf16 at every layer, the fp32 oracle never does.
+"""
+import pytest
+import torch
+import torch.nn as nn
+
+from helpers import assert_parity, norm_err
+from oracle import dmpnn_ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+BF = torch.bfloat16
+BLOCK_TOL = 2e-2
+ULP_TOL = 2.0 ** -8
+
+
+def _K():
+    from notorch_amd import kernels
+
+    return kernels
+
+
+def _graph(kind="zinc", n=32, seed=0, rev_offset="nodes"):
+    from notorch_amd.data.synth import make_batch
+
+    return make_batch(kind, n, seed=seed).collate(rev_offset)
+
+
+def _rand_bf16(*shape, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    return torch.randn(*shape, generator=g).to(BF)
+
+
+# ------------------------------------------------------------------ element kernels (bit-exact)
+@pytest.mark.parametrize("h", [512, 300, 13])  # 16-B pieces, 16-B pieces with h % 8 = 4 -> scalar, scalar
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
+def test_segment_reduce_bf16(h, reduce):
+    K = _K()
+    G = _graph("zinc", 24, seed=1)
+    E, V = G.num_edges, G.num_nodes
+    X = _rand_bf16(E, h, seed=h)
+    dst = G.edge_index[1]
+    seg_ptr, perm = K.csr_build(dst.to(DEV), V)
+    out = K.segment_reduce(X.to(DEV), seg_ptr, perm, V, reduce=reduce, act=K.act_code(nn.ReLU()))
+    assert out.dtype == BF
+    ref = dmpnn_ref.scatter(torch.relu(X.float()), dst, V, reduce).to(BF)
+    assert torch.equal(out.cpu(), ref)
+
+
+@pytest.mark.parametrize("h", [512, 300, 13])
+def test_init_bf16(h):
+    K = _K()
+    G = _graph("zinc", 24, seed=2)
+    E, V = G.num_edges, G.num_nodes
+    Xv, Xe = _rand_bf16(V, h, seed=1), _rand_bf16(E, h, seed=2)
+    src, dst = G.edge_index
+    seg_ptr, perm = K.csr_build(dst.to(DEV), V)
+    H0, S = K.dmpnn_init(Xv.to(DEV), Xe.to(DEV), src.to(DEV), seg_ptr, perm)
+    ref_H0 = (Xv.float()[src] + Xe.float()).to(BF)
+    assert torch.equal(H0.cpu(), ref_H0)
+    assert torch.equal(S.cpu(), dmpnn_ref.scatter(torch.relu(ref_H0.float()), dst, V, "sum").to(BF))
+    H0_only, none = K.dmpnn_init(Xv.to(DEV), Xe.to(DEV), src.to(DEV))
+    assert none is None and torch.equal(H0_only.cpu(), ref_H0)
+
+
+# ------------------------------------------------------------------ one update launch
+@pytest.mark.parametrize("h", [512, 304, 300, 64, 40, 13])
+@pytest.mark.parametrize("residual,bias", [(True, True), (False, False)])
+def test_update_bf16(h, residual, bias):
+    K = _K()
+    G = _graph("zinc", 40, seed=3)  # E not a multiple of the 64-edge tile
+    E, V = G.num_edges, G.num_nodes
+    H, S = _rand_bf16(E, h, seed=4), _rand_bf16(V, h, seed=5)
+    W = (_rand_bf16(h, h, seed=6).float() / h ** 0.5).to(BF)
+    b = _rand_bf16(h, seed=7) if bias else None
+    src, rev = G.edge_index[0], G.rev_index
+    Wp = K.pack_weights(W.to(DEV))
+    got = K.dmpnn_update(H.to(DEV), S.to(DEV), src.to(DEV), rev.to(DEV), Wp,
+                         None if b is None else b.to(DEV), residual=residual)
+    assert got.dtype == BF
+    # the message operand is rounded to bf16 before the MFMA (what a bf16 nn.Linear input holds)
+    A = (S.float()[src] - torch.relu(H.float()[rev])).to(BF).float()
+    ref = A @ W.float().T
+    if bias:
+        ref = ref + b.float()
+    if residual:
+        ref = ref + H.float()
+    assert_parity(got.float(), ref, ULP_TOL, f"update bf16 h={h}")
+
+
+def test_update_bf16_identity_and_silu():
+    K = _K()
+    G = _graph("zinc", 16, seed=8)
+    E, V, h = G.num_edges, G.num_nodes, 128
+    H, S = _rand_bf16(E, h, seed=9), _rand_bf16(V, h, seed=10)
+    W = (_rand_bf16(h, h, seed=11).float() / h ** 0.5).to(BF)
+    src, rev = G.edge_index[0], G.rev_index
+    Wp = K.pack_weights(W.to(DEV))
+    for mod, fn in ((nn.Identity(), lambda x: x), (nn.SiLU(), torch.nn.functional.silu)):
+        got = K.dmpnn_update(H.to(DEV), S.to(DEV), src.to(DEV), rev.to(DEV), Wp, None,
+                             act=K.act_code(mod))
+        A = (S.float()[src] - fn(H.float()[rev])).to(BF).float()
+        assert_parity(got.float(), H.float() + A @ W.float().T, ULP_TOL, type(mod).__name__)
+
+
+def test_bf16_mixed_dtypes_raise():
+    K = _K()
+    H = torch.zeros(4, 8, device=DEV, dtype=BF)
+    S = torch.zeros(2, 8, device=DEV)
+    idx = torch.zeros(4, dtype=torch.long, device=DEV)
+    Wp = K.pack_weights(torch.zeros(8, 8, device=DEV, dtype=BF))
+    with pytest.raises(TypeError):
+        K.dmpnn_update(H, S, idx, idx, Wp, None)
+    with pytest.raises(ValueError):  # an fp32 weight image for bf16 features
+        K.dmpnn_update(H, S.to(BF), idx, idx, K.pack_weights(torch.zeros(8, 8, device=DEV)), None)
+
+
+# ------------------------------------------------------------------ block + readout
+def _block_case(kind, n, h, depth, seed=0, **opts):
+    from notorch_amd.nn import ChempropBlock, Sum
+
+    G = _graph(kind, n, seed=seed)
+    torch.manual_seed(seed)
+    emb_v = nn.EmbeddingBag(42, h, mode="sum")
+    emb_e = nn.EmbeddingBag(13, h, mode="sum")
+    with torch.no_grad():
+        Xv, Xe = emb_v(G.node_feats).to(BF), emb_e(G.edge_feats).to(BF)
+    blk = ChempropBlock(hidden_dim=h, depth=depth, **opts).eval().to(BF)
+    Ws, bs = dmpnn_ref.block_params(blk)
+    act = {nn.ReLU: torch.relu, nn.SiLU: torch.nn.functional.silu}[type(blk._chemprop_layers()[0].act)]
+    with torch.inference_mode():
+        ref_node, ref_edge = dmpnn_ref.chemprop_block(
+            Xv.float(), Xe.float(), G.edge_index, G.rev_index, [W.float() for W in Ws],
+            [None if b is None else b.float() for b in bs], act=act,
+            residual=opts.get("residual", True), reduce=opts.get("reduce", "sum"))
+        ref_out = dmpnn_ref.readout(ref_node, G.batch_node_index, len(G), "sum")
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
+    with torch.no_grad():
+        out_G = blk.to(DEV)(Gd)
+        out = Sum()(out_G)
+    for name, a, b in (("edge", out_G.edge_feats, ref_edge), ("node", out_G.node_feats, ref_node),
+                       ("readout", out, ref_out)):
+        assert a.dtype == BF, name
+        assert_parity(a.float(), b, BLOCK_TOL, f"{kind} bf16 {name}")
+    return out_G
+
+
+def test_block_bf16_config3_shape():
+    """BASELINE config 3: 4096 ZINC-shaped molecules, depth 5, hidden 512, bf16."""
+    _block_case("zinc", 4096, 512, 5)
+
+
+@pytest.mark.parametrize("opts", [dict(), dict(residual=False), dict(bias=False), dict(reduce="mean"),
+                                  dict(act=nn.SiLU), dict(shared=True)])
+def test_block_bf16_options(opts):
+    _block_case("zinc", 64, 96, 3, seed=4, **opts)
+
+
+def test_block_bf16_polymer_hubs():
+    _block_case("polymer", 2, 64, 3, seed=5, reduce="mean")
+
+
+def test_block_bf16_rejects_mixed_dtypes():
+    from notorch_amd.nn import ChempropBlock
+
+    G = _graph("zinc", 4, seed=6)
+    blk = ChempropBlock(hidden_dim=16, depth=2).to(DEV)  # fp32 weights
+    Gd = G.update(node_feats=torch.zeros(G.num_nodes, 16, dtype=BF),
+                  edge_feats=torch.zeros(G.num_edges, 16, dtype=BF)).to(DEV)
+    with pytest.raises(RuntimeError):
+        blk(Gd)
+
+
+def test_block_bf16_trains_through_recompute_backward():
+    """bf16 training: forward on the bf16 kernels, gradients from the device-op recompute."""
+    from notorch_amd.nn import ChempropBlock, Sum
+
+    G = _graph("zinc", 8, seed=7)
+    h = 32
+    torch.manual_seed(0)
+    blk = ChempropBlock(hidden_dim=h, depth=2).to(DEV).to(BF).train()
+    Xv = torch.randn(G.num_nodes, h, device=DEV, dtype=BF, requires_grad=True)
+    Xe = torch.randn(G.num_edges, h, device=DEV, dtype=BF, requires_grad=True)
+    out = Sum()(blk(G.to(DEV).update(node_feats=Xv, edge_feats=Xe)))
+    out.float().pow(2).sum().backward()
+    for p in [Xv, Xe] + list(blk.parameters()):
+        assert p.grad is not None and p.grad.dtype == BF and torch.isfinite(p.grad.float()).all()
