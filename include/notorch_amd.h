@@ -38,7 +38,8 @@ extern "C" {
 
 enum nt_status { NT_OK = 0, NT_EINVAL = 1, NT_EHIP = 2, NT_EUNSUPPORTED = 3 };
 
-/* element type of feature matrices */
+/* element type of feature matrices, weights and bias.  NT_BF16: bf16 storage, fp32 arithmetic, one
+ * rounding per stored element (BASELINE config 3); the backward entry points are NT_F32 only. */
 enum nt_dtype { NT_F32 = 0, NT_BF16 = 1 };
 
 /* reduce domain of notorch.types.Reduction (types.py:57) with torch_scatter semantics:
@@ -62,6 +63,31 @@ NT_API int nt_abi_version(void);
 
 /* Message of the last failed call on this thread ("" if none). */
 NT_API const char* nt_last_error(void);
+
+/*
+ * GraphEmbedding (notorch/nn/gnn/embed.py:11-36), one sum-mode nn.EmbeddingBag (embed.py:21-22,29):
+ *   out[i] = sum_{j < k} table[idx[i * k + j]]          (ascending j, fp32 accumulation)
+ * table: num_types x h (dtype); idx: n x k int64 type indices (the featurised node_feats V x 7 or
+ * edge_feats E x 2, transforms/graph.py:32-43); out: n x h.  Indices outside [0, num_types) are
+ * skipped (the host validates them and raises IndexError as nn.EmbeddingBag would).
+ */
+NT_API int nt_embed_bag(const void* table, int64_t num_types, const int64_t* idx, int64_t n, int64_t k,
+                        int64_t h, int dtype, void* out, void* stream);
+
+/*
+ * GraphEmbedding fused into the initial gather (embed.py:29 then
+ * chemprop.py:82-83 and layer 0's chemprop.py:37-39), without materialising Xv / Xe:
+ *   H0[e] = Xv[src e] + Xe[e],  Xv[s] = sum_j node_table[node_types[s][j]],
+ *                               Xe[e] = sum_j edge_table[edge_types[e][j]]
+ *   S[v]  = reduce_{e: dst e = v} act(H0[e])   if S != NULL (then seg_ptr / perm = dst CSR)
+ * Bit-identical to nt_embed_bag twice followed by nt_dmpnn_init.
+ */
+NT_API int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_types,
+                               const int64_t* node_types, int64_t kv, const void* edge_table,
+                               int64_t num_edge_types, const int64_t* edge_types, int64_t ke,
+                               const int64_t* src, const int32_t* seg_ptr, const int32_t* perm,
+                               int64_t V, int64_t E, int64_t h, int act, float act_alpha, int reduce,
+                               int dtype, void* H0, void* S, void* stream);
 
 /* Number of bytes of device workspace nt_csr_build needs for n indices into nseg segments. */
 NT_API size_t nt_csr_workspace_bytes(int64_t n, int64_t nseg);

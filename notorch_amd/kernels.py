@@ -27,6 +27,8 @@ __all__ = [
     "dmpnn_message",
     "dmpnn_edge_backward",
     "gather_rows",
+    "embed_bag",
+    "dmpnn_init_embed",
 ]
 
 
@@ -441,3 +443,69 @@ def gather_rows(X: Tensor, idx: Tensor, *, base: Tensor | None = None, seg_ptr: 
         _ptr(base), _ptr(X), _ptr(idx), _ptr(seg_ptr), n, nseg, h, NT_F32, _ptr(out), _stream(dev)
     ))
     return out
+
+
+# ------------------------------------------------------------------------------------ embedding
+def _check_types(name: str, idx: Tensor, num_types: int) -> None:
+    _require_i64(name, idx)
+    if idx.dim() != 2:
+        raise ValueError(f"{name} must be n x k type indices")
+    if idx.numel():
+        mm = torch.stack([idx.min(), idx.max()]).cpu()
+        if mm[0] < 0 or mm[1] >= num_types:
+            raise IndexError(f"{name}: type index out of range for an embedding of {num_types} rows")
+
+
+def embed_bag(table: Tensor, idx: Tensor, *, validate: bool = True, out: Tensor | None = None) -> Tensor:
+    """nn.EmbeddingBag(mode="sum") of an n x k index matrix: out[i] = sum_j table[idx[i, j]]."""
+    dev = _require_device(table, idx, out)
+    code = _require_feat("table", table)
+    ntypes, h = table.shape
+    if validate:
+        _check_types("idx", idx, ntypes)
+    else:
+        _require_i64("idx", idx)
+    n, k = idx.shape
+    if out is None:
+        out = torch.empty(n, h, dtype=table.dtype, device=dev)
+    check(_lib.load().nt_embed_bag(_ptr(table), ntypes, _ptr(idx), n, k, h, code, _ptr(out), _stream(dev)))
+    return out
+
+
+def dmpnn_init_embed(
+    node_table: Tensor,
+    node_types: Tensor,
+    edge_table: Tensor,
+    edge_types: Tensor,
+    src: Tensor,
+    seg_ptr: Tensor | None = None,
+    perm: Tensor | None = None,
+    *,
+    act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
+    reduce: str = "sum",
+    validate: bool = True,
+) -> tuple[Tensor, Tensor | None]:
+    """H0 = Xv[src] + Xe with Xv = EmbeddingBag(node_table)(node_types), Xe likewise, never
+    materialised; optionally fused with S = scatter(act(H0), dst) (needs the dst CSR)."""
+    dev = _require_device(node_table, node_types, edge_table, edge_types, src, seg_ptr, perm)
+    code = _require_feat("node_table", node_table)
+    _require_feat("edge_table", edge_table, node_table.dtype)
+    if node_table.shape[1] != edge_table.shape[1]:
+        raise RuntimeError("node and edge embedding tables must share the hidden dimension")
+    if validate:
+        _check_types("node_types", node_types, node_table.shape[0])
+        _check_types("edge_types", edge_types, edge_table.shape[0])
+    _require_i64("src", src)
+    V, kv = node_types.shape
+    E, ke = edge_types.shape
+    h = node_table.shape[1]
+    if src.numel() != E:
+        raise ValueError("src must have one entry per edge")
+    H0 = torch.empty(E, h, dtype=node_table.dtype, device=dev)
+    S = None if seg_ptr is None else torch.empty(V, h, dtype=node_table.dtype, device=dev)
+    check(_lib.load().nt_dmpnn_init_embed(
+        _ptr(node_table), node_table.shape[0], _ptr(node_types), kv, _ptr(edge_table),
+        edge_table.shape[0], _ptr(edge_types), ke, _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h,
+        act[0], act[1], reduce_code(reduce), code, _ptr(H0), _ptr(S), _stream(dev),
+    ))
+    return H0, S

@@ -2,6 +2,7 @@ from notorch_amd.nn.gnn import (
     Aggregation,
     ChempropBlock,
     ChempropLayer,
+    EmbeddedChempropBlock,
     GraphEmbedding,
     Max,
     Mean,
@@ -11,5 +12,5 @@ from notorch_amd.nn.gnn import (
 from notorch_amd.nn.residual import Residual
 
 __all__ = [
-    "Aggregation", "ChempropBlock", "ChempropLayer", "GraphEmbedding", "Max", "Mean", "Min", "Sum", "Residual",
+    "Aggregation", "ChempropBlock", "ChempropLayer", "GraphEmbedding", "EmbeddedChempropBlock", "Max", "Mean", "Min", "Sum", "Residual",
 ]

@@ -174,13 +174,48 @@ def block_forward(
     """Run the kernel sequence; returns (node, H_d, states) with states = [(H_l, S_l)] for
     l = 0..d-1 (each layer's input hidden state and its aggregation) if keep_states, else []."""
     V = Xv.shape[0]
+    if len(weights) == 0:
+        H, _ = K.dmpnn_init(Xv, Xe, src)
+        return _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states)
+    H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
+    return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states)
+
+
+def block_forward_embedded(
+    node_table: Tensor,
+    node_types: Tensor,
+    edge_table: Tensor,
+    edge_types: Tensor,
+    src: Tensor,
+    rev: Tensor,
+    lay: DeviceLayout,
+    weights: Sequence[Tensor],
+    biases: Sequence[Optional[Tensor]],
+    act: tuple[int, float],
+    reduce: str,
+    residual: bool,
+    validate: bool = True,
+) -> tuple[Tensor, Tensor]:
+    """block_forward with GraphEmbedding fused into the initial gather (nt_dmpnn_init_embed):
+    Xv / Xe are never materialised.  Returns (node, H_d)."""
+    V = node_types.shape[0]
+    if len(weights) == 0:
+        H, _ = K.dmpnn_init_embed(node_table, node_types, edge_table, edge_types, src, validate=validate)
+        node, H, _ = _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, False)
+        return node, H
+    H, S = K.dmpnn_init_embed(node_table, node_types, edge_table, edge_types, src, lay.dst_ptr,
+                              lay.dst_perm, act=act, reduce=reduce, validate=validate)
+    node, H, _ = _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, False)
+    return node, H
+
+
+def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states):
+    """The d layers + final node scatter, from H0 and layer 0's aggregation S."""
     d = len(weights)
     if d == 0:
-        H, _ = K.dmpnn_init(Xv, Xe, src)
         node = K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=_IDENTITY)
         return node, H, []
     Wps = pack_layer_weights(weights)
-    H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
     E, h = H.shape
     plan = fused_plan(lay, V, E) if _fused_enabled() and K.fused_supported(V, E, h, H.dtype) else None
     if plan is not None:
