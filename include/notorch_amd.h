@@ -179,6 +179,27 @@ NT_API int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* sr
                                  int reduce, int agg_act, float agg_alpha, int dtype, void* H_out,
                                  void* S_out, void* stream);
 
+/*
+ * Attention readout scores (notorch/nn/gnn/agg.py:50-86), one per node row X[v] (n x h):
+ *   Gated        (a != NULL, Q == NULL): s[v] = X[v] . a + (a_bias ? *a_bias : 0)   (agg.py:53,59)
+ *   SDPAttention (Q != NULL, a == NULL): s[v] = (Q[node_seg[v]] . X[v]) / sqrt_key   (agg.py:79-82)
+ * a: h (the nn.Linear(d, 1) weight row), Q: nseg x h, node_seg = batch_node_index (int64);
+ * scores: n fp32.
+ */
+NT_API int nt_node_scores(const void* X, int64_t n, int64_t h, const void* a, const void* a_bias,
+                          const void* Q, const int64_t* node_seg, float sqrt_key, int dtype,
+                          float* scores, void* stream);
+
+/*
+ * Softmax-weighted segment sum (agg.py:60-61, :83-84: scatter_softmax then scatter_sum):
+ *   alpha[v] = exp(s[v] - max_g s) / sum_{u in g} exp(s[u] - max_g s)
+ *   out[g]   = sum_{v in g} alpha[v] X[v]          (ascending v; empty segment -> 0)
+ * (seg_ptr, perm) = nt_csr_build(batch_node_index, n, nseg); perm may be NULL if sorted.
+ */
+NT_API int nt_softmax_pool(const void* X, const float* scores, const int32_t* seg_ptr,
+                           const int32_t* perm, int64_t nseg, int64_t h, int dtype, void* out,
+                           void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Backward (training through ChempropBlock, lightning_models/model.py:224-241).  The reference's
  * backward is ATen autograd of chemprop.py:28-43,81-88 (index_backward = index_add, scatter_add

@@ -70,6 +70,10 @@ SIGNATURES: dict[str, tuple] = {
         [_vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _vp, _c_i64,
          _vp, _vp, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp],
     ),
+    "nt_node_scores": (
+        _c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_f32, _c_int, _vp, _vp],
+    ),
+    "nt_softmax_pool": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_int, _vp, _vp]),
     "nt_dmpnn_message": (
         _c_int,
         [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _c_int, _vp, _vp],

@@ -187,26 +187,78 @@ inline int lds_bytes_bf16(int KS) {
   return a > kStageB ? a : kStageB;
 }
 
-template <int ACT, int W, int NW>
+// Fused aggregation of the layer output (nt_dmpnn_update_fused): tiles are the tile plan's cuts of
+// the dst-sorted edge order, so every node's in-edges are consecutive rows of one tile.
+struct BfAgg {
+  const int* tile_ptr;   // ntiles + 1 positions
+  const int* perm;       // dst CSR permutation: position -> edge
+  const int* dsts;       // position -> destination node
+  int reduce, aact;
+  float aalpha;
+  bf16_t* S_out;         // V x h, rows of in-degree-0 nodes pre-zeroed by the caller
+};
+
+// S_out[node] piece = R over rows [r0, r1) of the staged values (already aact(stored H'))
+template <int R>
+__device__ __forceinline__ void reduce_rows(const float* stage, int r0, int r1, int c, float (&y)[8]) {
+  Reducer<R> red[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[q].init();
+  for (int r = r0; r < r1; ++r) {
+    const float* st = stage + r * kSO + c;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[q].push(st[q]);
+  }
+#pragma unroll
+  for (int q = 0; q < 8; ++q) y[q] = red[q].result();
+}
+
+// AGG: 0 = no aggregation; 1 = fused aggregation of the stored H' (final node scatter, identity);
+// 2 = fused aggregation of act(H') (the next layer's chemprop.py:37-39, same act as this layer)
+template <int ACT, int W, int NW, int AGG>
 __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     const bf16_t* __restrict__ H, const bf16_t* __restrict__ S, const int64_t* __restrict__ src,
     const int64_t* __restrict__ rev, const uint4* __restrict__ Wp, const bf16_t* __restrict__ bias,
     int64_t V, int64_t E, int h, int KS, int NTn, int residual, int act, float alpha,
-    bf16_t* __restrict__ out) {
+    bf16_t* __restrict__ out, BfAgg agg) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
-  __shared__ int64_t soff[kM], qoff[kM];
+  __shared__ int64_t soff[kM], qoff[kM], erow[kM];
+  __shared__ int nstart[kM + 1], nnode[kM], nseg;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  const int64_t e0 = (int64_t)blockIdx.x * kM;
   const int lda = a_row_bytes(KS);
 
   if (tid < kM) {
-    const int64_t e = e0 + tid;
+    int64_t e = -1;
+    if constexpr (AGG != 0) {
+      const int T = agg.tile_ptr[blockIdx.x], n = agg.tile_ptr[blockIdx.x + 1] - T;
+      int node = -1;
+      if (tid < n) {
+        e = agg.perm[T + tid];
+        node = agg.dsts[T + tid];
+      }
+      // segment starts of the tile's nodes (one wave: ballot + prefix popcount)
+      const bool first = tid < n && (tid == 0 || agg.dsts[T + tid - 1] != node);
+      const unsigned long long m = __ballot(first);
+      const int k = __popcll(m & ((1ull << tid) - 1ull));
+      if (first) {
+        nstart[k] = tid;
+        nnode[k] = node;
+      }
+      if (tid == 0) {
+        nseg = __popcll(m);
+        nstart[__popcll(m)] = n;
+      }
+    } else {
+      const int64_t e1 = (int64_t)blockIdx.x * kM + tid;
+      e = e1 < E ? e1 : -1;
+    }
     int64_t so = -1, qo = -1;
-    if (e < E) {
+    if (e >= 0) {
       const int64_t s = src[e], q = rev[e];
       if (s >= 0 && s < V) so = s * h;
       if (q >= 0 && q < E) qo = q * h;
     }
+    erow[tid] = e;
     soff[tid] = so;
     qoff[tid] = qo;
   }
@@ -224,7 +276,39 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
   __syncthreads();
 
   // ---- 1. gather A = S[src] - act(H[rev]) (fp32) -> bf16 LDS tile [64][Kp] ----
-  {
+  if constexpr (W == 8) {
+    // wave w owns rows 16 w .. 16 w + 15; lane c takes the c-th 16-B piece of each row, and all 32
+    // loads of the wave are issued before the first is consumed (latency hidden by depth)
+    const int chunks = KS * 4;
+    for (int c = lane; c < chunks; c += 64) {
+      const int k0 = c * 8;
+      const int kc = k0 < h ? k0 : h - 8;  // clamped, unconditional loads
+      uint4 sraw[16], qraw[16];
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int64_t so = soff[16 * w + u], qo = qoff[16 * w + u];
+        sraw[u] = *reinterpret_cast<const uint4*>(S + (so >= 0 ? so : 0) + kc);
+        qraw[u] = *reinterpret_cast<const uint4*>(H + (qo >= 0 ? qo : 0) + kc);
+      }
+#pragma unroll
+      for (int u = 0; u < 16; ++u) {
+        const int r = 16 * w + u;
+        const bool sok = soff[r] >= 0 && k0 < h, qok = qoff[r] >= 0 && k0 < h;
+        const unsigned su[4] = {sraw[u].x, sraw[u].y, sraw[u].z, sraw[u].w};
+        const unsigned qu[4] = {qraw[u].x, qraw[u].y, qraw[u].z, qraw[u].w};
+        bf16x8 a;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const unsigned sb = (i & 1) ? (su[i >> 1] & 0xffff0000u) : (su[i >> 1] << 16);
+          const unsigned qb = (i & 1) ? (qu[i >> 1] & 0xffff0000u) : (qu[i >> 1] << 16);
+          const float sv = sok ? __uint_as_float(sb) : 0.f;
+          const float qv = qok ? __uint_as_float(qb) : 0.f;
+          a[i] = (__bf16)(sv - act_t<ACT>(qv, act, alpha));
+        }
+        *reinterpret_cast<uint4*>(lds + r * lda + c * 16) = __builtin_bit_cast(uint4, a);
+      }
+    }
+  } else {
     const int chunks = KS * 4;  // 8-element pieces per padded row
     constexpr int kRU = 4;      // rows in flight per wave
     for (int r0 = w * kRU; r0 < kM; r0 += 4 * kRU) {
@@ -234,24 +318,11 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
 #pragma unroll
         for (int u = 0; u < kRU; ++u) {
           const int64_t so = soff[r0 + u], qo = qoff[r0 + u];
-          if constexpr (W == 8) {
-            // clamped, unconditional loads; out-of-range pieces are zeroed after the load
-            const int kc = k0 < h ? k0 : h - 8;
-            load_chunk<8>(S + (so >= 0 ? so : 0) + kc, sv[u]);
-            load_chunk<8>(H + (qo >= 0 ? qo : 0) + kc, qv[u]);
-            const bool sok = so >= 0 && k0 < h, qok = qo >= 0 && k0 < h;
 #pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              sv[u][i] = sok ? sv[u][i] : 0.f;
-              qv[u][i] = qok ? qv[u][i] : 0.f;
-            }
-          } else {
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-              const bool in = k0 + i < h;
-              sv[u][i] = (in && so >= 0) ? bf2f(S[so + k0 + i]) : 0.f;
-              qv[u][i] = (in && qo >= 0) ? bf2f(H[qo + k0 + i]) : 0.f;
-            }
+          for (int i = 0; i < 8; ++i) {
+            const bool in = k0 + i < h;
+            sv[u][i] = (in && so >= 0) ? bf2f(S[so + k0 + i]) : 0.f;
+            qv[u][i] = (in && qo >= 0) ? bf2f(H[qo + k0 + i]) : 0.f;
           }
         }
 #pragma unroll
@@ -302,6 +373,22 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
 #pragma unroll
   for (int p = 0; p < (NW + 3) / 4; ++p) {
     if (p * 256 >= Np) break;
+    const int n0 = 256 * p;
+    const int ncols = h - n0 < 256 ? h - n0 : 256;
+    // W == 8: thread (tid) owns column piece c = 8 (tid & 31) of rows (tid >> 5) + 8 it, it < 8;
+    // its residual pieces are loaded before the staging round trip so their latency overlaps it
+    constexpr int kIt = kM * 32 / kThreads;
+    const int cpiece = 8 * (tid & 31);
+    const bool cok = cpiece < ncols;
+    uint4 hres[kIt];
+    if constexpr (W == 8) {
+#pragma unroll
+      for (int it = 0; it < kIt; ++it) {
+        const int64_t e = erow[(tid >> 5) + 8 * it];
+        const bool ok = cok && e >= 0 && residual;
+        hres[it] = *reinterpret_cast<const uint4*>(H + (ok ? e * h + n0 + cpiece : 0));
+      }
+    }
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
       const int j = 4 * p + jj;
@@ -314,35 +401,49 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
       }
     }
     __syncthreads();
-    const int n0 = 256 * p;
-    const int ncols = h - n0 < 256 ? h - n0 : 256;
     if constexpr (W == 8) {
-      for (int i = tid; i < kM * 32; i += kThreads) {
-        const int r = i >> 5, c = (i & 31) * 8;
-        const int64_t e = e0 + r;
-        if (c < ncols && e < E) {
-          float y[8], hres[8], bb[8];
-          const float* st = stage + r * kSO + c;
+      float bb[8];
+      if (bias && cok) load_chunk<8>(bias + n0 + cpiece, bb);
+      else for (int q = 0; q < 8; ++q) bb[q] = 0.f;
 #pragma unroll
-          for (int q = 0; q < 8; ++q) y[q] = st[q];
-          if (bias) {
-            load_chunk<8>(bias + n0 + c, bb);
+      for (int it = 0; it < kIt; ++it) {
+        const int r = (tid >> 5) + 8 * it;
+        const int64_t e = erow[r];
+        if (cok && e >= 0) {
+          float* st = stage + r * kSO + cpiece;
+          const unsigned hu[4] = {hres[it].x, hres[it].y, hres[it].z, hres[it].w};
+          float y[8];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) y[q] += bb[q];
+          for (int q = 0; q < 8; ++q) {
+            const unsigned hb = (q & 1) ? (hu[q >> 1] & 0xffff0000u) : (hu[q >> 1] << 16);
+            y[q] = st[q] + bb[q] + (residual ? __uint_as_float(hb) : 0.f);
           }
-          if (residual) {
-            load_chunk<8>(H + e * h + n0 + c, hres);
+          store_chunk<8>(out + e * h + n0 + cpiece, y);
+          if constexpr (AGG != 0) {  // the aggregation reads the stored (bf16) value, as unfused
 #pragma unroll
-            for (int q = 0; q < 8; ++q) y[q] += hres[q];
+            for (int q = 0; q < 8; ++q) st[q] = AGG == 2 ? act_t<ACT>(rbf(y[q]), act, alpha) : rbf(y[q]);
           }
-          store_chunk<8>(out + e * h + n0 + c, y);
+        }
+      }
+      if constexpr (AGG != 0) {
+        __syncthreads();
+        for (int k = tid >> 5; k < nseg; k += kThreads / 32) {
+          if (!cok) continue;
+          float y[8];
+          switch (agg.reduce) {
+            case NT_SUM: reduce_rows<NT_SUM>(stage, nstart[k], nstart[k + 1], cpiece, y); break;
+            case NT_MEAN: reduce_rows<NT_MEAN>(stage, nstart[k], nstart[k + 1], cpiece, y); break;
+            case NT_MAX: reduce_rows<NT_MAX>(stage, nstart[k], nstart[k + 1], cpiece, y); break;
+            default: reduce_rows<NT_MIN>(stage, nstart[k], nstart[k + 1], cpiece, y); break;
+          }
+          store_chunk<8>(agg.S_out + (int64_t)nnode[k] * h + n0 + cpiece, y);
         }
       }
     } else {
       for (int i = tid; i < kM * 256; i += kThreads) {
         const int r = i >> 8, c = i & 255;
-        const int64_t e = e0 + r;
-        if (c < ncols && e < E) {
+        const int64_t e = erow[r];
+        if (c < ncols && e >= 0) {
           float y = stage[r * kSO + c];
           if (bias) y += bf2f(bias[n0 + c]);
           if (residual) y += bf2f(H[e * h + n0 + c]);
@@ -372,19 +473,18 @@ static bool valid_reduce(int r) { return r >= NT_SUM && r <= NT_MIN; }
     }                                                                                           \
   } while (0)
 
-template <int ACT, int W, int NW>
+template <int ACT, int W, int NW, int AGG>
 int launch_upd(const void* H, const void* S, const int64_t* src, const int64_t* rev, const void* Wp,
                const void* b, int64_t V, int64_t E, int64_t h, int residual, int act, float alpha,
-               void* H_out, hipStream_t stream) {
+               void* H_out, int64_t grid, const BfAgg& agg, hipStream_t stream) {
   const int KS = (int)((h + 31) / 32), NTn = (int)((h + 15) / 16);
-  const int64_t grid = (E + kM - 1) / kM;
   const int lds = lds_bytes_bf16(KS);
-  auto kern = update_bf16_kernel<ACT, W, NW>;
+  auto kern = update_bf16_kernel<ACT, W, NW, AGG>;
   if (lds > 64 * 1024)
     NT_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   kern<<<(unsigned)grid, kThreads, lds, stream>>>(
       (const bf16_t*)H, (const bf16_t*)S, src, rev, (const uint4*)Wp, (const bf16_t*)b, V, E, (int)h,
-      KS, NTn, residual, act, alpha, (bf16_t*)H_out);
+      KS, NTn, residual, act, alpha, (bf16_t*)H_out, agg);
   NT_LAUNCH_CHECK();
   return NT_OK;
 }
@@ -464,14 +564,17 @@ int pack_weight_bf16(const void* W, int64_t nlayers, int64_t h, int64_t layer_st
   return NT_OK;
 }
 
-template <int ACT, int W>
+template <int ACT, int W, int AGG>
 static int launch_upd_nw(const void* H, const void* S, const int64_t* src, const int64_t* rev,
-                  const void* Wp, const void* b, int64_t V, int64_t E, int64_t h, int residual,
-                  int act, float alpha, void* H_out, hipStream_t stream) {
+                         const void* Wp, const void* b, int64_t V, int64_t E, int64_t h, int residual,
+                         int act, float alpha, void* H_out, int64_t grid, const BfAgg& agg,
+                         hipStream_t stream) {
   const int nw = (int)(((h + 15) / 16 + 3) / 4);
   switch (nw) {
-#define NT_NW(N) \
-  case N: return launch_upd<ACT, W, N>(H, S, src, rev, Wp, b, V, E, h, residual, act, alpha, H_out, stream);
+#define NT_NW(N)                                                                                  \
+  case N:                                                                                         \
+    return launch_upd<ACT, W, N, AGG>(H, S, src, rev, Wp, b, V, E, h, residual, act, alpha, H_out, \
+                                      grid, agg, stream);
     NT_NW(1) NT_NW(2) NT_NW(3) NT_NW(4) NT_NW(5) NT_NW(6) NT_NW(7) NT_NW(8)
 #undef NT_NW
   }
@@ -483,15 +586,44 @@ int launch_update_bf16(const void* H, const void* S, const int64_t* src, const i
                        const void* Wp, const void* b, int64_t V, int64_t E, int64_t h, int residual,
                        int act, float alpha, void* H_out, hipStream_t stream) {
   NT_REQUIRE(h <= 4 * kNWMax * 16, NT_EUNSUPPORTED, "bf16 update supports h <= 512");
-  NT_REQUIRE((E + kM - 1) / kM < (int64_t(1) << 31), NT_EINVAL, "too many edges");
+  const int64_t grid = (E + kM - 1) / kM;
+  NT_REQUIRE(grid < (int64_t(1) << 31), NT_EINVAL, "too many edges");
   const bool vec = h % 8 == 0 && aligned16(H) && aligned16(S) && aligned16(H_out) &&
                    (b == nullptr || aligned16(b));
+  const BfAgg none{nullptr, nullptr, nullptr, 0, 0, 0.f, nullptr};
   if (vec)
-    NT_BF_DISPATCH_A(act, return (launch_upd_nw<A_, 8>(H, S, src, rev, Wp, b, V, E, h, residual,
-                                                       act, alpha, H_out, stream)));
+    NT_BF_DISPATCH_A(act, return (launch_upd_nw<A_, 8, 0>(H, S, src, rev, Wp, b, V, E, h, residual,
+                                                              act, alpha, H_out, grid, none, stream)));
   else
-    NT_BF_DISPATCH_A(act, return (launch_upd_nw<A_, 1>(H, S, src, rev, Wp, b, V, E, h, residual,
-                                                       act, alpha, H_out, stream)));
+    NT_BF_DISPATCH_A(act, return (launch_upd_nw<A_, 1, 0>(H, S, src, rev, Wp, b, V, E, h, residual,
+                                                              act, alpha, H_out, grid, none, stream)));
+  return NT_OK;
+}
+
+bool bf16_fused_supported(int64_t h) { return h % 8 == 0 && h <= 4 * kNWMax * 16; }
+
+int launch_update_bf16_fused(const void* H, const void* S, const int64_t* src, const int64_t* rev,
+                             const void* Wp, const void* b, int64_t V, int64_t E, int64_t h,
+                             int residual, int act, float alpha, const int32_t* tile_ptr,
+                             int64_t ntiles, const int32_t* perm, const int32_t* dsts, int reduce,
+                             int aact, float aalpha, void* H_out, void* S_out, hipStream_t stream) {
+  if (tile_ptr == nullptr)  // no plan: the plain (unfused) kernel computes H_out only
+    return launch_update_bf16(H, S, src, rev, Wp, b, V, E, h, residual, act, alpha, H_out, stream);
+  NT_REQUIRE(bf16_fused_supported(h), NT_EUNSUPPORTED, "bf16 update_fused needs h % 8 == 0, h <= 512");
+  NT_REQUIRE(perm && dsts && S_out && aligned16(S_out), NT_EINVAL, "fused aggregation needs perm, "
+             "dst_sorted and a 16-byte aligned S_out");
+  NT_REQUIRE(ntiles > 0 && ntiles < (int64_t(1) << 31), NT_EINVAL, "bad ntiles");
+  // the kernel applies either identity (final node scatter) or this layer's own act (the next
+  // layer's aggregation, which ChempropBlock guarantees uses the same activation)
+  NT_REQUIRE(aact == NT_ACT_IDENTITY || (aact == act && aalpha == alpha), NT_EUNSUPPORTED,
+             "bf16 update_fused: agg_act must be identity or equal to act");
+  const BfAgg agg{tile_ptr, perm, dsts, reduce, aact, aalpha, (bf16_t*)S_out};
+  if (aact == NT_ACT_IDENTITY)
+    NT_BF_DISPATCH_A(act, return (launch_upd_nw<A_, 8, 1>(H, S, src, rev, Wp, b, V, E, h, residual,
+                                                          act, alpha, H_out, ntiles, agg, stream)));
+  else
+    NT_BF_DISPATCH_A(act, return (launch_upd_nw<A_, 8, 2>(H, S, src, rev, Wp, b, V, E, h, residual,
+                                                          act, alpha, H_out, ntiles, agg, stream)));
   return NT_OK;
 }
 

@@ -24,4 +24,12 @@ int launch_update_bf16(const void* H, const void* S, const int64_t* src, const i
                        const void* Wp, const void* b, int64_t V, int64_t E, int64_t h, int residual,
                        int act, float alpha, void* H_out, hipStream_t stream);
 
+// fused with the aggregation its output feeds (tile plan of nt_dmpnn_tile_plan); h % 8 == 0, <= 512
+bool bf16_fused_supported(int64_t h);
+int launch_update_bf16_fused(const void* H, const void* S, const int64_t* src, const int64_t* rev,
+                             const void* Wp, const void* b, int64_t V, int64_t E, int64_t h,
+                             int residual, int act, float alpha, const int32_t* tile_ptr,
+                             int64_t ntiles, const int32_t* perm, const int32_t* dsts, int reduce,
+                             int aact, float aalpha, void* H_out, void* S_out, hipStream_t stream);
+
 }  // namespace nt

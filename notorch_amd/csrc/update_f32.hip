@@ -627,18 +627,23 @@ extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t
                                      void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented for update_fused");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
   NT_REQUIRE(agg_act >= NT_ACT_IDENTITY && agg_act <= NT_ACT_SIGMOID, NT_EINVAL, "bad agg_act code");
   NT_REQUIRE(reduce >= NT_SUM && reduce <= NT_MIN, NT_EINVAL, "bad reduce code");
   NT_REQUIRE(V >= 0 && E >= 0 && E < (int64_t(1) << 31) && h > 0, NT_EINVAL, "bad sizes");
-  NT_REQUIRE(ps_supported(h), NT_EUNSUPPORTED, "update_fused needs h % 4 == 0 and h <= 304");
+  NT_REQUIRE(dtype == NT_BF16 ? bf16_fused_supported(h) : ps_supported(h), NT_EUNSUPPORTED,
+             "update_fused needs h % 4 == 0 and h <= 304 (fp32), h % 8 == 0 and h <= 512 (bf16)");
   if (E == 0) return NT_OK;
   NT_REQUIRE(H && S && src && rev && Wp && H_out, NT_EINVAL, "NULL pointer");
   NT_REQUIRE(H != H_out && (S_out == nullptr || S_out != S), NT_EINVAL, "outputs alias inputs");
   NT_REQUIRE(aligned16(H) && aligned16(S) && aligned16(H_out) && aligned16(Wp) &&
                  (b == nullptr || aligned16(b)) && (S_out == nullptr || aligned16(S_out)),
              NT_EINVAL, "feature pointers must be 16-byte aligned");
+  if (dtype == NT_BF16)
+    return launch_update_bf16_fused(H, S, src, rev, Wp, b, V, E, h, residual, act, act_alpha,
+                                    tile_ptr, ntiles, perm, dst_sorted, reduce, agg_act, agg_alpha,
+                                    H_out, S_out, as_stream(stream_));
   const UpdateGeom g = geom_for(h);
   UpdateArgs a{(const float*)H, (const float*)S, src, rev,
                (const char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), (const float*)b, V, E, h,

@@ -29,6 +29,8 @@ __all__ = [
     "gather_rows",
     "embed_bag",
     "dmpnn_init_embed",
+    "node_scores",
+    "softmax_pool",
 ]
 
 
@@ -286,7 +288,10 @@ def dmpnn_update(
 
 
 def fused_supported(V: int, E: int, h: int, dtype: torch.dtype = torch.float32) -> bool:
-    """Shapes the fused persistent kernel (nt_dmpnn_update_fused, fp32 only) accepts."""
+    """Shapes nt_dmpnn_update_fused accepts: the fp32 persistent kernel (h % 4 == 0, h <= 304) or
+    the bf16 tile kernel (h % 8 == 0, h <= 512)."""
+    if dtype == torch.bfloat16:
+        return h % 8 == 0 and 8 <= h <= 512 and E < 2**31
     return (dtype == torch.float32 and h % 4 == 0 and 4 <= h <= 304 and E * h // 4 < 2**31
             and V * h // 4 < 2**31 and E < 2**31)
 
@@ -332,18 +337,18 @@ def dmpnn_update_fused(
 
     ``zero_fill`` must be True when some node has no in-edge (its S_out row is then 0)."""
     dev = _require_device(H, S, src, rev, Wp, bias, out, S_out, perm)
-    _require_f32("H", H)
-    _require_f32("S", S)
+    code = _require_feat("H", H)
+    _require_feat("S", S, H.dtype)
     _require_i64("src", src)
     _require_i64("rev_index", rev)
     E, h = H.shape
     V = S.shape[0]
     if S.shape[1] != h or src.numel() != E or rev.numel() != E:
         raise ValueError("shape mismatch between H, S, src and rev_index")
-    if Wp.numel() != packed_weight_numel(h):
-        raise ValueError("Wp is not a packed weight image for this hidden size")
+    if Wp.numel() != packed_weight_numel(h, H.dtype):
+        raise ValueError(f"Wp is not a packed {H.dtype} weight image for this hidden size")
     if bias is not None:
-        _require_f32("bias", bias)
+        _require_feat("bias", bias, H.dtype)
         if bias.numel() != h:
             raise ValueError("bias must have h entries")
     if out is None:
@@ -366,7 +371,7 @@ def dmpnn_update_fused(
         lib.nt_dmpnn_update_fused(
             _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
             act[0], act[1], _ptr(tile_ptr), ntiles, _ptr(perm), _ptr(dsts), reduce_code(reduce),
-            agg_act[0], agg_act[1], NT_F32, _ptr(out), _ptr(S_out), _stream(dev),
+            agg_act[0], agg_act[1], code, _ptr(out), _ptr(S_out), _stream(dev),
         )
     )
     return out, S_out
@@ -509,3 +514,51 @@ def dmpnn_init_embed(
         act[0], act[1], reduce_code(reduce), code, _ptr(H0), _ptr(S), _stream(dev),
     ))
     return H0, S
+
+
+# ------------------------------------------------------------------------------------ attention readouts
+def node_scores(X: Tensor, *, a: Tensor | None = None, a_bias: Tensor | None = None,
+                Q: Tensor | None = None, node_seg: Tensor | None = None,
+                sqrt_key: float = 1.0) -> Tensor:
+    """Per-node readout scores (fp32): X @ a + a_bias (Gated) or (Q[node_seg] * X).sum(1) / sqrt_key
+    (SDPAttention)."""
+    dev = _require_device(X, a, a_bias, Q, node_seg)
+    code = _require_feat("X", X)
+    n, h = X.shape
+    if (a is None) == (Q is None):
+        raise ValueError("pass exactly one of a (Gated) and Q (SDPAttention)")
+    if a is not None:
+        _require_feat("a", a, X.dtype)
+        if a.numel() != h:
+            raise ValueError("a must have h entries")
+        if a_bias is not None:
+            _require_feat("a_bias", a_bias, X.dtype)
+    else:
+        _require_feat("Q", Q, X.dtype)
+        if Q.dim() != 2 or Q.shape[1] != h:
+            raise RuntimeError(f"Q must be b x {h}, got {tuple(Q.shape)}")
+        if node_seg is None:
+            raise ValueError("SDPAttention scores need batch_node_index")
+        _require_i64("batch_node_index", node_seg)
+    s = torch.empty(n, dtype=torch.float32, device=dev)
+    check(_lib.load().nt_node_scores(
+        _ptr(X), n, h, _ptr(a), _ptr(a_bias), _ptr(Q), _ptr(node_seg), float(sqrt_key), code,
+        _ptr(s), _stream(dev),
+    ))
+    return s
+
+
+def softmax_pool(X: Tensor, scores: Tensor, seg_ptr: Tensor, perm: Tensor | None, nseg: int) -> Tensor:
+    """out[g] = sum over v in segment g of softmax_g(scores)[v] * X[v]."""
+    dev = _require_device(X, scores, seg_ptr, perm)
+    code = _require_feat("X", X)
+    if scores.dtype != torch.float32 or scores.numel() != X.shape[0]:
+        raise ValueError("scores must be fp32 with one entry per row of X")
+    if seg_ptr.dtype != torch.int32 or seg_ptr.numel() != nseg + 1:
+        raise ValueError("seg_ptr must be int32 of length nseg + 1")
+    h = X.shape[1]
+    out = torch.empty(nseg, h, dtype=X.dtype, device=dev)
+    check(_lib.load().nt_softmax_pool(
+        _ptr(X), _ptr(scores), _ptr(seg_ptr), _ptr(perm), nseg, h, code, _ptr(out), _stream(dev)
+    ))
+    return out

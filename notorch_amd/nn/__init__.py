@@ -3,7 +3,9 @@ from notorch_amd.nn.gnn import (
     ChempropBlock,
     ChempropLayer,
     EmbeddedChempropBlock,
+    Gated,
     GraphEmbedding,
+    SDPAttention,
     Max,
     Mean,
     Min,
@@ -12,5 +14,5 @@ from notorch_amd.nn.gnn import (
 from notorch_amd.nn.residual import Residual
 
 __all__ = [
-    "Aggregation", "ChempropBlock", "ChempropLayer", "GraphEmbedding", "EmbeddedChempropBlock", "Max", "Mean", "Min", "Sum", "Residual",
+    "Aggregation", "Gated", "SDPAttention", "ChempropBlock", "ChempropLayer", "GraphEmbedding", "EmbeddedChempropBlock", "Max", "Mean", "Min", "Sum", "Residual",
 ]

@@ -5,16 +5,26 @@
 ``max(count, 1)``, an empty molecule reads 0 for every reduction.  ``Min`` is added for
 completeness of the ``Reduction`` domain (notorch/types.py:57).
 
-``Gated`` and ``SDPAttention`` (agg.py:50-86) are SURVEY §8(f) row 4 — not provided yet.
+``Gated`` and ``SDPAttention`` (agg.py:50-86) weight the nodes of each molecule
+by a per-molecule softmax of a node score (``nt_node_scores`` then ``nt_softmax_pool``).  ``Gated``
+uses alpha as the (V, 1) node weight agg.py:59-61 evidently means: the reference's extra
+``.unsqueeze(1)`` turns alpha into (V, 1, 1), which broadcasts against (V, d) into a (V, V, d) tensor
+and returns (b, V, d) — O(b V d) memory and not a readout.  This is the one documented divergence.
+Training through them runs the same math in device ops under autograd (recompute backward).
 """
 from __future__ import annotations
 
 from abc import abstractmethod
+from math import sqrt
 
+import torch
 import torch.nn as nn
 from torch import Tensor
 
+from notorch_amd import kernels as K
 from notorch_amd.nn.gnn import _engine
+
+DEFAULT_HIDDEN_DIM = 256  # notorch/conf.py
 
 
 class Aggregation(nn.Module):
@@ -58,3 +68,66 @@ class Max(_SegmentReadout):
 
 class Min(_SegmentReadout):
     reduce = "min"
+
+
+def _softmax_pool_torch(X: Tensor, scores: Tensor, bni: Tensor, B: int) -> Tensor:
+    """The same readout in device ops (autograd path): scatter_softmax + scatter_sum."""
+    idx = bni.view(-1)
+    mx = torch.full((B,), float("-inf"), dtype=scores.dtype, device=scores.device)
+    mx = mx.scatter_reduce(0, idx, scores, reduce="amax", include_self=True)
+    rec = (scores - mx[idx]).exp()
+    z = torch.zeros(B, dtype=scores.dtype, device=scores.device).scatter_add(0, idx, rec)
+    alpha = (rec / z[idx]).unsqueeze(1).to(X.dtype)
+    out = torch.zeros(B, X.shape[1], dtype=X.dtype, device=X.device)
+    return out.scatter_add(0, idx.view(-1, 1).expand_as(X), alpha * X)
+
+
+class _AttentionReadout(Aggregation):
+    def _pool(self, G, scores_fn, torch_scores_fn) -> Tensor:
+        X = G.node_feats
+        if X.device.type != "cuda":
+            raise RuntimeError(
+                f"notorch_amd.{type(self).__name__} runs on ROCm devices only; got '{X.device}'"
+            )
+        X = X.contiguous()
+        B = len(G)
+        needs_grad = torch.is_grad_enabled() and (
+            X.requires_grad or any(p.requires_grad for p in self.parameters()))
+        if needs_grad:
+            return _softmax_pool_torch(X, torch_scores_fn(X), G.batch_node_index, B)
+        mol_ptr, mol_perm = _engine.mol_layout(G)
+        return K.softmax_pool(X, scores_fn(X), mol_ptr, mol_perm, B)
+
+
+class Gated(_AttentionReadout):
+    """agg.py:50-63: alpha = softmax over each molecule of a(x_v); out[g] = sum_v alpha_v x_v."""
+
+    def __init__(self, input_dim: int = DEFAULT_HIDDEN_DIM):
+        super().__init__()
+        self.a = nn.Linear(input_dim, 1)
+
+    def forward(self, G, **kwargs) -> Tensor:
+        w, b = self.a.weight, self.a.bias
+        return self._pool(
+            G,
+            lambda X: K.node_scores(X, a=w.detach().reshape(-1).contiguous(),
+                                    a_bias=None if b is None else b.detach()),
+            lambda X: self.a(X).squeeze(-1).float(),
+        )
+
+
+class SDPAttention(_AttentionReadout):
+    """agg.py:66-86: scores = <Q[batch v], x_v> / sqrt(key_dim), softmax per molecule, weighted sum."""
+
+    def __init__(self, key_dim: int = DEFAULT_HIDDEN_DIM):
+        super().__init__()
+        self.sqrt_key_dim = sqrt(key_dim)
+
+    def forward(self, G, *, Q: Tensor, **kwargs) -> Tensor:
+        bni = G.batch_node_index
+        return self._pool(
+            G,
+            lambda X: K.node_scores(X, Q=Q.contiguous(), node_seg=bni.contiguous(),
+                                    sqrt_key=self.sqrt_key_dim),
+            lambda X: (torch.einsum("vd,vd->v", Q[bni], X) / self.sqrt_key_dim).float(),
+        )

@@ -11,6 +11,7 @@ Op for op, in the reference's order and on the same ATen kernels the reference d
 * ``chemprop_layer``     notorch/nn/gnn/chemprop.py:28-43
 * ``chemprop_block``     notorch/nn/gnn/chemprop.py:81-88 with Residual (notorch/nn/residual.py:27-28)
 * ``readout``            notorch/nn/gnn/agg.py:23-47 (Sum / Mean / Max)
+* ``readout_gated`` / ``readout_sdpa``   agg.py:50-86 (Gated / SDPAttention, scatter_softmax)
 """
 from __future__ import annotations
 
@@ -84,6 +85,33 @@ def chemprop_block(
 def readout(node_feats: Tensor, batch_node_index: Tensor, size: int, kind: str = "sum") -> Tensor:
     """agg.py:23-47: Sum / Mean / Max (+ Min) over molecules."""
     return scatter(node_feats, batch_node_index, dim_size=size, reduce=kind)
+
+
+def scatter_softmax(src: Tensor, index: Tensor, dim_size: int) -> Tensor:
+    """torch_scatter composite/softmax.py scatter_softmax along dim 0 (1-D scores):
+    exp(src - max_g) / sum_g exp(src - max_g), the max and sum by scatter."""
+    mx = scatter(src, index, dim_size, "max")
+    rec = (src - mx[index]).exp()
+    return rec / scatter(rec, index, dim_size, "sum")[index]
+
+
+def readout_gated(node_feats: Tensor, batch_node_index: Tensor, size: int, a_weight: Tensor,
+                  a_bias: Optional[Tensor]) -> Tensor:
+    """agg.py:50-63 with alpha used as the (V, 1) node weight it evidently means: scores = a(x)
+    (:59), alpha = scatter_softmax(scores) (:60), out = scatter_sum(alpha * x) (:61).  The
+    reference's extra .unsqueeze(1) broadcasts (V,1,1) * (V,d) to (V,V,d); that shape
+    bug is not restated."""
+    scores = torch.nn.functional.linear(node_feats, a_weight, a_bias).squeeze(-1)
+    alpha = scatter_softmax(scores, batch_node_index, size).unsqueeze(1)
+    return scatter(alpha * node_feats, batch_node_index, size, "sum")
+
+
+def readout_sdpa(node_feats: Tensor, batch_node_index: Tensor, size: int, Q: Tensor,
+                 sqrt_key_dim: float) -> Tensor:
+    """agg.py:66-86: scores = <Q[batch v], x_v> / sqrt(key_dim); softmax per molecule; weighted sum."""
+    scores = torch.einsum("vd,vd->v", Q[batch_node_index], node_feats) / sqrt_key_dim
+    alpha = scatter_softmax(scores, batch_node_index, size).unsqueeze(1)
+    return scatter(alpha * node_feats, batch_node_index, size, "sum")
 
 
 def block_params(module) -> tuple[list, list]:

@@ -195,3 +195,29 @@ def test_block_bf16_trains_through_recompute_backward():
     out.float().pow(2).sum().backward()
     for p in [Xv, Xe] + list(blk.parameters()):
         assert p.grad is not None and p.grad.dtype == BF and torch.isfinite(p.grad.float()).all()
+
+
+# ------------------------------------------------------------------ fused update + aggregation
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+@pytest.mark.parametrize("h", [512, 96])
+def test_block_bf16_fused_bit_identical_to_unfused(monkeypatch, reduce, h):
+    """nt_dmpnn_update_fused (bf16 tile kernel with the next layer's aggregation in its epilogue)
+    gives exactly the bytes of the unfused update + segment_reduce sequence."""
+    from notorch_amd import kernels as K
+    from notorch_amd.nn import ChempropBlock
+    from notorch_amd.nn.gnn import _engine
+
+    G = _graph("zinc", 256, seed=9)
+    torch.manual_seed(2)
+    blk = ChempropBlock(hidden_dim=h, depth=3, reduce=reduce).eval().to(BF).to(DEV)
+    Xv = torch.randn(G.num_nodes, h).to(BF)
+    Xe = torch.randn(G.num_edges, h).to(BF)
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
+    assert K.fused_supported(G.num_nodes, G.num_edges, h, BF)
+    with torch.no_grad():
+        fused = blk(Gd)
+        assert _engine.fused_plan(Gd._nt_layout, G.num_nodes, G.num_edges) is not None
+        monkeypatch.setenv("NT_FUSED", "0")
+        unfused = blk(Gd)
+    assert torch.equal(fused.edge_feats, unfused.edge_feats)
+    assert torch.equal(fused.node_feats, unfused.node_feats)

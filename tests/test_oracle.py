@@ -58,3 +58,20 @@ def test_fp32_vs_fp64_noise_floor():
     z = load_golden("config1.npz")
     assert z["err64_node"] / abs(z["out_node"]).max() <= FP32_NORM_TOL
     assert z["err64_edge"] / abs(z["out_edge"]).max() <= FP32_NORM_TOL
+
+
+def test_scatter_softmax_hand_case():
+    """torch_scatter scatter_softmax restatement on a hand-checkable case (molecules {0,1,2}, {3},
+    {} ): each molecule's weights are a softmax of its own scores, an empty molecule gets none."""
+    import math
+
+    s = torch.tensor([0.0, math.log(2.0), math.log(3.0), 5.0])
+    idx = torch.tensor([0, 0, 0, 1])
+    got = dmpnn_ref.scatter_softmax(s, idx, 3)
+    assert torch.allclose(got, torch.tensor([1 / 6, 2 / 6, 3 / 6, 1.0]), atol=1e-7)
+    X = torch.tensor([[6.0, 0.0], [0.0, 6.0], [6.0, 6.0], [1.0, 2.0]])
+    out = dmpnn_ref.readout_gated(X, idx, 3, torch.zeros(1, 2), torch.zeros(1))  # uniform alpha
+    assert torch.allclose(out, torch.tensor([[4.0, 4.0], [1.0, 2.0], [0.0, 0.0]]))
+    Q = torch.tensor([[0.0, 0.0], [1.0, 1.0], [0.0, 0.0]])
+    out = dmpnn_ref.readout_sdpa(X, idx, 3, Q, 2.0)  # molecule 0: Q = 0 -> uniform
+    assert torch.allclose(out, torch.tensor([[4.0, 4.0], [1.0, 2.0], [0.0, 0.0]]))
