@@ -22,6 +22,9 @@
 #include "bf16.hpp"
 
 namespace nt {
+
+int cu_count();  // update_ps.hip
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -220,79 +223,109 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     const bf16_t* __restrict__ H, const bf16_t* __restrict__ S, const int64_t* __restrict__ src,
     const int64_t* __restrict__ rev, const uint4* __restrict__ Wp, const bf16_t* __restrict__ bias,
     int64_t V, int64_t E, int h, int KS, int NTn, int residual, int act, float alpha,
-    bf16_t* __restrict__ out, BfAgg agg) {
+    bf16_t* __restrict__ out, BfAgg agg, int ntiles) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ int64_t soff[kM], qoff[kM], erow[kM];
   __shared__ int nstart[kM + 1], nnode[kM], nseg;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int lda = a_row_bytes(KS);
-
-  if (tid < kM) {
-    int64_t e = -1;
-    if constexpr (AGG != 0) {
-      const int T = agg.tile_ptr[blockIdx.x], n = agg.tile_ptr[blockIdx.x + 1] - T;
-      int node = -1;
-      if (tid < n) {
-        e = agg.perm[T + tid];
-        node = agg.dsts[T + tid];
-      }
-      // segment starts of the tile's nodes (one wave: ballot + prefix popcount)
-      const bool first = tid < n && (tid == 0 || agg.dsts[T + tid - 1] != node);
-      const unsigned long long m = __ballot(first);
-      const int k = __popcll(m & ((1ull << tid) - 1ull));
-      if (first) {
-        nstart[k] = tid;
-        nnode[k] = node;
-      }
-      if (tid == 0) {
-        nseg = __popcll(m);
-        nstart[__popcll(m)] = n;
-      }
-    } else {
-      const int64_t e1 = (int64_t)blockIdx.x * kM + tid;
-      e = e1 < E ? e1 : -1;
-    }
-    int64_t so = -1, qo = -1;
-    if (e >= 0) {
-      const int64_t s = src[e], q = rev[e];
-      if (s >= 0 && s < V) so = s * h;
-      if (q >= 0 && q < E) qo = q * h;
-    }
-    erow[tid] = e;
-    soff[tid] = so;
-    qoff[tid] = qo;
-  }
+  const int G = gridDim.x;
   // Column tile j of this wave is nt = w + 4 j, j < NW.  A wave's last tile may lie past NTn (h not
   // a multiple of 64): its loads are clamped to a valid fragment and its result is never stored,
   // so every load and MFMA below is unconditional (no branch for hipcc to drain vmcnt in front of).
-  int boff[NW];
-#pragma unroll
-  for (int j = 0; j < NW; ++j) boff[j] = (w + 4 * j < NTn ? w + 4 * j : NTn - 1) * 64 + lane;
+  // (recomputed where used, not kept in registers: the column tile of fragment j, clamped)
+  auto boff = [&](int j) { return (w + 4 * j < NTn ? w + 4 * j : NTn - 1) * 64 + lane; };
   const int64_t kstride = (int64_t)NTn * 64;
-  // B fragments of the first k step, in flight during the gather
-  uint4 bcur[NW];
+
+  // Persistent loop over tiles t = blockIdx.x + i G.  Wave 0 lane r holds row r's indices of the
+  // NEXT tile, fetched in three dependent stages spread over the current tile (tile bounds before
+  // the gather, edge / node ids before the MFMAs, src / rev before the epilogue) so the index
+  // chain tile_ptr -> perm -> src, rev never stalls the pipeline.
+  int cT = 0, cn = 0;           // stage A: tile start position and size
+  int ce = -1;                  // stage B: edge of row `lane` (E < 2^31)
+  int cnode = -1, cprev = -2;   // stage B: its destination node, and that of the row before
+  int cs = -1, cq = -1;         // stage C: src / rev of that edge (-1 when out of range)
+  auto stage_a = [&](int t) {
+    if constexpr (AGG != 0) {
+      cT = agg.tile_ptr[t];
+      cn = agg.tile_ptr[t + 1] - cT;
+    } else {
+      cT = t * kM;
+      cn = E - (int64_t)cT < kM ? (int)(E - cT) : kM;
+    }
+  };
+  auto stage_b = [&]() {
+    ce = -1;
+    cnode = -1;
+    cprev = -2;
+    if (lane < cn) {
+      if constexpr (AGG != 0) {
+        ce = agg.perm[cT + lane];
+        cnode = agg.dsts[cT + lane];
+        cprev = lane > 0 ? agg.dsts[cT + lane - 1] : -2;
+      } else {
+        ce = cT + lane;
+      }
+    }
+  };
+  auto stage_c = [&]() {
+    const int64_t s = ce >= 0 ? src[ce] : -1, q = ce >= 0 ? rev[ce] : -1;
+    cs = (s >= 0 && s < V) ? (int)s : -1;
+    cq = (q >= 0 && q < E) ? (int)q : -1;
+  };
+  if (w == 0 && (int)blockIdx.x < ntiles) {
+    stage_a(blockIdx.x);
+    stage_b();
+    stage_c();
+  }
+
+  for (int t = blockIdx.x; t < ntiles; t += G) {
+    const bool has_next = t + G < ntiles;
+    if (w == 0) {  // publish this tile's indices (the previous tile's epilogue ended with a barrier)
+      erow[lane] = ce;
+      soff[lane] = cs >= 0 ? (int64_t)cs * h : -1;
+      qoff[lane] = cq >= 0 ? (int64_t)cq * h : -1;
+      if constexpr (AGG != 0) {  // segment starts of the tile's nodes (ballot + prefix popcount)
+        const bool first = lane < cn && cnode != cprev;
+        const unsigned long long m = __ballot(first);
+        const int k = __popcll(m & ((1ull << lane) - 1ull));
+        if (first) {
+          nstart[k] = lane;
+          nnode[k] = cnode;
+        }
+        if (lane == 0) {
+          nseg = __popcll(m);
+          nstart[__popcll(m)] = cn;
+        }
+      }
+      if (has_next) stage_a(t + G);
+    }
+    // B fragments of the first k step, in flight during the gather
+    uint4 bcur[NW];
 #pragma unroll
-  for (int j = 0; j < NW; ++j) bcur[j] = Wp[boff[j]];
-  __syncthreads();
+    for (int j = 0; j < NW; ++j) bcur[j] = Wp[boff(j)];
+    __syncthreads();
 
   // ---- 1. gather A = S[src] - act(H[rev]) (fp32) -> bf16 LDS tile [64][Kp] ----
   if constexpr (W == 8) {
     // wave w owns rows 16 w .. 16 w + 15; lane c takes the c-th 16-B piece of each row, and all 32
     // loads of the wave are issued before the first is consumed (latency hidden by depth)
     const int chunks = KS * 4;
-    for (int c = lane; c < chunks; c += 64) {
+    constexpr int kRG = 8;  // rows in flight per round (2 rounds of 8: 64 VGPRs of raw pieces)
+    for (int idx = lane; idx < chunks * (16 / kRG); idx += 64) {
+      const int c = idx % chunks, r0 = 16 * w + kRG * (idx / chunks);
       const int k0 = c * 8;
       const int kc = k0 < h ? k0 : h - 8;  // clamped, unconditional loads
-      uint4 sraw[16], qraw[16];
+      uint4 sraw[kRG], qraw[kRG];
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int64_t so = soff[16 * w + u], qo = qoff[16 * w + u];
+      for (int u = 0; u < kRG; ++u) {
+        const int64_t so = soff[r0 + u], qo = qoff[r0 + u];
         sraw[u] = *reinterpret_cast<const uint4*>(S + (so >= 0 ? so : 0) + kc);
         qraw[u] = *reinterpret_cast<const uint4*>(H + (qo >= 0 ? qo : 0) + kc);
       }
 #pragma unroll
-      for (int u = 0; u < 16; ++u) {
-        const int r = 16 * w + u;
+      for (int u = 0; u < kRG; ++u) {
+        const int r = r0 + u;
         const bool sok = soff[r] >= 0 && k0 < h, qok = qoff[r] >= 0 && k0 < h;
         const unsigned su[4] = {sraw[u].x, sraw[u].y, sraw[u].z, sraw[u].w};
         const unsigned qu[4] = {qraw[u].x, qraw[u].y, qraw[u].z, qraw[u].w};
@@ -337,6 +370,8 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
   }
   __syncthreads();
 
+    if (w == 0 && has_next) stage_b();
+
   // ---- 2. MFMA over k: acc[mt][j] = rows 16 mt.., columns of tile w + 4 j ----
   f32x4 acc[4][NW];
 #pragma unroll
@@ -349,7 +384,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     const int64_t kn = (ks + 1 < KS ? ks + 1 : ks) * kstride;
     uint4 bnext[NW];
 #pragma unroll
-    for (int j = 0; j < NW; ++j) bnext[j] = Wp[kn + boff[j]];
+    for (int j = 0; j < NW; ++j) bnext[j] = Wp[kn + boff(j)];
     bf16x8 a[4];
 #pragma unroll
     for (int mt = 0; mt < 4; ++mt)
@@ -364,6 +399,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
 #pragma unroll
     for (int j = 0; j < NW; ++j) bcur[j] = bnext[j];
   }
+    if (w == 0 && has_next) stage_c();
   __syncthreads();  // every wave is done with the A tile: its LDS becomes the staging tile
 
   // ---- 3. epilogue: 256 columns per pass through LDS, + bias + residual, bf16 rows ----
@@ -453,6 +489,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     }
     __syncthreads();
   }
+  }  // tile loop
 }
 
 static bool valid_reduce(int r) { return r >= NT_SUM && r <= NT_MIN; }
@@ -482,9 +519,11 @@ int launch_upd(const void* H, const void* S, const int64_t* src, const int64_t* 
   auto kern = update_bf16_kernel<ACT, W, NW, AGG>;
   if (lds > 64 * 1024)
     NT_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
-  kern<<<(unsigned)grid, kThreads, lds, stream>>>(
+  const int64_t slots = 2 * (int64_t)cu_count();  // two resident workgroups per CU (LDS-bound)
+  const int64_t g = grid < slots ? grid : slots;
+  kern<<<(unsigned)g, kThreads, lds, stream>>>(
       (const bf16_t*)H, (const bf16_t*)S, src, rev, (const uint4*)Wp, (const bf16_t*)b, V, E, (int)h,
-      KS, NTn, residual, act, alpha, (bf16_t*)H_out, agg);
+      KS, NTn, residual, act, alpha, (bf16_t*)H_out, agg, (int)grid);
   NT_LAUNCH_CHECK();
   return NT_OK;
 }
