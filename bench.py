@@ -55,6 +55,7 @@ def parse():
     p.add_argument("--workload", default="qm9-4096", choices=sorted(WORKLOADS))
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-embedded", action="store_true", help="skip the embedded-encoder measurement")
     p.add_argument("--pmc-csv", default=None,
                    help="comma-separated rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs of the "
                    "same command (tools/profile.sh) to fill roofline.traffic")
@@ -162,7 +163,7 @@ def main():
 
     from notorch_amd import _lib
     from notorch_amd.data.synth import make_batch
-    from notorch_amd.nn import ChempropBlock, Sum
+    from notorch_amd.nn import ChempropBlock, EmbeddedChempropBlock, GraphEmbedding, Sum
     from notorch_amd.nn.gnn import _engine
 
     _lib.load()  # fail loudly if the HIP extension is missing
@@ -171,14 +172,14 @@ def main():
     torch.manual_seed(0)
     batch = make_batch(kind, n_mols, seed=1000 + env.rank)
     G = batch.collate("nodes")
-    emb_v = torch.nn.EmbeddingBag(42, h, mode="sum")
-    emb_e = torch.nn.EmbeddingBag(13, h, mode="sum")
+    embedding = GraphEmbedding(42, 13, h)  # same RNG draws as two EmbeddingBag(42|13, h) in order
     with torch.no_grad():
-        Xv, Xe = emb_v(G.node_feats), emb_e(G.edge_feats)
+        Xv, Xe = embedding.node(G.node_feats), embedding.edge(G.edge_feats)
     block = ChempropBlock(hidden_dim=h, depth=depth).eval()
     readout = Sum()
     if bf16:  # bf16 storage: the CPU baseline runs the fp32 oracle on the same bf16-rounded values
         block = block.to(torch.bfloat16)
+        embedding = embedding.to(torch.bfloat16)
         Xv, Xe = Xv.to(torch.bfloat16), Xe.to(torch.bfloat16)
     Ws = [l.linear.weight.detach().float().clone() for l in block._chemprop_layers()]
     bs = [l.linear.bias.detach().float().clone() for l in block._chemprop_layers()]
@@ -208,6 +209,34 @@ def main():
             dist.barrier()
         elapsed = time.perf_counter() - t0
         _engine.UPDATE_EVENTS = None
+
+    # Second, smaller measurement (not `value`): the whole encoder from the collated type indices,
+    # GraphEmbedding fused into the initial gather (EmbeddedChempropBlock) + Sum readout.
+    embedded = None
+    if not args.no_embedded:
+        enc = EmbeddedChempropBlock(embedding, block).eval().to(dev)
+        Graw = batch.collate("nodes").to(dev)
+        with torch.no_grad():
+            for _ in range(max(2, args.warmup // 2)):
+                readout(enc(Graw))
+            if env.distributed:
+                dist.barrier()
+            torch.cuda.synchronize(dev)
+            t1 = time.perf_counter()
+            for _ in range(args.steps):
+                readout(enc(Graw))
+            torch.cuda.synchronize(dev)
+            if env.distributed:
+                dist.barrier()
+            e_el = time.perf_counter() - t1
+        e_units, e_secs, e_rate = aggregate_throughput(E * depth * args.steps, e_el, device=dev)
+        embedded = {
+            "step": "GraphEmbedding fused into the initial gather (EmbeddedChempropBlock) + ChempropBlock + Sum, "
+                    "from the collated integer type indices",
+            "ms_per_step": e_secs / args.steps * 1e3,
+            "value": e_rate,
+            "unit": "edge-messages/s",
+        }
 
     from notorch_amd import kernels as K
 
@@ -328,6 +357,7 @@ def main():
             "alg_hbm_gbps": upd_bytes / (upd_ms * 1e-3) / 1e9,
             **extra,
         },
+        "embedded_encoder": embedded,
         "forward_roofline": {
             "alg_bytes": fwd_bytes,
             "flops": fwd_flops,

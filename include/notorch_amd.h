@@ -89,6 +89,26 @@ NT_API int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_types,
                                int64_t V, int64_t E, int64_t h, int act, float act_alpha, int reduce,
                                int dtype, void* H0, void* S, void* stream);
 
+/*
+ * Host-side collate of B per-molecule graphs (BatchedGraph.from_graphs, notorch/data/models/
+ * graph.py:186-223; MolToGraph.collate, transforms/graph.py:45).  HOST memory only, no device call.
+ * Inputs per graph g: node_feats[g] (n_nodes[g] rows of node_row_bytes), edge_feats[g] (n_edges[g]
+ * rows of edge_row_bytes), edge_index[g] (2 x n_edges[g] int64, row-major), rev_index[g]
+ * (n_edges[g] int64), all with graph-local indices.  Outputs (caller-allocated, V = sum n_nodes,
+ * E = sum n_edges): the concatenated feature rows, edge_index_out 2 x E (+ node offset, graph.py:199),
+ * rev_out E (+ node offset for rev_mode 0 = the reference's graph.py:200, + edge offset for
+ * rev_mode 1), batch_node_index V / batch_edge_index E (graph.py:201-202), and the CSR layout:
+ * dst_ptr V+1 / dst_perm E (in-edges per node, ascending edge id) and mol_ptr B+1.
+ * An out-of-range local index returns NT_EINVAL naming the graph and edge.
+ */
+NT_API int nt_collate_graphs(int64_t B, const void* const* node_feats, const int64_t* n_nodes,
+                             int64_t node_row_bytes, const void* const* edge_feats,
+                             const int64_t* n_edges, int64_t edge_row_bytes,
+                             const int64_t* const* edge_index, const int64_t* const* rev_index,
+                             int rev_mode, void* node_out, void* edge_out, int64_t* edge_index_out,
+                             int64_t* rev_out, int64_t* batch_node_index, int64_t* batch_edge_index,
+                             int32_t* dst_ptr, int32_t* dst_perm, int32_t* mol_ptr);
+
 /* Number of bytes of device workspace nt_csr_build needs for n indices into nseg segments. */
 NT_API size_t nt_csr_workspace_bytes(int64_t n, int64_t nseg);
 

@@ -47,6 +47,11 @@ SIGNATURES: dict[str, tuple] = {
         [_vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64,
          _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp],
     ),
+    "nt_collate_graphs": (
+        _c_int,
+        [_c_i64, _vp, _vp, _c_i64, _vp, _vp, _c_i64, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _vp, _vp,
+         _vp, _vp, _vp],
+    ),
     "nt_csr_workspace_bytes": (_c_size, [_c_i64, _c_i64]),
     "nt_csr_build": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_size, _vp, _vp]),
     "nt_dmpnn_init": (

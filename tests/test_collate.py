@@ -1,4 +1,4 @@
-"""CPU: the vectorised collate is bit-identical to the restated reference collate
+"""CPU: the collate (native nt_collate_graphs for host graphs, vectorised torch on a device) is bit-identical to the restated reference collate
 (notorch/data/models/graph.py:186-223) in both rev-offset modes, and its CSR layout is exact."""
 import numpy as np
 import pytest
@@ -72,3 +72,36 @@ def test_collate_is_picklable():
     G = make_batch("qm9", 4, seed=5).collate("nodes")
     G2 = pickle.loads(pickle.dumps(G))
     assert torch.equal(G2.edge_index, G.edge_index) and len(G2) == 4
+
+
+def test_native_collate_matches_device_path_and_layout():
+    """nt_collate_graphs (host C++) == the vectorised torch collate, field for field, and its
+    counting-sort CSR == a stable argsort."""
+    Gs = make_batch("zinc", 48, seed=6).to_graphs()
+    for mode in ("nodes", "edges"):
+        BG = BatchedGraph.from_graphs(Gs, rev_offset=mode)
+        TG = BatchedGraph._from_graphs_device(Gs, mode)
+        for f in FIELDS:
+            assert torch.equal(getattr(BG, f), getattr(TG, f)), f
+        lay = BG._nt_layout
+        dst = BG.edge_index[1].numpy()
+        assert np.array_equal(lay.dst_perm.numpy(), np.argsort(dst, kind="stable"))
+        assert np.array_equal(lay.mol_ptr.numpy(), TG._nt_layout.mol_ptr.numpy())
+
+
+def test_native_collate_float_features_and_errors():
+    from notorch_amd._lib import NativeLibraryError
+
+    Gs = make_batch("qm9", 5, seed=7).to_graphs()
+    Fs = [Graph(torch.randn(G.num_nodes, 3), torch.randn(G.num_edges, 5, dtype=torch.float64),
+                G.edge_index, G.rev_index) for G in Gs]
+    BG = BatchedGraph.from_graphs(Fs)
+    assert torch.equal(BG.node_feats, torch.cat([G.node_feats for G in Fs]))
+    assert torch.equal(BG.edge_feats, torch.cat([G.edge_feats for G in Fs]))
+    bad = Graph(Gs[0].node_feats, Gs[0].edge_feats, Gs[0].edge_index.clone(), Gs[0].rev_index)
+    bad.edge_index[1, 0] = Gs[0].num_nodes  # one past the molecule's atoms
+    with pytest.raises(NativeLibraryError, match="out of range"):
+        BatchedGraph.from_graphs([Gs[1], bad])
+    mixed = [Gs[0], Graph(Gs[1].node_feats.float(), Gs[1].edge_feats, Gs[1].edge_index, Gs[1].rev_index)]
+    with pytest.raises(RuntimeError, match="differ"):
+        BatchedGraph.from_graphs(mixed)
