@@ -214,29 +214,32 @@ def main():
     # GraphEmbedding fused into the initial gather (EmbeddedChempropBlock) + Sum readout.
     embedded = None
     if not args.no_embedded:
-        enc = EmbeddedChempropBlock(embedding, block).eval().to(dev)
         Graw = batch.collate("nodes").to(dev)
-        with torch.no_grad():
-            for _ in range(max(2, args.warmup // 2)):
-                readout(enc(Graw))
-            if env.distributed:
-                dist.barrier()
-            torch.cuda.synchronize(dev)
-            t1 = time.perf_counter()
-            for _ in range(args.steps):
-                readout(enc(Graw))
-            torch.cuda.synchronize(dev)
-            if env.distributed:
-                dist.barrier()
-            e_el = time.perf_counter() - t1
-        e_units, e_secs, e_rate = aggregate_throughput(E * depth * args.steps, e_el, device=dev)
         embedded = {
-            "step": "GraphEmbedding fused into the initial gather (EmbeddedChempropBlock) + ChempropBlock + Sum, "
-                    "from the collated integer type indices",
-            "ms_per_step": e_secs / args.steps * 1e3,
-            "value": e_rate,
+            "step": "GraphEmbedding + ChempropBlock + Sum from the collated integer type indices "
+                    "(EmbeddedChempropBlock; fused = embedding folded into the initial gather, "
+                    "unfused = nt_embed_bag kernels then the block)",
             "unit": "edge-messages/s",
         }
+        for fuse in (True, False):
+            enc = EmbeddedChempropBlock(embedding, block, fuse=fuse).eval().to(dev)
+            with torch.no_grad():
+                for _ in range(max(2, args.warmup // 2)):
+                    readout(enc(Graw))
+                if env.distributed:
+                    dist.barrier()
+                torch.cuda.synchronize(dev)
+                t1 = time.perf_counter()
+                for _ in range(args.steps):
+                    readout(enc(Graw))
+                torch.cuda.synchronize(dev)
+                if env.distributed:
+                    dist.barrier()
+                e_el = time.perf_counter() - t1
+            _, e_secs, e_rate = aggregate_throughput(E * depth * args.steps, e_el, device=dev)
+            tag = "fused" if fuse else "unfused"
+            embedded[f"{tag}_ms_per_step"] = e_secs / args.steps * 1e3
+            embedded[f"{tag}_value"] = e_rate
 
     from notorch_amd import kernels as K
 

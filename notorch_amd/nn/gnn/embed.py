@@ -74,16 +74,18 @@ class GraphEmbedding(nn.Module):
 class EmbeddedChempropBlock(nn.Module):
     """``block(embedding(G))`` with the embedding fused into the block's initial gather."""
 
-    def __init__(self, embedding: GraphEmbedding, block: ChempropBlock):
+    def __init__(self, embedding: GraphEmbedding, block: ChempropBlock, fuse: bool = True):
         super().__init__()
         self.embedding = embedding
         self.block = block
+        self.fuse = fuse  # False: GraphEmbedding kernel, then the block (same bytes out)
 
     def forward(self, G):
         emb, blk = self.embedding, self.block
         needs_grad = torch.is_grad_enabled() and any(p.requires_grad for p in self.parameters())
         fusable = (
-            G.node_feats.device.type == "cuda"
+            self.fuse
+            and G.node_feats.device.type == "cuda"
             and not needs_grad
             and emb._use_kernel(G)
             and emb.node.weight.dtype == emb.edge.weight.dtype
