@@ -259,6 +259,8 @@ def main():
     upd_bytes = update_bytes(V, E, h)
     variant = os.environ.get("NT_UPDATE_KERNEL", "as")
     fused = used_fused
+    persistent = (not fused and not bf16 and _engine._fused_enabled()
+                  and K.fused_supported(V, E, h, Gd.edge_feats.dtype))
     traffic = read_pmc_traffic(args.pmc_csv) if args.pmc_csv else None
     if bf16:
         # native bf16 MFMA (16x16x32, K padded to 32, N to 16); HBM bytes at 2 B per element
@@ -280,10 +282,10 @@ def main():
             "t_min_us": max(t_hbm, t_mfma) * 1e6,
         }
         x6 = False
-    elif fused or (h % 4 == 0 and 97 <= h <= 512 and variant[0] in "axp"):
+    elif fused or persistent or (h % 4 == 0 and 97 <= h <= 512 and variant[0] in "axp"):
         # bf16x6 fp32 emulation: 6 bf16 MFMA products per fp32 product.  Fused / as16 kernels run
         # v_mfma_f32_16x16x32_bf16 (K padded to 32, N to 16); x6 runs 32x32x16 (K to 16, N to 32).
-        if fused or variant[0] == "a":
+        if fused or persistent or variant[0] == "a":
             kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
         else:
             kp, np_ = 16 * ((h + 15) // 16), 32 * ((h + 31) // 32)
@@ -292,6 +294,9 @@ def main():
             fk = os.environ.get("NT_FUSED_KERNEL", "pk")
             kname = ("nt_dmpnn_update_fused (update_%s_kernel: persistent producer/consumer, "
                      "bf16x6 16x16x32 MFMA, aggregation of the next layer fused)" % ("ps" if fk == "ps" else "pk"))
+        elif persistent:
+            kname = ("nt_dmpnn_update_fused without tile plan (update_pk_kernel, bf16x6 16x16x32 MFMA; "
+                     "hub graph: aggregation by the chunked segment reduce)")
         else:
             kname = f"nt_dmpnn_update (bf16x6 variant {variant})"
         bf16_flops = 6 * 2 * E * kp * np_

@@ -226,3 +226,140 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
   NT_LAUNCH_CHECK();
   return NT_OK;
 }
+
+// ------------------------------------------------------------------------------ long segments
+// Load-balanced two-pass reduction for segments far longer than the rest (polymer hubs with
+// in-degree ~512, readouts over 1k-10k-atom molecules: SURVEY §8(d) config 5).  The one-lane-per-
+// (segment, piece) kernel above walks a whole segment serially, so one hub sets the kernel time.
+// Here every segment is cut into chunks of at most kChunk rows (chunk_pos: monotone CSR positions,
+// segment boundaries included); pass 1 reduces each chunk (one lane per (chunk, piece), 4 rows in
+// flight), pass 2 combines a segment's chunk partials in chunk order.  Deterministic; sums differ
+// from the serial ascending order only by the regrouping (fp32 reassociation at chunk boundaries).
+#include "rows.hpp"
+
+namespace nt {
+namespace {
+
+template <typename T, bool VEC, int R, int ACT>
+__global__ void __launch_bounds__(256) seg_chunk_partial(const T* __restrict__ X,
+                                                         const int32_t* __restrict__ perm,
+                                                         const int32_t* __restrict__ chunk_pos,
+                                                         int64_t nchunks, int64_t h, int act,
+                                                         float alpha, float* __restrict__ P) {
+  constexpr int N = Piece<T, VEC>::N;
+  constexpr int RR = R == NT_MEAN ? NT_SUM : R;  // the mean divides in pass 2
+  const int64_t hw = h / N;
+  const int64_t total = nchunks * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = t / hw, c = (t - k * hw) * N;
+    const int32_t b = chunk_pos[k], e = chunk_pos[k + 1];
+    Reducer<RR> r[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) r[i].init();
+    for (int32_t j = b; j < e; j += 4) {
+      float x[4][N];
+      int64_t row[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) row[u] = j + u < e ? (perm ? perm[j + u] : j + u) : (perm ? perm[b] : b);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) Piece<T, VEC>::load(X + row[u] * h + c, x[u]);
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (j + u >= e) break;
+#pragma unroll
+        for (int i = 0; i < N; ++i) r[i].push(act_t<ACT>(x[u][i], act, alpha));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) P[k * h + c + i] = r[i].acc;  // raw accumulator (chunk non-empty)
+  }
+}
+
+template <typename T, bool VEC, int R>
+__global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict__ P,
+                                                         const int32_t* __restrict__ chunk_ptr,
+                                                         const int32_t* __restrict__ seg_ptr,
+                                                         int64_t nseg, int64_t h,
+                                                         T* __restrict__ out) {
+  constexpr int N = Piece<T, VEC>::N;
+  const int64_t hw = h / N;
+  const int64_t total = nseg * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t s = t / hw, c = (t - s * hw) * N;
+    const int32_t b = chunk_ptr[s], e = chunk_ptr[s + 1];
+    float y[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) y[i] = 0.f;  // empty segment -> 0 for every reduction
+    for (int32_t k = b; k < e; ++k) {
+#pragma unroll
+      for (int i = 0; i < N; ++i) {
+        const float p = P[(int64_t)k * h + c + i];
+        if constexpr (R == NT_MAX) y[i] = k == b ? p : fmaxf(y[i], p);
+        else if constexpr (R == NT_MIN) y[i] = k == b ? p : fminf(y[i], p);
+        else y[i] += p;
+      }
+    }
+    if constexpr (R == NT_MEAN) {
+      const int n = seg_ptr[s + 1] - seg_ptr[s];
+#pragma unroll
+      for (int i = 0; i < N; ++i) y[i] /= (float)(n > 1 ? n : 1);
+    }
+    Piece<T, VEC>::store(out + s * h + c, y);
+  }
+}
+
+template <typename T, bool VEC>
+int launch_chunked(const void* X, const int32_t* perm, const int32_t* chunk_pos, int64_t nchunks,
+                   const int32_t* chunk_ptr, const int32_t* seg_ptr, int64_t nseg, int64_t h,
+                   int reduce, int act, float alpha, float* P, void* out, hipStream_t stream) {
+  constexpr int N = Piece<T, VEC>::N;
+  if (nchunks > 0) {
+    const int g1 = grid_for(nchunks * (h / N), 256, 256 * 32);
+    NT_DISPATCH_RA(reduce, act,
+                   (seg_chunk_partial<T, VEC, R_, A_><<<g1, 256, 0, stream>>>(
+                       (const T*)X, perm, chunk_pos, nchunks, h, act, alpha, P)));
+    NT_LAUNCH_CHECK();
+  }
+  const int g2 = grid_for(nseg * (h / N), 256, 256 * 32);
+  switch (reduce) {
+    case NT_SUM: seg_chunk_combine<T, VEC, NT_SUM><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out); break;
+    case NT_MEAN: seg_chunk_combine<T, VEC, NT_MEAN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out); break;
+    case NT_MAX: seg_chunk_combine<T, VEC, NT_MAX><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out); break;
+    default: seg_chunk_combine<T, VEC, NT_MIN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out); break;
+  }
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+}  // namespace
+}  // namespace nt
+
+extern "C" int nt_segment_reduce_chunked(const void* X, const int32_t* perm, const int32_t* chunk_pos,
+                                         int64_t nchunks, const int32_t* chunk_ptr,
+                                         const int32_t* seg_ptr, int64_t nseg, int64_t h, int reduce,
+                                         int act, float act_alpha, int dtype, float* partial,
+                                         void* out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
+  NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
+  NT_REQUIRE(nseg >= 0 && nchunks >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  if (nseg == 0) return NT_OK;
+  NT_REQUIRE(chunk_ptr && seg_ptr && out && (nchunks == 0 || (X && chunk_pos && partial)), NT_EINVAL,
+             "NULL pointer");
+  hipStream_t stream = as_stream(stream_);
+  const bool al = aligned16(X) && aligned16(out) && aligned16(partial);
+  if (dtype == NT_F32)
+    return (h % 4 == 0 && al)
+               ? launch_chunked<float, true>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
+                                             reduce, act, act_alpha, partial, out, stream)
+               : launch_chunked<float, false>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
+                                              reduce, act, act_alpha, partial, out, stream);
+  return (h % 8 == 0 && al)
+             ? launch_chunked<bf16_raw, true>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
+                                              reduce, act, act_alpha, partial, out, stream)
+             : launch_chunked<bf16_raw, false>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
+                                               reduce, act, act_alpha, partial, out, stream);
+}

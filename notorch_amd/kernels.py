@@ -17,6 +17,7 @@ __all__ = [
     "csr_build",
     "dmpnn_init",
     "segment_reduce",
+    "chunk_plan",
     "pack_weights",
     "dmpnn_update",
     "tile_plan",
@@ -218,6 +219,58 @@ def segment_reduce(
             _ptr(out), _stream(dev),
         )
     )
+    return out
+
+
+CHUNK_ROWS = 32  # rows per chunk of the load-balanced segment reduce
+
+
+def chunk_plan(seg_ptr: Tensor, chunk: int = CHUNK_ROWS) -> tuple[Tensor, int, Tensor]:
+    """(chunk_pos[nchunks+1], nchunks, chunk_ptr[nseg+1]) for nt_segment_reduce_chunked: every segment
+    cut into chunks of at most ``chunk`` CSR positions.  Device ops; one host sync (the chunk count)."""
+    _require_device(seg_ptr)
+    sp = seg_ptr.to(torch.int64)
+    n = sp[1:] - sp[:-1]
+    nch = (n + chunk - 1) // chunk
+    chunk_ptr64 = torch.zeros(n.numel() + 1, dtype=torch.int64, device=seg_ptr.device)
+    torch.cumsum(nch, 0, out=chunk_ptr64[1:])
+    nchunks = int(chunk_ptr64[-1])
+    seg_of = torch.repeat_interleave(torch.arange(n.numel(), device=seg_ptr.device), nch,
+                                     output_size=nchunks)
+    k_in_seg = torch.arange(nchunks, device=seg_ptr.device) - chunk_ptr64[seg_of]
+    chunk_pos = torch.empty(nchunks + 1, dtype=torch.int32, device=seg_ptr.device)
+    chunk_pos[:nchunks] = (sp[seg_of] + k_in_seg * chunk).to(torch.int32)
+    chunk_pos[nchunks] = seg_ptr[-1]
+    return chunk_pos, nchunks, chunk_ptr64.to(torch.int32)
+
+
+def segment_reduce_chunked(
+    X: Tensor,
+    seg_ptr: Tensor,
+    perm: Tensor | None,
+    nseg: int,
+    plan: tuple[Tensor, int, Tensor],
+    *,
+    reduce: str = "sum",
+    act: tuple[int, float] = (_lib.NT_ACT_IDENTITY, 0.0),
+    out: Tensor | None = None,
+) -> Tensor:
+    """segment_reduce load-balanced over chunks (plan = chunk_plan(seg_ptr)) for skewed segments."""
+    dev = _require_device(X, seg_ptr, perm)
+    code = _require_feat("X", X)
+    if seg_ptr.dtype != torch.int32 or seg_ptr.numel() != nseg + 1:
+        raise ValueError("seg_ptr must be int32 of length nseg + 1")
+    chunk_pos, nchunks, chunk_ptr = plan
+    h = X.shape[1]
+    if out is None:
+        out = torch.empty(nseg, h, dtype=X.dtype, device=dev)
+    else:
+        _require_feat("out", out, X.dtype)
+    partial = torch.empty(max(nchunks, 1), h, dtype=torch.float32, device=dev)
+    check(_lib.load().nt_segment_reduce_chunked(
+        _ptr(X), _ptr(perm), _ptr(chunk_pos), nchunks, _ptr(chunk_ptr), _ptr(seg_ptr), nseg, h,
+        reduce_code(reduce), act[0], act[1], code, _ptr(partial), _ptr(out), _stream(dev),
+    ))
     return out
 
 

@@ -113,20 +113,52 @@ def mol_layout(G) -> tuple[Tensor, Optional[Tensor]]:
     return mol_ptr, mol_perm
 
 
+LONG_SEGMENT = 64  # segments longer than this switch the aggregation to the chunked reduce
+
+
+def _degree_range(lay: DeviceLayout) -> tuple[int, int]:
+    """(max, min) in-degree of the layout's dst CSR; one host sync per layout, cached."""
+    mm = getattr(lay, "deg_range", None)
+    if mm is None:
+        deg = lay.dst_ptr[1:] - lay.dst_ptr[:-1]
+        if deg.numel() == 0:
+            mm = (0, 0)
+        else:
+            t = torch.stack([deg.max(), deg.min()]).cpu()
+            mm = (int(t[0]), int(t[1]))
+        lay.deg_range = mm
+    return mm
+
+
 def fused_plan(lay: DeviceLayout, V: int, E: int):
     """Tile plan of the fused update for this layout (cached on it), or None when some node has more
     than 32 in-edges (polymer hubs): those graphs take the unfused path.  One sync per layout."""
     if lay.plan is None:
         plan = False
         if E > 0 and V > 0:
-            deg = lay.dst_ptr[1:] - lay.dst_ptr[:-1]
-            mm = torch.stack([deg.max(), deg.min()]).cpu()
-            maxdeg, mindeg = int(mm[0]), int(mm[1])
+            maxdeg, mindeg = _degree_range(lay)
             if maxdeg <= 32:
                 tile_ptr, ntiles, dsts = K.tile_plan(lay.dst_ptr, E, maxdeg)
                 plan = (tile_ptr, ntiles, dsts, mindeg == 0)
         lay.plan = plan
     return lay.plan or None
+
+
+def dst_chunks(lay: DeviceLayout):
+    """Chunk plan of the dst CSR when some node's in-degree exceeds LONG_SEGMENT (hubs), else None."""
+    ch = getattr(lay, "dst_chunks", None)
+    if ch is None:
+        ch = False
+        if lay.dst_ptr.numel() > 1 and _degree_range(lay)[0] > LONG_SEGMENT:
+            ch = K.chunk_plan(lay.dst_ptr)
+        lay.dst_chunks = ch
+    return ch or None
+
+
+def _aggregate(X, seg_ptr, perm, nseg, reduce, act, chunks, out=None):
+    if chunks is not None:
+        return K.segment_reduce_chunked(X, seg_ptr, perm, nseg, chunks, reduce=reduce, act=act, out=out)
+    return K.segment_reduce(X, seg_ptr, perm, nseg, reduce=reduce, act=act, out=out)
 
 
 def _fused_enabled() -> bool:
@@ -177,7 +209,12 @@ def block_forward(
     if len(weights) == 0:
         H, _ = K.dmpnn_init(Xv, Xe, src)
         return _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states)
-    H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
+    chunks = dst_chunks(lay)
+    if chunks is not None:  # hubs: the fused init would walk a hub's in-edges on one lane
+        H, _ = K.dmpnn_init(Xv, Xe, src)
+        S = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks)
+    else:
+        H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
     return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states)
 
 
@@ -212,8 +249,9 @@ def block_forward_embedded(
 def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states):
     """The d layers + final node scatter, from H0 and layer 0's aggregation S."""
     d = len(weights)
+    chunks = dst_chunks(lay)
     if d == 0:
-        node = K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=_IDENTITY)
+        node = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, _IDENTITY, chunks)
         return node, H, []
     Wps = pack_layer_weights(weights)
     E, h = H.shape
@@ -222,6 +260,9 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
         return _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual, keep_states)
     states = []
     spare: Optional[Tensor] = None  # ping-pong buffer when states are not kept
+    # graphs the fused plan cannot take (in-degree > 32): fp32 still runs the persistent kernel,
+    # unfused, with the aggregation as a separate segment reduce
+    persistent = _fused_enabled() and H.dtype == torch.float32 and K.fused_supported(V, E, h, H.dtype)
     timer = UPDATE_EVENTS
     for l in range(d):
         if keep_states:
@@ -229,20 +270,22 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
         if timer is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        Hn = K.dmpnn_update(
-            H, S, src, rev, Wps[l], None if biases[l] is None else biases[l].detach(),
-            residual=residual, act=act, out=spare,
-        )
+        b_l = None if biases[l] is None else biases[l].detach()
+        if persistent:  # the persistent pk kernel without its fused aggregation (hub graphs)
+            Hn, _ = K.dmpnn_update_fused(H, S, src, rev, Wps[l], b_l, residual=residual, act=act,
+                                         out=spare)
+        else:
+            Hn = K.dmpnn_update(H, S, src, rev, Wps[l], b_l, residual=residual, act=act, out=spare)
         if timer is not None:
             ev[1].record()
             timer.append(ev)
         if l < d - 1:
-            S = K.segment_reduce(Hn, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=act,
-                                 out=None if keep_states else S)
+            S = _aggregate(Hn, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks,
+                           out=None if keep_states else S)
         if not keep_states:
             spare = H  # H_l is dead once H_{l+1} exists: reuse its buffer for H_{l+2}
         H = Hn
-    node = K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, reduce=reduce, act=_IDENTITY)
+    node = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, _IDENTITY, chunks)
     return node, H, states
 
 
@@ -416,19 +459,35 @@ class ChempropBlockFunction(torch.autograd.Function):
         return (*res_inputs, None, None, None, None, None, None, None, None, *res_params)
 
 
+def mol_chunks(G, mol_ptr: Tensor):
+    """Chunk plan of the molecule CSR when some molecule has more than LONG_SEGMENT atoms (polymers,
+    config 5), else None; cached on the layout with the molecule CSR it belongs to."""
+    lay = getattr(G, "_nt_layout", None)
+    hit = getattr(lay, "mol_chunks", None) if lay is not None else None
+    if hit is not None and hit[0] is mol_ptr:
+        return hit[1] or None
+    n = mol_ptr[1:] - mol_ptr[:-1]
+    ch = False
+    if n.numel() and int(n.max()) > LONG_SEGMENT:
+        ch = K.chunk_plan(mol_ptr)
+    if lay is not None:
+        lay.mol_chunks = (mol_ptr, ch)
+    return ch or None
+
+
 def segment_reduce_readout(X: Tensor, mol_ptr: Tensor, mol_perm: Optional[Tensor], B: int, reduce: str,
-                           batch_node_index: Tensor) -> Tensor:
+                           batch_node_index: Tensor, chunks=None) -> Tensor:
     if torch.is_grad_enabled() and X.requires_grad:
-        return ReadoutFunction.apply(X, mol_ptr, mol_perm, B, reduce, batch_node_index)
-    return K.segment_reduce(X, mol_ptr, mol_perm, B, reduce=reduce, act=_IDENTITY)
+        return ReadoutFunction.apply(X, mol_ptr, mol_perm, B, reduce, batch_node_index, chunks)
+    return _aggregate(X, mol_ptr, mol_perm, B, reduce, _IDENTITY, chunks)
 
 
 class ReadoutFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, X, mol_ptr, mol_perm, B, reduce, batch_node_index):
+    def forward(ctx, X, mol_ptr, mol_perm, B, reduce, batch_node_index, chunks=None):
         ctx.save_for_backward(X, batch_node_index)
         ctx.cfg = (B, reduce, mol_ptr)
-        return K.segment_reduce(X, mol_ptr, mol_perm, B, reduce=reduce, act=_IDENTITY)
+        return _aggregate(X, mol_ptr, mol_perm, B, reduce, _IDENTITY, chunks)
 
     @staticmethod
     def backward(ctx, dout):
@@ -437,9 +496,9 @@ class ReadoutFunction(torch.autograd.Function):
         if reduce in ("sum", "mean") and dout.dtype == torch.float32:
             # dX[v] = dout[batch v] (/ count for mean): one gather kernel
             dX = K.gather_rows(dout.contiguous(), bni, seg_ptr=mol_ptr if reduce == "mean" else None)
-            return dX, None, None, None, None, None
+            return dX, None, None, None, None, None, None
         with torch.enable_grad():
             X_ = X.detach().requires_grad_(True)
             out = _torch_scatter(X_, bni, B, reduce)
             (dX,) = torch.autograd.grad(out, X_, dout)
-        return dX, None, None, None, None, None
+        return dX, None, None, None, None, None, None

@@ -44,7 +44,8 @@ class _SegmentReadout(Aggregation):
             )
         mol_ptr, mol_perm = _engine.mol_layout(G)
         return _engine.segment_reduce_readout(
-            X.contiguous(), mol_ptr, mol_perm, len(G), self.reduce, G.batch_node_index
+            X.contiguous(), mol_ptr, mol_perm, len(G), self.reduce, G.batch_node_index,
+            _engine.mol_chunks(G, mol_ptr),
         )
 
 
