@@ -416,14 +416,19 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     constexpr int kIt = kM * 32 / kThreads;
     const int cpiece = 8 * (tid & 31);
     const bool cok = cpiece < ncols;
-    uint4 hres[kIt];
+    // the first kPre residual pieces are in flight across the staging round trip; with the fused
+    // aggregation only half are (its segment loop runs beside the next pass's live accumulators,
+    // and 8 would spill)
+    constexpr int kPre = AGG != 0 ? kIt / 2 : kIt;
+    auto load_res = [&](int it) {
+      const int64_t e = erow[(tid >> 5) + 8 * it];
+      const bool ok = cok && e >= 0 && residual;
+      return *reinterpret_cast<const uint4*>(H + (ok ? e * h + n0 + cpiece : 0));
+    };
+    uint4 hres[kPre];
     if constexpr (W == 8) {
 #pragma unroll
-      for (int it = 0; it < kIt; ++it) {
-        const int64_t e = erow[(tid >> 5) + 8 * it];
-        const bool ok = cok && e >= 0 && residual;
-        hres[it] = *reinterpret_cast<const uint4*>(H + (ok ? e * h + n0 + cpiece : 0));
-      }
+      for (int it = 0; it < kPre; ++it) hres[it] = load_res(it);
     }
 #pragma unroll
     for (int jj = 0; jj < 4; ++jj) {
@@ -447,7 +452,8 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
         const int64_t e = erow[r];
         if (cok && e >= 0) {
           float* st = stage + r * kSO + cpiece;
-          const unsigned hu[4] = {hres[it].x, hres[it].y, hres[it].z, hres[it].w};
+          const uint4 hr = it < kPre ? hres[it < kPre ? it : 0] : load_res(it);
+          const unsigned hu[4] = {hr.x, hr.y, hr.z, hr.w};
           float y[8];
 #pragma unroll
           for (int q = 0; q < 8; ++q) {

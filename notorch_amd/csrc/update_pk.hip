@@ -167,6 +167,12 @@ __device__ __forceinline__ RowSrc row_src(const Args& a, int e) {
   return rs;
 }
 
+// select by value, field by field: `c ? a : b` on the structs themselves made hipcc take their
+// addresses and keep both in scratch memory (a dependent scratch load in front of every gather)
+__device__ __forceinline__ RowSrc pick_src(bool c, const RowSrc& x, const RowSrc& y) {
+  return RowSrc{c ? x.soff : y.soff, c ? x.qoff : y.qoff};
+}
+
 struct SliceRegs {
   float4 s0, s1, q0, q1;
   int p0;  // first piece
@@ -213,7 +219,7 @@ __device__ __forceinline__ float reduce_step(float acc, float x, int reduce, boo
 // Finish tile t from the staging tile (the consumers staged final rows: residual + W A + bias):
 // H_out rows and, fused, S_out.  Wave pw owns a node-aligned quarter of the rows; lane l owns
 // pieces l and l + 64 of each row.
-template <int AACT, bool SUMONLY>
+template <int AACT, bool SUMONLY, bool CWR>
 __device__ __forceinline__ void finish_tile(const Args& a, int t, const float* __restrict__ so,
                                             int pw, int lane) {
   const TileRange tr = tile_range(a.tile_ptr, t, a.E);
@@ -254,8 +260,10 @@ __device__ __forceinline__ void finish_tile(const Args& a, int t, const float* _
     const float* srow = so + (rs + r) * kSO;
     const float4 o0 = in0 ? *reinterpret_cast<const float4*>(srow + 4 * c0) : z;
     const float4 o1 = in1 ? *reinterpret_cast<const float4*>(srow + 4 * c1) : z;
-    if (in0) a.O4[e * hv + c0] = o0;
-    if (in1) a.O4[e * hv + c1] = o1;
+    if constexpr (!CWR) {
+      if (in0) a.O4[e * hv + c0] = o0;
+      if (in1) a.O4[e * hv + c1] = o1;
+    }
     if (fused) {
       const int v = __builtin_amdgcn_readlane(vv, rs + r);
       const int vn = r + 1 < nr ? __builtin_amdgcn_readlane(vv, rs + r + 1) : -1;
@@ -295,7 +303,13 @@ __device__ __forceinline__ void finish_tile(const Args& a, int t, const float* _
 // ------------------------------------------------------------------------------ kernel
 // ABL (timing-only builds, outputs wrong; NT_PK_ABL): 1 = producers skip gathers and finishes
 // (protocol only), 2 = no W loads, 4 = no residual loads, 8 = no MFMA
-template <int KS, int ACT, int AACT, bool SUMONLY, bool D = false, int ABL = 0>
+// CWR: the consumers store the finished H' rows straight from their accumulators (16-B row pieces)
+// and the producers' finish only runs the fused aggregation from the staged tile.
+// PF: rows of the next step's A fragments prefetched during the current step (of 4); the other rows
+// are read after the step's MFMAs.  PF = 2 frees 24 VGPRs, which removes the scratch spills the
+// full prefetch (PF = 4) caused inside the consumers' MFMA loop.
+template <int KS, int ACT, int AACT, bool SUMONLY, bool D = false, int ABL = 0, bool CWR = false,
+          int PF = 2>
 __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
   unsigned long long st[4] = {0, 0, 0, 0};
   const unsigned long long t_begin = D ? pk_now() : 0;
@@ -333,12 +347,14 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
     SliceRegs q[L];
 #pragma unroll
     for (int u = 0; u < L; ++u)
-      if (u < G) load_slice(a, u / KS == 0 ? rs_cur : rs_nxt, u % KS, kg, q[u]);
+      if (u < G) load_slice(a, pick_src(u / KS == 0, rs_cur, rs_nxt), u % KS, kg, q[u]);
     int fin = 0;  // next tile to finish: before slice (fin + 1) KS + kR - 1 is produced
     auto finish_next = [&]() {
       wait_ge<D>(flags + kStageReady, 4 * (fin + 1), gave_up, &st[1]);  // consumers staged tile fin
       const unsigned long long tf = D ? pk_now() : 0;
-      if constexpr ((ABL & 1) == 0) finish_tile<AACT, SUMONLY>(a, tile_of(fin), stage, pw, lane);
+      if constexpr ((ABL & 1) == 0) {
+        if (!CWR || a.SO4 != nullptr) finish_tile<AACT, SUMONLY, CWR>(a, tile_of(fin), stage, pw, lane);
+      }
       if constexpr (D) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         st[2] += pk_now() - tf;
@@ -368,7 +384,7 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
           const int gl = g + L;  // refill this register slot with slice g + L
           if ((ABL & 1) == 0 && gl < G) {
             const int il = gl / KS;
-            load_slice(a, il == i ? rs_cur : rs_nxt, gl - il * KS, kg, q[u]);
+            load_slice(a, pick_src(il == i, rs_cur, rs_nxt), gl - il * KS, kg, q[u]);
           }
         }
       }
@@ -399,7 +415,7 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
     constexpr int NC = decltype(nc_tag)::value;
     f32x4 acc[4][CT];
     uint4 bw[NC][3];
-    bf16x8 af[4][3], an[4][3];
+    bf16x8 af[4][3], an[PF][3];
     auto load_w = [&](int ks, int j) {
       const int base = __builtin_amdgcn_readfirstlane(ks * step_bytes + wave * 3 * 1024);
 #pragma unroll
@@ -407,14 +423,15 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
         bw[j][p] = __builtin_bit_cast(
             uint4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff, base + (4 * j * 3 + p) * 1024, 0));
     };
-    auto read_frags = [&](int g, bf16x8 (&dst)[4][3]) {
+    auto read_row = [&](int g, int rt, bf16x8 (&dst)[3]) {
       const char* base = ring + (g % kR) * kSliceB;
+      const int off = pslot(16 * rt + fr, g16) * 16;
 #pragma unroll
-      for (int rt = 0; rt < 4; ++rt) {
-        const int off = pslot(16 * rt + fr, g16) * 16;
+      for (int p = 0; p < 3; ++p) dst[p] = *reinterpret_cast<const bf16x8*>(base + p * kPartB + off);
+    };
+    auto read_frags = [&](int g, bf16x8 (&dst)[4][3]) {
 #pragma unroll
-        for (int p = 0; p < 3; ++p) dst[rt][p] = *reinterpret_cast<const bf16x8*>(base + p * kPartB + off);
-      }
+      for (int rt = 0; rt < 4; ++rt) read_row(g, rt, dst[rt]);
     };
     wait_ge(flags + kReady + 0, 4, gave_up);
     read_frags(0, af);
@@ -457,7 +474,8 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
         const bool more = g + 1 < G;
         const int gn = more ? g + 1 : g;  // the last step re-reads its own slice (no branch)
         wait_ge<D>(flags + kReady + gn % kR, more ? 4 * (gn / kR + 1) : 0, gave_up, &st[0]);
-        read_frags(gn, an);
+#pragma unroll
+        for (int rt = 0; rt < PF; ++rt) read_row(gn, rt, an[rt]);
         const bool reload = s + 1 < KS;  // the next tile's step-0 W is loaded at its start
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
@@ -484,9 +502,11 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
           }
         }
         __builtin_amdgcn_sched_barrier(0);
-        if (more) signal(flags + kFreed + (g + 1) % kR, lane);
 #pragma unroll
-        for (int rt = 0; rt < 4; ++rt)
+        for (int rt = PF; rt < 4; ++rt) read_row(gn, rt, af[rt]);  // late rows: af[rt] is free now
+        if (more) signal(flags + kFreed + (g + 1) % kR, lane);       // (waits for those reads)
+#pragma unroll
+        for (int rt = 0; rt < PF; ++rt)
 #pragma unroll
           for (int p = 0; p < 3; ++p) af[rt][p] = an[rt][p];
       };
@@ -496,16 +516,24 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
       if (i > 0) wait_ge<D>(flags + kStageFree, 4 * i, gave_up, &st[1]);
       {
         const float* bf = reinterpret_cast<const float*>(a.b4);
+        const int* em = emap + (i % kEmaps) * 64;
+        float* Of = reinterpret_cast<float*>(a.O4);
+        const bool stage_it = !CWR || a.SO4 != nullptr;
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
           const int col = 16 * (wave + 4 * j) + 4 * g16;
           const float4 bj = (bf && col < hh) ? *reinterpret_cast<const float4*>(bf + col)
                                              : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-          for (int rt = 0; rt < 4; ++rt)
-            *reinterpret_cast<float4*>(stage + (16 * rt + fr) * kSO + col) =
-                make_float4(acc[rt][j][0] + bj.x, acc[rt][j][1] + bj.y, acc[rt][j][2] + bj.z,
-                            acc[rt][j][3] + bj.w);
+          for (int rt = 0; rt < 4; ++rt) {
+            const float4 o = make_float4(acc[rt][j][0] + bj.x, acc[rt][j][1] + bj.y,
+                                         acc[rt][j][2] + bj.z, acc[rt][j][3] + bj.w);
+            if (stage_it) *reinterpret_cast<float4*>(stage + (16 * rt + fr) * kSO + col) = o;
+            if constexpr (CWR) {
+              const int er = em[16 * rt + fr];  // re-read from LDS: no registers held across the tile
+              if (er >= 0 && col < hh) *reinterpret_cast<float4*>(Of + (int64_t)er * hh + col) = o;
+            }
+          }
         }
       }
       signal(flags + kStageReady, lane);
@@ -541,7 +569,13 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
 
 template <int KS, int ACT, int AACT, bool SUMONLY>
 int launch_pk(const Args& a, int grid, hipStream_t stream) {
-  auto kern = update_pk_kernel<KS, ACT, AACT, SUMONLY>;
+  // NT_PK_CW=1: consumers store H' (measured slower at config 2: 157 vs 143 us; the consumers, not
+  // the producers, are the critical role), kept for A/B
+  const char* cw = getenv("NT_PK_CW");
+  auto kern = (cw && cw[0] == '1') ? update_pk_kernel<KS, ACT, AACT, SUMONLY, false, 0, true>
+                                   : update_pk_kernel<KS, ACT, AACT, SUMONLY>;
+  const char* pf = getenv("NT_PK_PF");  // NT_PK_PF=4: the full next-step prefetch, for A/B
+  if (pf && pf[0] == '4') kern = update_pk_kernel<KS, ACT, AACT, SUMONLY, false, 0, false, 4>;
   if constexpr (KS == 10 && ACT == NT_ACT_RELU && SUMONLY) {
     const char* d = getenv("NT_PK_DIAG");
     if (d && d[0] == '1') kern = update_pk_kernel<KS, ACT, AACT, SUMONLY, true>;
