@@ -416,10 +416,9 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     constexpr int kIt = kM * 32 / kThreads;
     const int cpiece = 8 * (tid & 31);
     const bool cok = cpiece < ncols;
-    // the first kPre residual pieces are in flight across the staging round trip; with the fused
-    // aggregation only half are (its segment loop runs beside the next pass's live accumulators,
-    // and 8 would spill)
-    constexpr int kPre = AGG != 0 ? kIt / 2 : kIt;
+    // all residual pieces are in flight across the staging round trip (halving that for the fused
+    // aggregation did not remove its spill and cost ~5% at config 3)
+    constexpr int kPre = kIt;
     auto load_res = [&](int it) {
       const int64_t e = erow[(tid >> 5) + 8 * it];
       const bool ok = cok && e >= 0 && residual;

@@ -478,3 +478,31 @@ def test_segment_reduce_chunked_skewed(reduce, dtype):
         else:
             assert_parity(got.float(), ref, 2.0 ** -8, f"chunked bf16 {reduce}")
         assert got[nseg - 1].abs().sum() == 0  # trailing empty segments read 0
+
+
+def test_batch_with_zero_bond_molecules():
+    """Single-atom molecules (E_i = 0; the reference MolToGraph would crash on them)
+    mixed into a batch: their nodes have no in-edge, so S and node rows are 0 (torch_scatter empty
+    segment) through the fused zero-filled path, and the readout of such a molecule is 0."""
+    from notorch_amd.data.models.graph import BatchedGraph, Graph
+    from notorch_amd.data.synth import make_batch
+    from notorch_amd.nn import Sum
+
+    Gs = make_batch("qm9", 6, seed=9).to_graphs()
+    one = Graph(torch.tensor([[1, 12, 20, 25, 30, 36, 41]]), torch.zeros(0, 2, dtype=torch.long),
+                torch.zeros(2, 0, dtype=torch.long), torch.zeros(0, dtype=torch.long))
+    G = BatchedGraph.from_graphs([Gs[0], one, Gs[1], Gs[2], one, Gs[3]])
+    h = 64
+    Xv, Xe = _embed(G, h, seed=4)
+    torch.manual_seed(5)
+    Ws = [torch.randn(h, h) / 8 for _ in range(3)]
+    bs = [torch.randn(h) * 0.1 for _ in range(3)]
+    ref_n, ref_e = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, Ws, bs)
+    ref_r = dmpnn_ref.readout(ref_n, G.batch_node_index, len(G), "sum")
+    _, _, out = _module_forward(G, Xv, Xe, Ws, bs)
+    with torch.no_grad():
+        r = Sum()(out)
+    assert_parity(out.edge_feats, ref_e, what="edge")
+    assert_parity(out.node_feats, ref_n, what="node")
+    assert_parity(r, ref_r, what="readout")
+    assert r[1].abs().sum() == 0 and r[4].abs().sum() == 0
