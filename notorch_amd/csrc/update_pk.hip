@@ -103,6 +103,7 @@ struct Args {
   float aalpha;
   float4* O4;
   float4* SO4;
+  int prio;  // NT_PK_PRIO: 1 = producers at s_setprio 1, 2 = consumers (A/B; 0 = none)
 };
 
 // ------------------------------------------------------------------------------ LDS counters
@@ -219,7 +220,7 @@ __device__ __forceinline__ float reduce_step(float acc, float x, int reduce, boo
 // Finish tile t from the staging tile (the consumers staged final rows: residual + W A + bias):
 // H_out rows and, fused, S_out.  Wave pw owns a node-aligned quarter of the rows; lane l owns
 // pieces l and l + 64 of each row.
-template <int AACT, bool SUMONLY, bool CWR>
+template <int AACT, bool SUMONLY, bool CWR, int FU = 4>
 __device__ __forceinline__ void finish_tile(const Args& a, int t, const float* __restrict__ so,
                                             int pw, int lane) {
   const TileRange tr = tile_range(a.tile_ptr, t, a.E);
@@ -255,11 +256,13 @@ __device__ __forceinline__ void finish_tile(const Args& a, int t, const float* _
   const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
   float4 acc0 = z, acc1 = z;
   int cnt = 0;
-  for (int r = 0; r < nr; ++r) {
-    const int64_t e = __builtin_amdgcn_readlane(ev, rs + r);
+  auto row_vals = [&](int r, float4& o0, float4& o1) {
     const float* srow = so + (rs + r) * kSO;
-    const float4 o0 = in0 ? *reinterpret_cast<const float4*>(srow + 4 * c0) : z;
-    const float4 o1 = in1 ? *reinterpret_cast<const float4*>(srow + 4 * c1) : z;
+    o0 = in0 ? *reinterpret_cast<const float4*>(srow + 4 * c0) : z;
+    o1 = in1 ? *reinterpret_cast<const float4*>(srow + 4 * c1) : z;
+  };
+  auto process = [&](int r, const float4& o0, const float4& o1) {
+    const int64_t e = __builtin_amdgcn_readlane(ev, rs + r);
     if constexpr (!CWR) {
       if (in0) a.O4[e * hv + c0] = o0;
       if (in1) a.O4[e * hv + c1] = o1;
@@ -297,6 +300,22 @@ __device__ __forceinline__ void finish_tile(const Args& a, int t, const float* _
         cnt = 0;
       }
     }
+  };
+  // rows four at a time: their eight staged-piece LDS reads are in flight together
+  int r = 0;
+  if constexpr (FU > 1) {
+    for (; r + FU <= nr; r += FU) {
+      float4 p0[FU], p1[FU];
+#pragma unroll
+      for (int u = 0; u < FU; ++u) row_vals(r + u, p0[u], p1[u]);
+#pragma unroll
+      for (int u = 0; u < FU; ++u) process(r + u, p0[u], p1[u]);
+    }
+  }
+  for (; r < nr; ++r) {
+    float4 o0, o1;
+    row_vals(r, o0, o1);
+    process(r, o0, o1);
   }
 }
 
@@ -332,6 +351,8 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
   auto tile_of = [&](int i) { return (int)blockIdx.x + i * (int)gridDim.x; };
   const int G = nt * KS;
 
+  if (a.prio == 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  if (a.prio == 2 && wave < 4) __builtin_amdgcn_s_setprio(1);
   if (wave >= 4) {
     // =============================================================== producers
     const int pw = wave - 4;
@@ -635,6 +656,12 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
   a.aalpha = aalpha;
   a.O4 = (float4*)u.H_out;
   a.SO4 = (float4*)S_out;
+  {
+    // default 0 (age arbitration): consumer priority was ~1% ahead before the finish rows were
+    // batched, and ~1% behind after (A/B in tools/pk_ab.sh); kept selectable
+    const char* pr = getenv("NT_PK_PRIO");
+    a.prio = pr && pr[0] ? atoi(pr) : 0;
+  }
   if (a.ntiles == 0) return NT_OK;
   const int grid = a.ntiles < cu_count() ? a.ntiles : cu_count();
   const int KS = (int)((u.h + 31) / 32);
