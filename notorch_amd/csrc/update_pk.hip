@@ -43,6 +43,7 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 constexpr int kRows = 64;
 constexpr int kThreads = 512;
 constexpr int kR = 6;                         // ring slots
+constexpr int kLCap = 6;                      // slices a producer keeps loading ahead (4 before)
 constexpr int kPartB = kRows * 4 * 16;        // one bf16 part of a slice: 4096 B
 constexpr int kSliceB = 3 * kPartB;           // 12,288 B
 constexpr int kSO = 304;                      // staging row stride (floats)
@@ -360,7 +361,7 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
     // Slice loads run L slices ahead of the LDS writes (a register ring, loop unrolled by L), so
     // each slice's gather latency overlaps L consumer steps.  Slice g + L belongs to the tile of
     // slice g or the next one (L < KS): rs_cur / rs_nxt, rotated when slice g starts a tile.
-    constexpr int L = KS == 1 ? 1 : (KS - 1 < 4 ? KS - 1 : 4);
+    constexpr int L = KS == 1 ? 1 : (KS - 1 < kLCap ? KS - 1 : kLCap);
     int e_cur = row_edge(a, tile_of(0), row);
     int e_nxt = nt > 1 ? row_edge(a, tile_of(1), row) : -1;
     RowSrc rs_cur = row_src(a, e_cur);
