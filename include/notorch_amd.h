@@ -39,7 +39,7 @@ extern "C" {
 enum nt_status { NT_OK = 0, NT_EINVAL = 1, NT_EHIP = 2, NT_EUNSUPPORTED = 3 };
 
 /* element type of feature matrices, weights and bias.  NT_BF16: bf16 storage, fp32 arithmetic, one
- * rounding per stored element (BASELINE config 3); the backward entry points are NT_F32 only. */
+ * rounding per stored element (BASELINE config 3); the backward entry points take both. */
 enum nt_dtype { NT_F32 = 0, NT_BF16 = 1 };
 
 /* reduce domain of notorch.types.Reduction (types.py:57) with torch_scatter semantics:

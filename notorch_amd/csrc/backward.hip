@@ -18,6 +18,7 @@
 //   nt_gather_rows          out[i] = base[i] + X[idx i] / c_{idx i}        3 rows / row
 //                           (dnode[dst] into dL/dH_d, chemprop.py:86; readout backward, agg.py:23-38)
 #include "common.hpp"
+#include "rows.hpp"
 
 namespace nt {
 
@@ -134,6 +135,99 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const T* __restrict__ 
   }
 }
 
+// ---- bf16 storage (bf16 training): same math in fp32 registers, one rounding per stored element ----
+template <bool VEC, int ACT>
+__global__ void __launch_bounds__(256) message_bf16(const bf16_raw* __restrict__ H,
+                                                    const bf16_raw* __restrict__ S,
+                                                    const int64_t* __restrict__ src,
+                                                    const int64_t* __restrict__ rev, int64_t E,
+                                                    int64_t h, int act, float alpha,
+                                                    bf16_raw* __restrict__ A) {
+  using P = Piece<bf16_raw, VEC>;
+  constexpr int N = P::N;
+  const int64_t hw = h / N, total = E * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / hw, c = (t - e * hw) * N;
+    float sv[N], qv[N];
+    P::load(S + src[e] * h + c, sv);
+    P::load(H + rev[e] * h + c, qv);
+#pragma unroll
+    for (int i = 0; i < N; ++i) sv[i] -= act_t<ACT>(qv[i], act, alpha);
+    P::store(A + e * h + c, sv);
+  }
+}
+
+template <bool VEC, int ACT, bool MEAN>
+__global__ void __launch_bounds__(256) edge_backward_bf16(
+    const bf16_raw* __restrict__ G, const bf16_raw* __restrict__ H, const bf16_raw* __restrict__ dA,
+    const bf16_raw* __restrict__ dS, const int64_t* __restrict__ dst,
+    const int32_t* __restrict__ rev_ptr, const int32_t* __restrict__ rev_perm,
+    const int32_t* __restrict__ dst_ptr, int64_t E, int64_t h, int residual, int act, float alpha,
+    bf16_raw* __restrict__ Gout) {
+  using P = Piece<bf16_raw, VEC>;
+  constexpr int N = P::N;
+  const int64_t hw = h / N, total = E * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / hw, c = (t - e * hw) * N;
+    const int64_t v = dst[e];
+    float dm[N], x[N];
+    P::load(dS + v * h + c, dm);
+    if constexpr (MEAN) {
+      const int cnt = dst_ptr[v + 1] - dst_ptr[v];
+      const float inv = 1.f / (float)(cnt > 1 ? cnt : 1);
+#pragma unroll
+      for (int i = 0; i < N; ++i) dm[i] *= inv;
+    }
+    for (int32_t j = rev_ptr[e]; j < rev_ptr[e + 1]; ++j) {
+      P::load(dA + (int64_t)rev_perm[j] * h + c, x);
+#pragma unroll
+      for (int i = 0; i < N; ++i) dm[i] -= x[i];
+    }
+    P::load(H + e * h + c, x);
+#pragma unroll
+    for (int i = 0; i < N; ++i) dm[i] *= act_grad_t<ACT>(x[i], act, alpha);
+    if (residual) {
+      P::load(G + e * h + c, x);
+#pragma unroll
+      for (int i = 0; i < N; ++i) dm[i] += x[i];
+    }
+    P::store(Gout + e * h + c, dm);
+  }
+}
+
+template <bool VEC, bool MEAN>
+__global__ void __launch_bounds__(256) gather_rows_bf16(const bf16_raw* __restrict__ base,
+                                                        const bf16_raw* __restrict__ X,
+                                                        const int64_t* __restrict__ idx,
+                                                        const int32_t* __restrict__ seg_ptr,
+                                                        int64_t n, int64_t h,
+                                                        bf16_raw* __restrict__ out) {
+  using P = Piece<bf16_raw, VEC>;
+  constexpr int N = P::N;
+  const int64_t hw = h / N, total = n * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / hw, c = (t - i * hw) * N;
+    const int64_t s = idx[i];
+    float x[N], b[N];
+    P::load(X + s * h + c, x);
+    if constexpr (MEAN) {
+      const int cnt = seg_ptr[s + 1] - seg_ptr[s];
+      const float inv = 1.f / (float)(cnt > 1 ? cnt : 1);
+#pragma unroll
+      for (int q = 0; q < N; ++q) x[q] *= inv;
+    }
+    if (base) {
+      P::load(base + i * h + c, b);
+#pragma unroll
+      for (int q = 0; q < N; ++q) x[q] += b[q];
+    }
+    P::store(out + i * h + c, x);
+  }
+}
+
 static bool valid_act(int a) { return a >= NT_ACT_IDENTITY && a <= NT_ACT_SIGMOID; }
 
 #define NT_BW_DISPATCH_ACT(ACT, LAUNCH)                                          \
@@ -150,12 +244,26 @@ extern "C" int nt_dmpnn_message(const void* H, const void* S, const int64_t* src
                                 void* A_out, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(valid_act(act), NT_EINVAL, "bad act code");
   NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
   if (E == 0) return NT_OK;
   NT_REQUIRE(H && S && src && rev && A_out, NT_EINVAL, "NULL pointer");
   hipStream_t stream = as_stream(stream_);
+  if (dtype == NT_BF16) {
+    const bool vec = h % 8 == 0 && aligned16(H) && aligned16(S) && aligned16(A_out);
+    const int grid = grid_for(E * (vec ? h / 8 : h), 256, 256 * 32);
+    if (vec)
+      NT_BW_DISPATCH_ACT(act, (message_bf16<true, A_><<<grid, 256, 0, stream>>>(
+                                  (const bf16_raw*)H, (const bf16_raw*)S, src, rev, E, h, act,
+                                  act_alpha, (bf16_raw*)A_out)));
+    else
+      NT_BW_DISPATCH_ACT(act, (message_bf16<false, A_><<<grid, 256, 0, stream>>>(
+                                  (const bf16_raw*)H, (const bf16_raw*)S, src, rev, E, h, act,
+                                  act_alpha, (bf16_raw*)A_out)));
+    NT_LAUNCH_CHECK();
+    return NT_OK;
+  }
   if (h % 4 == 0 && aligned16(H) && aligned16(S) && aligned16(A_out)) {
     const int64_t hw = h / 4;
     NT_BW_DISPATCH_ACT(act, (message_kernel<float4, A_><<<grid_for(E * hw, 256, 256 * 32), 256, 0, stream>>>(
@@ -177,7 +285,7 @@ extern "C" int nt_dmpnn_edge_backward(const void* G, const void* H, const void* 
                                       int reduce, int dtype, void* G_out, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(valid_act(act), NT_EINVAL, "bad act code");
   NT_REQUIRE(reduce == NT_SUM || reduce == NT_MEAN, NT_EUNSUPPORTED,
              "edge backward covers reduce = sum | mean");
@@ -188,6 +296,21 @@ extern "C" int nt_dmpnn_edge_backward(const void* G, const void* H, const void* 
   NT_REQUIRE(reduce != NT_MEAN || dst_ptr, NT_EINVAL, "mean needs the dst CSR");
   hipStream_t stream = as_stream(stream_);
   const bool mean = reduce == NT_MEAN;
+  if (dtype == NT_BF16) {
+    const bool vec = h % 8 == 0 && aligned16(H) && aligned16(dA) && aligned16(dS) &&
+                     aligned16(G_out) && (!residual || aligned16(G));
+    const int grid = grid_for(E * (vec ? h / 8 : h), 256, 256 * 32);
+#define NT_EB16(VEC_, MEAN_)                                                                        \
+  NT_BW_DISPATCH_ACT(act, (edge_backward_bf16<VEC_, A_, MEAN_><<<grid, 256, 0, stream>>>(           \
+                              (const bf16_raw*)G, (const bf16_raw*)H, (const bf16_raw*)dA,          \
+                              (const bf16_raw*)dS, dst, rev_ptr, rev_perm, dst_ptr, E, h, residual, \
+                              act, act_alpha, (bf16_raw*)G_out)))
+    if (vec) { if (mean) NT_EB16(true, true); else NT_EB16(true, false); }
+    else { if (mean) NT_EB16(false, true); else NT_EB16(false, false); }
+#undef NT_EB16
+    NT_LAUNCH_CHECK();
+    return NT_OK;
+  }
   if (h % 4 == 0 && aligned16(H) && aligned16(dA) && aligned16(dS) && aligned16(G_out) &&
       (!residual || aligned16(G))) {
     const int64_t hw = h / 4;
@@ -218,12 +341,25 @@ extern "C" int nt_gather_rows(const void* base, const void* X, const int64_t* id
                               void* out, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "only NT_F32 is implemented");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(n >= 0 && nseg >= 0 && h > 0, NT_EINVAL, "bad sizes");
   if (n == 0) return NT_OK;
   NT_REQUIRE(X && idx && out, NT_EINVAL, "NULL pointer");
   hipStream_t stream = as_stream(stream_);
   const bool mean = seg_ptr != nullptr;
+  if (dtype == NT_BF16) {
+    const bool vec = h % 8 == 0 && aligned16(X) && aligned16(out) && (!base || aligned16(base));
+    const int grid = grid_for(n * (vec ? h / 8 : h), 256, 256 * 32);
+    const bf16_raw* b16 = (const bf16_raw*)base;
+    const bf16_raw* x16 = (const bf16_raw*)X;
+    bf16_raw* o16 = (bf16_raw*)out;
+    if (vec && mean) gather_rows_bf16<true, true><<<grid, 256, 0, stream>>>(b16, x16, idx, seg_ptr, n, h, o16);
+    else if (vec) gather_rows_bf16<true, false><<<grid, 256, 0, stream>>>(b16, x16, idx, seg_ptr, n, h, o16);
+    else if (mean) gather_rows_bf16<false, true><<<grid, 256, 0, stream>>>(b16, x16, idx, seg_ptr, n, h, o16);
+    else gather_rows_bf16<false, false><<<grid, 256, 0, stream>>>(b16, x16, idx, seg_ptr, n, h, o16);
+    NT_LAUNCH_CHECK();
+    return NT_OK;
+  }
   if (h % 4 == 0 && aligned16(X) && aligned16(out) && (!base || aligned16(base))) {
     const int64_t hw = h / 4;
     const int grid = grid_for(n * hw, 256, 256 * 32);

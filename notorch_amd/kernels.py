@@ -435,8 +435,8 @@ def dmpnn_message(H: Tensor, S: Tensor, src: Tensor, rev: Tensor, *,
                   act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0), out: Tensor | None = None) -> Tensor:
     """A = S[src] - act(H[rev])  (the layer message, recomputed for the weight gradient)."""
     dev = _require_device(H, S, src, rev, out)
-    _require_f32("H", H)
-    _require_f32("S", S)
+    code = _require_feat("H", H)
+    _require_feat("S", S, H.dtype)
     _require_i64("src", src)
     _require_i64("rev_index", rev)
     E, h = H.shape
@@ -445,8 +445,10 @@ def dmpnn_message(H: Tensor, S: Tensor, src: Tensor, rev: Tensor, *,
         raise ValueError("shape mismatch between H, S, src and rev_index")
     if out is None:
         out = torch.empty_like(H)
+    else:
+        _require_feat("out", out, H.dtype)
     check(_lib.load().nt_dmpnn_message(
-        _ptr(H), _ptr(S), _ptr(src), _ptr(rev), V, E, h, act[0], act[1], NT_F32, _ptr(out), _stream(dev)
+        _ptr(H), _ptr(S), _ptr(src), _ptr(rev), V, E, h, act[0], act[1], code, _ptr(out), _stream(dev)
     ))
     return out
 
@@ -457,12 +459,13 @@ def dmpnn_edge_backward(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor, dst
                         reduce: str = "sum", out: Tensor | None = None) -> Tensor:
     """dL/dH_l = (residual ? G : 0) + act'(H) * (dS[dst] / c - scatter(dA, rev))  (see header)."""
     dev = _require_device(G, H, dA, dS, dst, rev_ptr, rev_perm, dst_ptr, out)
-    for name, t in (("H", H), ("dA", dA), ("dS", dS)):
-        _require_f32(name, t)
+    code = _require_feat("H", H)
+    for name, t in (("dA", dA), ("dS", dS)):
+        _require_feat(name, t, H.dtype)
     if residual:
         if G is None:
             raise ValueError("residual backward needs G")
-        _require_f32("G", G)
+        _require_feat("G", G, H.dtype)
     _require_i64("dst", dst)
     E, h = H.shape
     V = dS.shape[0]
@@ -472,10 +475,12 @@ def dmpnn_edge_backward(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor, dst
         raise ValueError("mean reduce needs the dst CSR")
     if out is None:
         out = torch.empty_like(H)
+    else:
+        _require_feat("out", out, H.dtype)
     check(_lib.load().nt_dmpnn_edge_backward(
         _ptr(G if residual else None), _ptr(H), _ptr(dA), _ptr(dS), _ptr(dst), _ptr(rev_ptr),
         _ptr(rev_perm), _ptr(dst_ptr), V, E, h, int(residual), act[0], act[1], reduce_code(reduce),
-        NT_F32, _ptr(out), _stream(dev),
+        code, _ptr(out), _stream(dev),
     ))
     return out
 
@@ -485,20 +490,22 @@ def gather_rows(X: Tensor, idx: Tensor, *, base: Tensor | None = None, seg_ptr: 
     """out[i] = (base[i] if base is given) + X[idx[i]], divided by max(segment size of idx[i], 1)
     when ``seg_ptr`` is given (the backward of a mean scatter)."""
     dev = _require_device(X, idx, base, seg_ptr, out)
-    _require_f32("X", X)
+    code = _require_feat("X", X)
     _require_i64("idx", idx)
     nseg, h = X.shape
     n = idx.numel()
     if base is not None:
-        _require_f32("base", base)
+        _require_feat("base", base, X.dtype)
         if base.shape != (n, h):
             raise ValueError("base must be n x h")
     if seg_ptr is not None and (seg_ptr.dtype != torch.int32 or seg_ptr.numel() != nseg + 1):
         raise ValueError("seg_ptr must be int32 of length nseg + 1")
     if out is None:
         out = torch.empty(n, h, dtype=X.dtype, device=dev)
+    else:
+        _require_feat("out", out, X.dtype)
     check(_lib.load().nt_gather_rows(
-        _ptr(base), _ptr(X), _ptr(idx), _ptr(seg_ptr), n, nseg, h, NT_F32, _ptr(out), _stream(dev)
+        _ptr(base), _ptr(X), _ptr(idx), _ptr(seg_ptr), n, nseg, h, code, _ptr(out), _stream(dev)
     ))
     return out
 

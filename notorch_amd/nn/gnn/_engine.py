@@ -366,7 +366,9 @@ def _weight_grad(G: Tensor, A: Tensor) -> Tensor:
         return torch.mm(G.t(), A)
     rows = E // k
     Eb = rows * k
-    dW = torch.bmm(G[:Eb].view(k, rows, h).transpose(1, 2), A[:Eb].view(k, rows, h)).sum(0)
+    # bf16: the k partials are summed in fp32 and rounded once
+    dW = torch.bmm(G[:Eb].view(k, rows, h).transpose(1, 2), A[:Eb].view(k, rows, h)).sum(
+        0, dtype=torch.float32).to(G.dtype)
     if Eb < E:
         dW.addmm_(G[Eb:].t(), A[Eb:])
     return dW
@@ -379,7 +381,7 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
     src_ptr, src_perm, rev_ptr, rev_perm = backward_layout(lay, src, rev, V, E)
     mean_ptr = lay.dst_ptr if reduce == "mean" else None
     if dH is None:
-        G = torch.zeros(E, h, dtype=torch.float32, device=src.device)
+        G = torch.zeros(E, h, dtype=dnode.dtype, device=src.device)
     else:
         G = dH.contiguous()
     if dnode is not None:
@@ -411,7 +413,7 @@ class ChempropBlockFunction(torch.autograd.Function):
         weights = list(params[:nlayers])
         biases = list(params[nlayers:])
         src = edge_index[0].contiguous()
-        kernel_bwd = (reduce in ("sum", "mean") and Xv.dtype == torch.float32
+        kernel_bwd = (reduce in ("sum", "mean") and Xv.dtype in (torch.float32, torch.bfloat16)
                       and os.environ.get("NT_BWD", "kernel") != "torch")
         node, H, states = block_forward(Xv, Xe, src, rev, lay, weights, biases, act, reduce, residual,
                                         keep_states=kernel_bwd)
@@ -493,7 +495,7 @@ class ReadoutFunction(torch.autograd.Function):
     def backward(ctx, dout):
         X, bni = ctx.saved_tensors
         B, reduce, mol_ptr = ctx.cfg
-        if reduce in ("sum", "mean") and dout.dtype == torch.float32:
+        if reduce in ("sum", "mean") and dout.dtype in (torch.float32, torch.bfloat16):
             # dX[v] = dout[batch v] (/ count for mean): one gather kernel
             dX = K.gather_rows(dout.contiguous(), bni, seg_ptr=mol_ptr if reduce == "mean" else None)
             return dX, None, None, None, None, None, None

@@ -57,7 +57,9 @@ def test_abi_version_and_errors_without_gpu():
     assert rc == 3  # NT_EUNSUPPORTED: unknown dtype code
     assert lib.nt_dmpnn_packed_weight_bytes(512, 1) == 16 * 32 * 64 * 16  # bf16 image, h = 512
     rc = lib.nt_dmpnn_message(None, None, None, None, 4, 8, 16, 1, 0.0, 1, None, None)
-    assert rc == 3  # backward kernels are fp32-only (bf16 trains through the recompute)
+    assert rc == 1 and b"NULL" in lib.nt_last_error()  # bf16 backward is implemented
+    rc = lib.nt_dmpnn_message(None, None, None, None, 4, 8, 16, 1, 0.0, 7, None, None)
+    assert rc == 3
     rc = lib.nt_csr_build(None, -1, 3, None, None, None, 0, None, None)
     assert rc == 1
     # backward entry points validate before touching the device
