@@ -1,6 +1,7 @@
 """Training-step timing of ChempropBlock + Sum readout (forward + backward) at config 2:
 kernel backward (default) vs the recompute-in-torch backward (NT_BWD=torch).
-Usage: python tools/train_bench.py [--mols 4096] [--h 300] [--depth 3] [--steps 20]"""
+Usage: python tools/train_bench.py [--kind qm9] [--mols 4096] [--h 300] [--depth 3] [--dtype f32|bf16]
+                                  [--steps 20]"""
 import argparse
 import os
 import statistics
@@ -15,20 +16,23 @@ from notorch_amd.nn import ChempropBlock, Sum  # noqa: E402
 
 def main():
     p = argparse.ArgumentParser()
+    p.add_argument("--kind", default="qm9")
+    p.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     p.add_argument("--mols", type=int, default=4096)
     p.add_argument("--h", type=int, default=300)
     p.add_argument("--depth", type=int, default=3)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--modes", default="kernel,torch")
     a = p.parse_args()
-    G = make_batch("qm9", a.mols, seed=0).collate("nodes")
+    dt = {"f32": torch.float32, "bf16": torch.bfloat16}[a.dtype]
+    G = make_batch(a.kind, a.mols, seed=0).collate("nodes")
     torch.manual_seed(0)
     ev = torch.nn.EmbeddingBag(42, a.h, mode="sum")
     ee = torch.nn.EmbeddingBag(13, a.h, mode="sum")
     with torch.no_grad():
-        Xv, Xe = ev(G.node_feats), ee(G.edge_feats)
+        Xv, Xe = ev(G.node_feats).to(dt), ee(G.edge_feats).to(dt)
     Gd = G.update(node_feats=Xv, edge_feats=Xe).to("cuda")
-    blk = ChempropBlock(a.h, depth=a.depth).cuda().train()
+    blk = ChempropBlock(a.h, depth=a.depth).to("cuda", dt).train()
     ro = Sum()
     Xv_d = Gd.node_feats.requires_grad_(True)
     Xe_d = Gd.edge_feats.requires_grad_(True)
@@ -38,7 +42,7 @@ def main():
         blk.zero_grad(set_to_none=True)
         Xv_d.grad = Xe_d.grad = None
         out = blk(Gd.update(node_feats=Xv_d, edge_feats=Xe_d))
-        ro(out).pow(2).sum().backward()
+        ro(out).float().pow(2).sum().backward()
 
     def fwd():
         with torch.no_grad():
@@ -60,7 +64,7 @@ def main():
                 e.synchronize()
                 ts.append(s.elapsed_time(e))
             res[name] = statistics.median(ts)
-    print(f"V={G.num_nodes} E={E} h={a.h} depth={a.depth}")
+    print(f"{a.kind} V={G.num_nodes} E={E} h={a.h} depth={a.depth} {a.dtype}")
     for k, v in res.items():
         print(f"{k:14s} {v:8.3f} ms/step  {E * a.depth / (v * 1e-3):.3e} edge-msg/s")
 
