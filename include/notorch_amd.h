@@ -272,6 +272,16 @@ NT_API int nt_dmpnn_edge_backward(const void* G, const void* H, const void* dA, 
 NT_API int nt_gather_rows(const void* base, const void* X, const int64_t* idx, const int32_t* seg_ptr,
                           int64_t n, int64_t nseg, int64_t h, int dtype, void* out, void* stream);
 
+/* Dropout of the layer update fused with its residual add: replaces `nn.Dropout(p)` inside
+ * ChempropLayer.update (notorch/nn/gnn/chemprop.py:26, applied at :42) followed by
+ * Residual's `inputs[0] + module(*inputs)` (notorch/nn/residual.py:28), training mode.
+ *   out[i] = (base ? base[i] : 0) + keep(seed, offset + i) * Y[i] / (1 - p),   i < n
+ * keep() is a counter-based hash (no mask is stored); P(keep) = 1 - p; p = 1 drops every element.
+ * The backward is the same call on the incoming gradient with base = NULL and the same
+ * (seed, offset).  out may alias base or Y. */
+NT_API int nt_dropout_residual(const void* base, const void* Y, int64_t n, float p, uint64_t seed,
+                               uint64_t offset, int dtype, void* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

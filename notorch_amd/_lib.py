@@ -93,6 +93,8 @@ SIGNATURES: dict[str, tuple] = {
          _c_int, _c_int, _vp, _vp],
     ),
     "nt_gather_rows": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp]),
+    "nt_dropout_residual": (_c_int, [_vp, _vp, _c_i64, ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64,
+                                     _c_int, _vp, _vp]),
 }
 
 

@@ -622,3 +622,30 @@ def softmax_pool(X: Tensor, scores: Tensor, seg_ptr: Tensor, perm: Tensor | None
         _ptr(X), _ptr(scores), _ptr(seg_ptr), _ptr(perm), nseg, h, code, _ptr(out), _stream(dev)
     ))
     return out
+
+
+# ------------------------------------------------------------------------------------ dropout
+def dropout_residual(Y: Tensor, p: float, seed: int, offset: int = 0, *, base: Tensor | None = None,
+                     out: Tensor | None = None) -> Tensor:
+    """out = (base or 0) + keep * Y / (1 - p), keep a counter-based hash of (seed, offset + i)
+    (chemprop.py:26 Dropout + residual.py:28; see include/notorch_amd.h).  The same call on a
+    gradient with base=None is the backward."""
+    dev = _require_device(Y, base, out)
+    code = _require_feat("Y", Y)
+    if not Y.is_contiguous():
+        raise ValueError("Y must be contiguous")
+    if base is not None:
+        _require_feat("base", base, Y.dtype)
+        if base.shape != Y.shape or not base.is_contiguous():
+            raise ValueError("base must be a contiguous tensor shaped like Y")
+    if out is None:
+        out = torch.empty_like(Y)
+    else:
+        _require_feat("out", out, Y.dtype)
+        if out.shape != Y.shape or not out.is_contiguous():
+            raise ValueError("out must be a contiguous tensor shaped like Y")
+    check(_lib.load().nt_dropout_residual(
+        _ptr(base), _ptr(Y), Y.numel(), float(p), int(seed) & (2**64 - 1), int(offset), code, _ptr(out),
+        _stream(dev),
+    ))
+    return out

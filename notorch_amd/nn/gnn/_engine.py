@@ -202,20 +202,34 @@ def block_forward(
     reduce: str,
     residual: bool,
     keep_states: bool = False,
+    drop: Optional[tuple[float, int]] = None,
 ) -> tuple[Tensor, Tensor, list[tuple[Tensor, Tensor]]]:
     """Run the kernel sequence; returns (node, H_d, states) with states = [(H_l, S_l)] for
-    l = 0..d-1 (each layer's input hidden state and its aggregation) if keep_states, else []."""
+    l = 0..d-1 (each layer's input hidden state and its aggregation) if keep_states, else [].
+    drop = (p, seed): training-mode dropout of every layer update (layer l draws from
+    dropout_offset(l, E, h))."""
     V = Xv.shape[0]
     if len(weights) == 0:
         H, _ = K.dmpnn_init(Xv, Xe, src)
-        return _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states)
+        return _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states,
+                               drop)
     chunks = dst_chunks(lay)
     if chunks is not None:  # hubs: the fused init would walk a hub's in-edges on one lane
         H, _ = K.dmpnn_init(Xv, Xe, src)
         S = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks)
     else:
         H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
-    return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states)
+    return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop)
+
+
+def dropout_offset(l: int, E: int, h: int) -> int:
+    """First hash counter of layer l's dropout mask: layers draw disjoint counter ranges."""
+    return l * E * h
+
+
+def draw_dropout_seed() -> int:
+    """One 62-bit seed from torch's default CPU generator (so torch.manual_seed reproduces masks)."""
+    return int(torch.randint(0, 2**62, (1,), dtype=torch.int64).item())
 
 
 def block_forward_embedded(
@@ -246,8 +260,10 @@ def block_forward_embedded(
     return node, H
 
 
-def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states):
-    """The d layers + final node scatter, from H0 and layer 0's aggregation S."""
+def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop=None):
+    """The d layers + final node scatter, from H0 and layer 0's aggregation S.  With dropout the
+    update runs without its residual and nt_dropout_residual adds it back (the fused and persistent
+    kernels write H_out directly, so dropout takes the unfused update)."""
     d = len(weights)
     chunks = dst_chunks(lay)
     if d == 0:
@@ -255,14 +271,16 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
         return node, H, []
     Wps = pack_layer_weights(weights)
     E, h = H.shape
-    plan = fused_plan(lay, V, E) if _fused_enabled() and K.fused_supported(V, E, h, H.dtype) else None
+    plan = (fused_plan(lay, V, E) if drop is None and _fused_enabled() and K.fused_supported(V, E, h, H.dtype)
+            else None)
     if plan is not None:
         return _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual, keep_states)
     states = []
     spare: Optional[Tensor] = None  # ping-pong buffer when states are not kept
     # graphs the fused plan cannot take (in-degree > 32): fp32 still runs the persistent kernel,
     # unfused, with the aggregation as a separate segment reduce
-    persistent = _fused_enabled() and H.dtype == torch.float32 and K.fused_supported(V, E, h, H.dtype)
+    persistent = (drop is None and _fused_enabled() and H.dtype == torch.float32
+                  and K.fused_supported(V, E, h, H.dtype))
     timer = UPDATE_EVENTS
     for l in range(d):
         if keep_states:
@@ -271,7 +289,11 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         b_l = None if biases[l] is None else biases[l].detach()
-        if persistent:  # the persistent pk kernel without its fused aggregation (hub graphs)
+        if drop is not None:
+            U = K.dmpnn_update(H, S, src, rev, Wps[l], b_l, residual=False, act=act, out=spare)
+            Hn = K.dropout_residual(U, drop[0], drop[1], dropout_offset(l, E, h),
+                                    base=H if residual else None, out=U)
+        elif persistent:  # the persistent pk kernel without its fused aggregation (hub graphs)
             Hn, _ = K.dmpnn_update_fused(H, S, src, rev, Wps[l], b_l, residual=residual, act=act,
                                          out=spare)
         else:
@@ -330,14 +352,16 @@ def _torch_scatter(x: Tensor, index: Tensor, dim_size: int, reduce: str) -> Tens
     return out.scatter_reduce(0, idx, x, reduce=red, include_self=False)
 
 
-def _torch_block(Xv, Xe, edge_index, rev, weights, biases, act_mod, reduce, residual):
+def _torch_block(Xv, Xe, edge_index, rev, weights, biases, act_mod, reduce, residual, masks=None):
     src, dst = edge_index[0], edge_index[1]
     V = Xv.shape[0]
     H = Xv[src] + Xe
-    for W, b in zip(weights, biases):
+    for l, (W, b) in enumerate(zip(weights, biases)):
         M = act_mod(H)
         S = _torch_scatter(M, dst, V, reduce)
         U = torch.nn.functional.linear(S[src] - M[rev], W, b)
+        if masks is not None:  # dropout: keep / (1 - p), regenerated by the kernel's hash
+            U = U * masks[l]
         H = H + U if residual else U
     return _torch_scatter(H, dst, V, reduce), H
 
@@ -374,7 +398,8 @@ def _weight_grad(G: Tensor, A: Tensor) -> Tensor:
     return dW
 
 
-def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, residual, V, need_x):
+def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, residual, V, need_x,
+                   drop=None):
     """Kernel backward of block_forward for reduce in {sum, mean} (see csrc/backward.hip).
     Returns (dXv, dXe, [dW_l], [db_l])."""
     E, h = states[0][0].shape if states else dH.shape
@@ -393,10 +418,13 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
         H_l, S_l = states[l]
         W = weights[l].detach()
         A = K.dmpnn_message(H_l, S_l, src, rev, act=act)
-        dWs[l] = _weight_grad(G, A)
-        dbs[l] = G.sum(0)
+        # dropout: the update's gradient is keep * G / (1 - p); the residual path keeps G
+        Gu = G if drop is None else K.dropout_residual(G, drop[0], drop[1], dropout_offset(l, E, h))
+        dWs[l] = _weight_grad(Gu, A)
+        dbs[l] = Gu.sum(0)
         del A
-        dA = torch.mm(G, W)
+        dA = torch.mm(Gu, W)
+        del Gu
         dS = K.segment_reduce(dA, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY)
         G = K.dmpnn_edge_backward(G, H_l, dA, dS, dst, rev_ptr, rev_perm, lay.dst_ptr,
                                   residual=residual, act=act, reduce=reduce)
@@ -409,23 +437,23 @@ class ChempropBlockFunction(torch.autograd.Function):
     kernels + two library GEMMs per layer), recompute-in-torch-device-ops backward for max/min."""
 
     @staticmethod
-    def forward(ctx, Xv, Xe, edge_index, rev, lay, act_mod, act, reduce, residual, nlayers, *params):
+    def forward(ctx, Xv, Xe, edge_index, rev, lay, act_mod, act, reduce, residual, nlayers, drop, *params):
         weights = list(params[:nlayers])
         biases = list(params[nlayers:])
         src = edge_index[0].contiguous()
         kernel_bwd = (reduce in ("sum", "mean") and Xv.dtype in (torch.float32, torch.bfloat16)
                       and os.environ.get("NT_BWD", "kernel") != "torch")
         node, H, states = block_forward(Xv, Xe, src, rev, lay, weights, biases, act, reduce, residual,
-                                        keep_states=kernel_bwd)
+                                        keep_states=kernel_bwd, drop=drop)
         flat = [t for hs in states for t in hs]
         ctx.save_for_backward(Xv, Xe, edge_index, rev,
                               *[p if p is not None else torch.empty(0) for p in params], *flat)
-        ctx.cfg = (act_mod, act, reduce, residual, nlayers, [p is None for p in params], lay, kernel_bwd)
+        ctx.cfg = (act_mod, act, reduce, residual, nlayers, [p is None for p in params], lay, kernel_bwd, drop)
         return node, H
 
     @staticmethod
     def backward(ctx, dnode, dH):
-        act_mod, act, reduce, residual, nlayers, is_none, lay, kernel_bwd = ctx.cfg
+        act_mod, act, reduce, residual, nlayers, is_none, lay, kernel_bwd, drop = ctx.cfg
         Xv, Xe, edge_index, rev, *rest = ctx.saved_tensors
         nparams = len(is_none)
         params = [None if n else p for p, n in zip(rest[:nparams], is_none)]
@@ -437,17 +465,24 @@ class ChempropBlockFunction(torch.autograd.Function):
             dst = edge_index[1].contiguous()
             dXv, dXe, dWs, dbs = block_backward(
                 dnode, dH, states, params[:nlayers], src, dst, rev, lay, act, reduce, residual,
-                Xv.shape[0], (need[0], need[1]),
+                Xv.shape[0], (need[0], need[1]), drop,
             )
-            res_params = [dW if need[10 + i] else None for i, dW in enumerate(dWs)]
-            res_params += [None if p is None or not need[10 + nlayers + i] else dbs[i]
+            res_params = [dW if need[11 + i] else None for i, dW in enumerate(dWs)]
+            res_params += [None if p is None or not need[11 + nlayers + i] else dbs[i]
                            for i, p in enumerate(params[nlayers:])]
-            return (dXv, dXe, None, None, None, None, None, None, None, None, *res_params)
+            return (dXv, dXe, None, None, None, None, None, None, None, None, None, *res_params)
         with torch.enable_grad():
             Xv_ = Xv.detach().requires_grad_(need[0])
             Xe_ = Xe.detach().requires_grad_(need[1])
             ps = [None if p is None else p.detach().requires_grad_(True) for p in params]
-            node, H = _torch_block(Xv_, Xe_, edge_index, rev, ps[:nlayers], ps[nlayers:], act_mod, reduce, residual)
+            masks = None
+            if drop is not None:
+                E, h = Xe.shape
+                ones = torch.ones_like(Xe)
+                masks = [K.dropout_residual(ones, drop[0], drop[1], dropout_offset(l, E, h))
+                         for l in range(nlayers)]
+            node, H = _torch_block(Xv_, Xe_, edge_index, rev, ps[:nlayers], ps[nlayers:], act_mod, reduce,
+                                   residual, masks)
             leaves = [t for t in [Xv_, Xe_] + ps if t is not None and t.requires_grad]
             outs, grads = [], []
             for o, g in ((node, dnode), (H, dH)):
@@ -458,7 +493,7 @@ class ChempropBlockFunction(torch.autograd.Function):
         it = iter(got)
         res_inputs = [next(it) if need[0] else None, next(it) if need[1] else None]
         res_params = [None if p is None else next(it) for p in ps]
-        return (*res_inputs, None, None, None, None, None, None, None, None, *res_params)
+        return (*res_inputs, None, None, None, None, None, None, None, None, None, *res_params)
 
 
 def mol_chunks(G, mol_ptr: Tensor):

@@ -10,8 +10,10 @@ Differences by design:
 
 * the forward runs only on ROCm device tensors; a CPU graph raises ``RuntimeError`` (there is no
   CPU fallback — the CPU restatement lives in ``oracle/`` and is test-only);
-* ``dropout > 0`` in training mode raises ``NotImplementedError`` (eval mode, or dropout 0, is the
-  reference's inference path and is fully supported);
+* ``dropout > 0`` in training mode draws its mask from a counter-based hash on the device
+  (``nt_dropout_residual``) seeded from torch's default generator, not from torch's Philox stream:
+  same distribution and scaling as ``nn.Dropout`` (keep with probability 1 - p, scale 1 / (1 - p)),
+  different draws;
 * ``act`` must be one of ReLU, Identity, LeakyReLU, ELU, GELU, SiLU, Tanh, Sigmoid.
 """
 from __future__ import annotations
@@ -37,12 +39,14 @@ def _check_reduce(reduce: str) -> str:
     return reduce
 
 
-def _check_dropout(module: "ChempropLayer") -> None:
-    p = module.update[1].p
-    if module.training and p > 0 and torch.is_grad_enabled():
-        raise NotImplementedError(
-            "ChempropLayer dropout > 0 in training mode is not implemented on the HIP path yet"
-        )
+def _dropout(layers: list["ChempropLayer"]):
+    """(p, seed) when the update's Dropout is active (training mode, p > 0; chemprop.py:26), else None."""
+    ps = {float(l.update[1].p) for l in layers if l.training and l.update[1].p > 0}
+    if not ps:
+        return None
+    if len(ps) > 1 or any(not l.training for l in layers):
+        raise NotImplementedError("layers with different dropout settings are not supported")
+    return ps.pop(), _engine.draw_dropout_seed()
 
 
 class ChempropLayer(nn.Module):
@@ -80,10 +84,11 @@ class ChempropLayer(nn.Module):
 
     def forward(self, edge_feats: Tensor, node_feats: Tensor, edge_index: Tensor, rev_index: Tensor) -> Tensor:
         """U = Dropout(Linear(S[src] - act(H)[rev])), S = scatter(act(H), dst) — no residual here."""
-        _check_dropout(self)
+        drop = _dropout([self])
         V = len(node_feats)
         act = K.act_code(self.act)
-        if torch.is_grad_enabled() and (edge_feats.requires_grad or self.linear.weight.requires_grad):
+        if drop is not None or (torch.is_grad_enabled()
+                                and (edge_feats.requires_grad or self.linear.weight.requires_grad)):
             # training through a standalone layer: route through the block function with depth 1
             # and no residual, then subtract nothing (the block function returns H_1 = U).
             lay = _engine.DeviceLayout(*self._csr(edge_index, rev_index, V), edge_index=edge_index, validated=True)
@@ -91,7 +96,7 @@ class ChempropLayer(nn.Module):
             # H0 = Xv[src] + Xe = edge_feats exactly (adding +0.0)
             _, H = _engine.ChempropBlockFunction.apply(
                 Xv, edge_feats, edge_index, rev_index.contiguous(), lay, self.act, act, self.reduce,
-                False, 1, self.linear.weight, self.linear.bias,
+                False, 1, drop, self.linear.weight, self.linear.bias,
             )
             return H
         seg_ptr, perm = self._csr(edge_index, rev_index, V)
@@ -159,8 +164,7 @@ class ChempropBlock(nn.Module):
                 f"node_feats ({Xv.dtype}), edge_feats ({Xe.dtype}) and the layer weights must share "
                 "one dtype (float32, or bfloat16 after block.to(torch.bfloat16))"
             )
-        for layer in layers:
-            _check_dropout(layer)
+        drop = _dropout(layers)
         acts = {K.act_code(layer.act) for layer in layers}
         if len(acts) > 1:
             raise NotImplementedError("layers with different activations are not supported")
@@ -178,11 +182,11 @@ class ChempropBlock(nn.Module):
         if needs_grad:
             node, H = _engine.ChempropBlockFunction.apply(
                 Xv, Xe, G.edge_index, rev, lay, layers[0].act if layers else nn.Identity(), act,
-                self.reduce, residual, len(layers), *weights, *biases,
+                self.reduce, residual, len(layers), drop, *weights, *biases,
             )
         else:
             src = G.edge_index[0].contiguous()
             node, H, _ = _engine.block_forward(
-                Xv, Xe, src, rev, lay, weights, biases, act, self.reduce, residual
+                Xv, Xe, src, rev, lay, weights, biases, act, self.reduce, residual, drop=drop
             )
         return G.update(node_feats=node, edge_feats=H)

@@ -89,6 +89,7 @@ class EmbeddedChempropBlock(nn.Module):
             and not needs_grad
             and emb._use_kernel(G)
             and emb.node.weight.dtype == emb.edge.weight.dtype
+            and not any(l.training and l.update[1].p > 0 for l in blk._chemprop_layers())  # dropout
         )
         if not fusable:
             return blk(emb(G))

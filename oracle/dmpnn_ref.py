@@ -71,12 +71,16 @@ def chemprop_block(
     act: Callable[[Tensor], Tensor] = torch.relu,
     residual: bool = True,
     reduce: str = "sum",
+    dropout_masks: Optional[Sequence[Tensor]] = None,
 ) -> tuple[Tensor, Tensor]:
-    """chemprop.py:81-88 -> (node_hiddens V x h, edge_hiddens E x h)."""
+    """chemprop.py:81-88 -> (node_hiddens V x h, edge_hiddens E x h).  dropout_masks: per layer, the
+    E x h factor nn.Dropout applied to the update in training mode (keep / (1 - p), chemprop.py:26)."""
     src, dest = edge_index.unbind(0)
     edge_hiddens = node_feats[src] + edge_feats                                       # :82-83
-    for W, b in zip(weights, biases):                                                 # :84
+    for l, (W, b) in enumerate(zip(weights, biases)):                                 # :84
         out = chemprop_layer(edge_hiddens, node_feats, edge_index, rev_index, W, b, act, reduce)
+        if dropout_masks is not None:
+            out = out * dropout_masks[l]                                              # :26 Dropout
         edge_hiddens = edge_hiddens + out if residual else out                        # residual.py:28
     node_hiddens = scatter(edge_hiddens, dest, dim_size=len(node_feats), reduce=reduce)  # :86
     return node_hiddens, edge_hiddens
