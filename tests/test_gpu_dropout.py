@@ -158,12 +158,12 @@ def test_standalone_layer_dropout_matches_oracle():
     torch.manual_seed(7)
     seed = _engine.draw_dropout_seed()
     (mask,) = _masks(seed, p, G.num_edges, h, 1)
+    ei, rev = G.edge_index.clone(), G.rev_index.clone()
     torch.manual_seed(7)
-    Gd = G.to(DEV)
     with torch.no_grad():
-        got = layer(H.to(DEV), torch.zeros(G.num_nodes, h, device=DEV), Gd.edge_index, Gd.rev_index)
+        got = layer(H.to(DEV), torch.zeros(G.num_nodes, h, device=DEV), ei.to(DEV), rev.to(DEV))
     W = layer.linear.weight.detach().double().cpu()
     b = layer.linear.bias.detach().double().cpu()
     ref = dmpnn_ref.chemprop_layer(H.double(), torch.zeros(G.num_nodes, h, dtype=torch.float64),
-                                   G.edge_index, G.rev_index, W, b) * mask
+                                   ei, rev, W, b) * mask
     assert_parity(got, ref, TOL, "layer dropout")
