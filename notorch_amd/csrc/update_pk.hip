@@ -345,11 +345,23 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
   int* emap = flags + kFlagInts;  // [kEmaps][64]: edge of every row of tile i in emap[i % kEmaps]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int nt = (a.ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  // XCD-aware tile walk: workgroups are dispatched round-robin over the 8 XCDs (XCD = blockIdx % 8),
+  // so give each XCD one contiguous eighth of the tile plan.  Neighbouring tiles share S / H rows
+  // (molecules straddle tile cuts), which then stay in that XCD's L2.
+  int t0 = (int)blockIdx.x, tstride = (int)gridDim.x, nt;
+  if ((gridDim.x & 7) == 0) {
+    const int x = (int)blockIdx.x & 7, chunk = (a.ntiles + 7) >> 3;
+    const int lo = x * chunk, hi = min(a.ntiles, lo + chunk);
+    t0 = lo + ((int)blockIdx.x >> 3);
+    tstride = (int)gridDim.x >> 3;
+    nt = hi > t0 ? (hi - t0 + tstride - 1) / tstride : 0;
+  } else {
+    nt = (a.ntiles - t0 + tstride - 1) / tstride;
+  }
   if (nt <= 0) return;
   if (tid < kFlagInts) flags[tid] = 0;
   __syncthreads();  // the only barrier: counters zeroed
-  auto tile_of = [&](int i) { return (int)blockIdx.x + i * (int)gridDim.x; };
+  auto tile_of = [&](int i) { return t0 + i * tstride; };
   const int G = nt * KS;
 
   if (a.prio == 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
