@@ -2,17 +2,26 @@
 HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
 SRC_DIR := notorch_amd/csrc
-OUT     := notorch_amd/lib/libnotorch_amd.so
 SRCS    := $(wildcard $(SRC_DIR)/*.hip)
-OBJS    := $(patsubst $(SRC_DIR)/%.hip,build/%.o,$(SRCS))
 HDRS    := $(wildcard $(SRC_DIR)/*.hpp) include/notorch_amd.h
 FLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result \
            -fvisibility=hidden -DNT_BUILD
+# DIAG=1: the diagnostic library (A/B kernel variants, ablation and stamp builds selected by NT_*
+# environment variables) next to the shipping one; notorch_amd._lib loads it when NT_LIB=diag.
+ifeq ($(DIAG),1)
+OUT     := notorch_amd/lib/libnotorch_amd_diag.so
+BDIR    := build_diag
+FLAGS   += -DNT_DIAG
+else
+OUT     := notorch_amd/lib/libnotorch_amd.so
+BDIR    := build
+endif
+OBJS    := $(patsubst $(SRC_DIR)/%.hip,$(BDIR)/%.o,$(SRCS))
 
 all: $(OUT)
 
-build/%.o: $(SRC_DIR)/%.hip $(HDRS)
-	@mkdir -p build
+$(BDIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
+	@mkdir -p $(BDIR)
 	$(HIPCC) $(FLAGS) -c $< -o $@
 
 $(OUT): $(OBJS)
@@ -24,6 +33,6 @@ resource-usage: $(SRCS)
 	@for f in $(SRCS); do $(HIPCC) $(FLAGS) -c $$f -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|LDS Size|Occupancy|SGPRs:"; done
 
 clean:
-	rm -rf build $(OUT)
+	rm -rf build build_diag notorch_amd/lib/libnotorch_amd.so notorch_amd/lib/libnotorch_amd_diag.so
 
 .PHONY: all clean resource-usage

@@ -1,22 +1,41 @@
 """bench.py — edge-messages/s of the D-MPNN forward (ChempropBlock + Sum readout) on MI355X.
 
 Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N > 1 launched by
-``torch.distributed.run`` (one rank per GPU, RCCL).  Rank 0 prints ONE JSON line.
+``torch.distributed.run`` (one rank per GPU, RCCL only for bench bookkeeping).  Rank 0 prints ONE
+JSON line.
 
-Workload (BASELINE.json configs[1]): per GPU a 4096-molecule QM9-shaped batch (synthetic, seeded
-per rank -> weak scaling), hidden 300, depth 3, fp32, ReLU, residual, sum reduce, reference
-collate semantics (rev offset by nodes).  A "step" = one forward of ChempropBlock + Sum readout
-with the collated graph (incl. its CSR layout) and the embedded features already resident in HBM.
-value = sum over ranks of E_r * depth * K / max over ranks of the timed seconds.
+Headline workload (BASELINE.json configs[1] = SURVEY §8(d) config 2): per GPU a 4096-molecule
+QM9-shaped batch (synthetic, seeded per rank -> weak scaling), hidden 300, depth 3, fp32, ReLU,
+residual, sum reduce, reference collate semantics (rev offset by nodes).  A "step" = one forward
+of ChempropBlock + Sum readout with the collated graph (incl. its CSR layout) and the embedded
+features already resident in HBM.  value = sum over ranks of E_r * depth * K / max over ranks of
+the timed seconds.
 
-Also reported: ``roofline`` for the dominant kernel (nt_dmpnn_update_fused, or nt_dmpnn_update on
-the unfused path; per-launch duration from
-torch.cuda events recorded on the launch stream around every launch inside the timed region) and
-``cpu_baseline`` (the oracle restatement on the host CPU, rank 0, N=1, bounded sample).
+Other workloads (``--workload``): ``qm9-1m-sharded`` is BASELINE config 4: ONE seeded
+1,000,000-molecule batch cut into 8 edge-balanced contiguous shards (shard.edge_balanced_ranges);
+rank r of N runs shards r, r + N, ... each as its own collated batch (N = 8: one 125k shard per
+GPU; N = 1: all eight in turn) -> fixed total work ("strong").  ``zinc-4096-bf16`` is config 3,
+``polymer-16`` config 5; both are also measured in every default run as ``secondary`` keys.
+
+Also in the line:
+* ``roofline`` for the dominant kernel (the fused layer update; per-launch duration from HIP events
+  recorded on the launch stream around every launch inside the timed region), with SURVEY §8(d)'s
+  definitions: ``frac`` = fp32 algorithmic flops / launch time / 157.3 TF fp32 MFMA peak (fp32
+  workloads; may exceed 1 because the kernel emulates fp32 on faster 16-bit MFMA), ``hbm_frac`` =
+  algorithmic bytes / launch time / 8 TB/s, ``emu_issue_frac`` = the 16-bit MFMA products actually
+  issued / launch time / 2.5 PF; ``traffic`` = HBM bytes per launch from rocprofv3 FETCH_SIZE (x2,
+  gfx950) + WRITE_SIZE, read from ``--pmc-csv`` or from the committed profile of this workload
+  (labelled with the commit it was taken at);
+* ``cpu_baseline``: the oracle restatement (ATen CPU) on the host, rank 0, N=1, a bounded sample,
+  at P = 1 and at P = the box's CPU share;
+* ``fresh_batch``: the same forward on never-seen collated graphs (CSR + plans shipped by the
+  collate, no device->host sync), ``end_to_end``: host Graphs -> collate -> H2D -> forward.
 """
 from __future__ import annotations
 
 import argparse
+import copy
+import glob
 import json
 import os
 import statistics
@@ -29,22 +48,25 @@ sys.path.insert(0, ROOT)
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from notorch_amd.shard import aggregate_throughput, dist_env  # noqa: E402
+from notorch_amd.shard import aggregate_throughput, dist_env, edge_balanced_ranges  # noqa: E402
 
 METRIC = "edge-messages/sec D-MPNN depth=3 h=300, QM9-shaped batches, 1/2/4/8 MI355X"
 PEAK_FP32_MFMA_TFLOPS = 157.3  # MI355X_MICROARCH.md: dense fp32 MFMA (= vector) peak
 PEAK_HBM_GBPS = 8000.0
-PEAK_BF16_MFMA_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md)
+PEAK_16BIT_MFMA_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA (MI355X_MICROARCH.md)
 
 WORKLOADS = {
-    # name: (generator, molecules per GPU, hidden, depth, storage dtype)
+    # name: (generator, molecules, hidden, depth, storage dtype)
     "qm9-4096": ("qm9", 4096, 300, 3, "f32"),  # BASELINE config 2 (the metric's configuration)
     "qm9-32k": ("qm9", 32768, 300, 3, "f32"),  # HBM-scale batch (working set >> Infinity Cache)
-    "qm9-125k": ("qm9", 125000, 300, 3, "f32"),  # config 4: one GPU's whole 1M/8 shard in one batch
+    "qm9-125k": ("qm9", 125000, 300, 3, "f32"),  # one GPU's 1M/8 shard size in one batch
+    "qm9-1m-sharded": ("qm9v", 1_000_000, 300, 3, "f32"),  # BASELINE config 4 (see header)
     "zinc-4096-bf16": ("zinc", 4096, 512, 5, "bf16"),  # BASELINE config 3 (bf16)
     "zinc-4096": ("zinc", 4096, 512, 5, "f32"),  # config 3 shape, fp32
-    "polymer-16": ("polymer", 16, 300, 3, "f32"),  # config 5 shape
+    "polymer-16": ("polymer", 16, 300, 3, "f32"),  # BASELINE config 5
 }
+SECONDARY = ("zinc-4096-bf16", "polymer-16")
+N_SHARDS = 8  # config 4: 1M molecules over 8 MI355X
 
 
 def parse():
@@ -53,15 +75,17 @@ def parse():
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--workload", default="qm9-4096", choices=sorted(WORKLOADS))
-    p.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline sample budget")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget per thread count")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--no-embedded", action="store_true", help="skip the embedded-encoder measurement")
+    p.add_argument("--no-embedded", action="store_true", help="skip embedded / fresh / end-to-end legs")
+    p.add_argument("--no-secondary", action="store_true", help="skip the config-3 / config-5 keys")
     p.add_argument("--pmc-csv", default=None,
                    help="comma-separated rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs of the "
                    "same command (tools/profile.sh) to fill roofline.traffic")
     return p.parse_args()
 
 
+# --------------------------------------------------------------------------- roofline models
 def forward_bytes_flops(V, E, B, h, d, b=4):
     """SURVEY §8(d) minimal-traffic model of the fused forward + its MFMA flops."""
     rows = b * h * ((2 * d + 3) * (E + V) + B)
@@ -71,56 +95,117 @@ def forward_bytes_flops(V, E, B, h, d, b=4):
 
 
 def fused_bytes(V, E, h, b=4):
-    """Algorithmic bytes of ONE nt_dmpnn_update_fused launch (SURVEY §8(d) minimal model of a
-    layer: read H, read S, write H', write S' = 2E + 2V rows; int32 src/rev/perm; weights once)."""
+    """Algorithmic bytes of ONE fused layer launch (SURVEY §8(d) minimal model of a layer: read H,
+    read S, write H', write S' = 2E + 2V rows; int32 src/rev/perm; weights once)."""
     return b * h * (2 * E + 2 * V) + 4 * 3 * E + (h * h + h) * b
 
 
 def update_bytes(V, E, h, b=4):
-    """Algorithmic HBM bytes of ONE nt_dmpnn_update launch: read H[e], gather S[src[e]] and
-    H[rev[e]], write H_out[e] (4 rows per edge), src+rev int64, weights once."""
+    """Algorithmic bytes of ONE unfused update launch: read H[e], gather S[src[e]] and H[rev[e]],
+    write H_out[e] (4 rows per edge), src + rev int64, weights once."""
     return 4 * E * h * b + 16 * E + (h * h + h) * b
 
 
-def cpu_baseline(G, Xv, Xe, Ws, bs, depth, budget_s):
-    """Oracle restatement (ATen CPU) timed on the host; median of runs within the budget."""
-    from oracle import dmpnn_ref
+# --------------------------------------------------------------------------- workloads
+class Job:
+    """One collated batch resident on the device, ready for block(Gd)."""
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    threads = max(1, min(16, cores))
-    torch.set_num_threads(threads)
-    ei, rev, bni, B = G.edge_index.cpu(), G.rev_index.cpu(), G.batch_node_index.cpu(), len(G)
-    Xv, Xe = Xv.cpu(), Xe.cpu()
-    Ws = [w.detach().cpu() for w in Ws]
-    bs = [b.detach().cpu() for b in bs]
+    def __init__(self, batch, G, Gd, h, depth, bf16):
+        self.batch, self.G, self.Gd = batch, G, Gd
+        self.V, self.E, self.B = G.num_nodes, G.num_edges, len(G)
+        self.h, self.depth, self.bf16 = h, depth, bf16
 
-    def one():
-        with torch.inference_mode():
-            n, _ = dmpnn_ref.chemprop_block(Xv, Xe, ei, rev, Ws, bs)
-            dmpnn_ref.readout(n, bni, B, "sum")
 
-    one()  # warm-up
-    times, t_start = [], time.perf_counter()
-    while (time.perf_counter() - t_start < budget_s and len(times) < 200) or len(times) < 3:
+def make_model(h, depth, bf16, dev):
+    from notorch_amd.nn import ChempropBlock, GraphEmbedding
+
+    torch.manual_seed(0)
+    embedding = GraphEmbedding(42, 13, h)  # same RNG draws as two EmbeddingBag(42|13, h) in order
+    block = ChempropBlock(hidden_dim=h, depth=depth).eval()
+    if bf16:
+        block = block.to(torch.bfloat16)
+        embedding = embedding.to(torch.bfloat16)
+    return embedding.to(dev), block.to(dev)
+
+
+def embed_on_device(embedding, G, dev):
+    """Collated type indices -> device, embedded by the GraphEmbedding kernel (nt_embed_bag)."""
+    Gt = copy.copy(G).to(dev)  # Graph.to moves in place: keep the host graph for the CPU baseline
+    with torch.no_grad():
+        return embedding(Gt)
+
+
+def make_jobs(name, rank, world, dev, embedding):
+    from notorch_amd.data.synth import make_batch, make_qm9_batch_vectorized
+
+    kind, n_mols, h, depth, sdtype = WORKLOADS[name]
+    bf16 = sdtype == "bf16"
+    jobs = []
+    if kind == "qm9v":
+        full = make_qm9_batch_vectorized(n_mols, seed=1000)
+        ranges = edge_balanced_ranges(2 * full.n_bonds, N_SHARDS)
+        for i in range(rank, N_SHARDS, world):
+            sub = full.subset(*ranges[i])
+            G = sub.collate("nodes")
+            jobs.append(Job(sub, G, embed_on_device(embedding, G, dev), h, depth, bf16))
+        return jobs, full, ranges
+    batch = make_batch(kind, n_mols, seed=1000 + rank)
+    G = batch.collate("nodes")
+    jobs.append(Job(batch, G, embed_on_device(embedding, G, dev), h, depth, bf16))
+    return jobs, batch, None
+
+
+def timed_steps(step, steps, warmup, env, dev):
+    with torch.no_grad():
+        for _ in range(warmup):
+            step()
+        if env.distributed:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
-        one()
-        times.append(time.perf_counter() - t0)
-    med = statistics.median(times)
-    E = ei.shape[1]
-    return {
-        "value": E * depth / med,
-        "unit": "edge-messages/s",
-        "cores": threads,
-        "kind": "port",
-        "sample": f"oracle/dmpnn_ref.py (ATen CPU restatement of chemprop.py+agg.py) on the same "
-        f"{B}-molecule batch, fp32, torch.set_num_threads({threads}), median of {len(times)} "
-        f"forwards ({med * 1e3:.1f} ms each) after 1 warm-up; host cpus visible {cores}",
-    }
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize(dev)
+        if env.distributed:
+            dist.barrier()
+        return time.perf_counter() - t0
 
 
+def launch_roofline(jobs, events, engine_info, traffic, traffic_src):
+    """Roofline of the dominant kernel (the layer update) from the per-launch HIP events."""
+    upd_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
+    t = upd_ms * 1e-3
+    j = max(jobs, key=lambda x: x.E)
+    V, E, h = j.V, j.E, j.h
+    b = 2 if j.bf16 else 4
+    fused = engine_info.get("fused", False)
+    alg_bytes = fused_bytes(V, E, h, b) if fused else update_bytes(V, E, h, b)
+    flops = 2 * E * h * h
+    kp, np_ = engine_info.get("kpad", h), engine_info.get("npad", h)
+    emu_flops = engine_info.get("products", 1) * 2 * E * kp * np_
+    hbm_gbps = alg_bytes / t / 1e9
+    out = {"kernel": engine_info.get("kernel", "?"), "numerics": engine_info.get("numerics", "?")}
+    if j.bf16:
+        # bf16 storage: 1 bf16 product per MAC; HBM-bound (SURVEY §8(d) table, config 3)
+        out.update(bound="hbm", achieved=hbm_gbps, peak=PEAK_HBM_GBPS, unit="GB/s",
+                   frac=hbm_gbps / PEAK_HBM_GBPS)
+    else:
+        tf = flops / t / 1e12
+        out.update(bound="mfma", achieved=tf, peak=PEAK_FP32_MFMA_TFLOPS, unit="TFLOP/s",
+                   frac=tf / PEAK_FP32_MFMA_TFLOPS)
+    out.update(
+        traffic=traffic, traffic_source=traffic_src,
+        traffic_over_alg=None if traffic is None else traffic / alg_bytes,
+        launch_us=upd_ms * 1e3, launches_timed=len(events),
+        alg_bytes_per_launch=alg_bytes, flops_per_launch_fp32=flops,
+        hbm_frac=hbm_gbps / PEAK_HBM_GBPS, alg_hbm_gbps=hbm_gbps,
+        emu_mfma_tflops=emu_flops / t / 1e12, emu_issue_frac=emu_flops / t / 1e12 / PEAK_16BIT_MFMA_TFLOPS,
+        t_min_us=max(alg_bytes / (PEAK_HBM_GBPS * 1e9), emu_flops / (PEAK_16BIT_MFMA_TFLOPS * 1e12)) * 1e6,
+    )
+    return out
+
+
+# --------------------------------------------------------------------------- PMC traffic
 def read_pmc_traffic(paths, kernel_substr="update"):
     """Average HBM bytes per launch of the update kernel from rocprofv3 --pmc counter_collection
     CSVs (comma-separated; FETCH_SIZE and WRITE_SIZE come from separate passes).
@@ -153,6 +238,216 @@ def read_pmc_traffic(paths, kernel_substr="update"):
     return per
 
 
+def committed_traffic(workload, kernel_substr):
+    """Traffic per launch from the newest committed profile of this workload (profiles/*/<workload>/
+    PMC.json, written by tools/save_profile.py from the same command's --pmc passes)."""
+    best = None
+    for f in glob.glob(os.path.join(ROOT, "profiles", "*", workload, "PMC.json")):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if kernel_substr in d.get("kernel", "") and (best is None or d.get("time", 0) > best[0].get("time", 0)):
+            best = (d, f)
+    if best is None:
+        return None, None
+    d, f = best
+    return d["traffic_per_launch"], f"rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, builder-profiled at {d['commit']} " \
+        f"({os.path.relpath(f, ROOT)})"
+
+
+# --------------------------------------------------------------------------- CPU baseline
+def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
+    """Oracle restatement (ATen CPU) timed on the host at P = 1 and at P = the box's CPU share
+    (OMP_NUM_THREADS, which the GPU box sets to its per-GPU share), median of runs per budget."""
+    from oracle import dmpnn_ref
+
+    if job.B > sample_mols:  # bounded sample: the first sample_mols molecules of the job
+        G = job.batch.subset(0, sample_mols).collate("nodes")
+        sample = f"first {sample_mols} molecules of the job's batch"
+    else:
+        G = job.G
+        sample = f"the same {job.B}-molecule batch"
+    emb = copy.deepcopy(embedding).float().cpu()
+    blk_Ws, blk_bs = WS_BS
+    with torch.no_grad():
+        Xv, Xe = emb.node(G.node_feats), emb.edge(G.edge_feats)
+        if job.bf16:  # the fp32 oracle on the bf16-rounded values the device path stores
+            Xv, Xe = Xv.to(torch.bfloat16).float(), Xe.to(torch.bfloat16).float()
+    ei, rev, bni, B = G.edge_index, G.rev_index, G.batch_node_index, len(G)
+    try:
+        visible = len(os.sched_getaffinity(0))
+    except AttributeError:
+        visible = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, visible)
+
+    def one():
+        with torch.inference_mode():
+            n, _ = dmpnn_ref.chemprop_block(Xv, Xe, ei, rev, blk_Ws, blk_bs)
+            dmpnn_ref.readout(n, bni, B, "sum")
+
+    res = {}
+    prev = torch.get_num_threads()
+    for P in sorted({1, share}):
+        torch.set_num_threads(P)
+        one()  # warm-up
+        times, t_start = [], time.perf_counter()
+        while (time.perf_counter() - t_start < budget_s and len(times) < 200) or len(times) < 3:
+            t0 = time.perf_counter()
+            one()
+            times.append(time.perf_counter() - t0)
+        res[P] = (statistics.median(times), len(times))
+    torch.set_num_threads(prev)
+    E = ei.shape[1]
+    best_P = min(res, key=lambda p: res[p][0])
+    return {
+        "value": E * job.depth / res[best_P][0],
+        "unit": "edge-messages/s",
+        "cores": best_P,
+        "kind": "port",
+        "by_threads": {str(p): {"value": E * job.depth / m, "ms": m * 1e3, "runs": n} for p, (m, n) in res.items()},
+        "sample": f"oracle/dmpnn_ref.py (ATen CPU restatement of chemprop.py+agg.py) on {sample} "
+        f"(V={G.num_nodes}, E={E}), fp32, torch.set_num_threads(P) for P in {sorted(res)} (P = 1 and "
+        f"the box's per-GPU CPU share, OMP_NUM_THREADS={share}); median of runs within {budget_s:.0f} s "
+        f"each after 1 warm-up; host cpus visible {visible}",
+    }
+
+
+WS_BS = None  # (weights, biases) of the headline block on the host, for the CPU baseline
+
+
+# --------------------------------------------------------------------------- main
+def run_workload(name, args, env, dev, headline):
+    from notorch_amd.nn import Sum
+    from notorch_amd.nn.gnn import _engine
+
+    kind, n_mols, h, depth, sdtype = WORKLOADS[name]
+    bf16 = sdtype == "bf16"
+    embedding, block = make_model(h, depth, bf16, dev)
+    jobs, batch, ranges = make_jobs(name, env.rank, env.world_size, dev, embedding)
+    readout = Sum()
+    torch.cuda.synchronize(dev)
+
+    def step():
+        for j in jobs:
+            readout(block(j.Gd))
+
+    events = []
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            step()
+    _engine.UPDATE_EVENTS = events
+    elapsed = timed_steps(step, args.steps, 0, env, dev)
+    _engine.UPDATE_EVENTS = None
+    info = dict(_engine.LAST_UPDATE_INFO)
+    E_rank = sum(j.E for j in jobs)
+    units, secs, rate = aggregate_throughput(E_rank * depth * args.steps, elapsed, device=dev)
+    res = {"jobs": jobs, "embedding": embedding, "block": block, "readout": readout, "events": events,
+           "info": info, "units": units, "secs": secs, "rate": rate, "batch": batch, "ranges": ranges,
+           "name": name, "kind": kind, "h": h, "depth": depth, "bf16": bf16, "n_mols": n_mols}
+    if headline:
+        global WS_BS
+        layers = block._chemprop_layers()
+        WS_BS = ([l.linear.weight.detach().float().cpu().clone() for l in layers],
+                 [l.linear.bias.detach().float().cpu().clone() for l in layers])
+    return res
+
+
+def fresh_batch_leg(res, args, env, dev, n_fresh=6):
+    """Forward on graphs the engine has never seen (collated on the host, CSR + plans shipped)."""
+    job = res["jobs"][0]
+    block, readout = res["block"], res["readout"]
+    Xv, Xe = job.Gd.node_feats, job.Gd.edge_feats
+    fresh = [job.batch.collate("nodes").to(dev).update(node_feats=Xv, edge_feats=Xe) for _ in range(n_fresh + 1)]
+    torch.cuda.synchronize(dev)
+    with torch.no_grad():
+        readout(block(fresh[0]))  # first call of the process for this shape (allocator, packs)
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for G in fresh[1:]:
+            readout(block(G))
+        torch.cuda.synchronize(dev)
+        t = (time.perf_counter() - t0) / n_fresh
+    resident = res["secs"] / args.steps / len(res["jobs"])
+    return {"step": f"{n_fresh} never-seen collated graphs (host CSR + tile plan shipped by the collate), "
+                    "resident features, back to back", "fresh_batch_ms": t * 1e3,
+            "resident_ms": resident * 1e3, "ratio": t / resident}
+
+
+def embedded_leg(res, args, env, dev):
+    from notorch_amd.nn import EmbeddedChempropBlock
+
+    job = res["jobs"][0]
+    Graw = copy.copy(job.G).to(dev)
+    out = {"step": "GraphEmbedding + ChempropBlock + Sum from the collated integer type indices "
+                   "(EmbeddedChempropBlock; fused = embedding folded into the initial gather, "
+                   "unfused = nt_embed_bag kernels then the block)", "unit": "edge-messages/s"}
+    for fuse in (True, False):
+        enc = EmbeddedChempropBlock(res["embedding"], res["block"], fuse=fuse).eval()
+        el = timed_steps(lambda: res["readout"](enc(Graw)), args.steps, max(2, args.warmup // 2), env, dev)
+        _, e_secs, e_rate = aggregate_throughput(job.E * job.depth * args.steps, el, device=dev)
+        tag = "fused" if fuse else "unfused"
+        out[f"{tag}_ms_per_step"] = e_secs / args.steps * 1e3
+        out[f"{tag}_value"] = e_rate
+    return out
+
+
+def end_to_end_leg(res, dev):
+    from notorch_amd.data.models.graph import BatchedGraph
+    from notorch_amd.nn import EmbeddedChempropBlock
+
+    job = res["jobs"][0]
+    graphs = job.batch.to_graphs()
+    enc = EmbeddedChempropBlock(res["embedding"], res["block"], fuse=True).eval()
+    parts = {"collate": [], "h2d": [], "device": []}
+    with torch.no_grad():
+        for it in range(6):
+            torch.cuda.synchronize(dev)
+            t_a = time.perf_counter()
+            Gh = BatchedGraph.from_graphs(graphs)
+            t_b = time.perf_counter()
+            Gdev = Gh.to(dev)
+            torch.cuda.synchronize(dev)
+            t_c = time.perf_counter()
+            res["readout"](enc(Gdev))
+            torch.cuda.synchronize(dev)
+            t_d = time.perf_counter()
+            if it:  # the first pass builds caches
+                parts["collate"].append(t_b - t_a)
+                parts["h2d"].append(t_c - t_b)
+                parts["device"].append(t_d - t_c)
+    med = {k: statistics.median(v) * 1e3 for k, v in parts.items()}
+    total = sum(med.values())
+    return {"step": f"{job.B} host Graphs -> BatchedGraph.from_graphs (native collate) -> .to(device) "
+                    "(pageable H2D) -> EmbeddedChempropBlock + Sum; rank 0, median of 5, serial",
+            "collate_ms": med["collate"], "h2d_ms": med["h2d"], "device_ms": med["device"],
+            "total_ms": total, "value": job.E * job.depth / (total * 1e-3), "unit": "edge-messages/s"}
+
+
+def summary(res, args, env, pmc_csv=None):
+    jobs = res["jobs"]
+    info = res["info"]
+    kern = info.get("kernel_short", "update")
+    if pmc_csv:
+        traffic, tsrc = read_pmc_traffic(pmc_csv, kern), "rocprofv3 --pmc of this command (--pmc-csv)"
+    else:
+        traffic, tsrc = committed_traffic(res["name"], kern)
+    roof = launch_roofline(jobs, res["events"], info, traffic, tsrc)
+    t_step = res["secs"] / args.steps
+    V = sum(j.V for j in jobs)
+    E = sum(j.E for j in jobs)
+    B = sum(j.B for j in jobs)
+    fwd_bytes, fwd_flops = forward_bytes_flops(V, E, B, res["h"], res["depth"], b=2 if res["bf16"] else 4)
+    mfma_peak = PEAK_16BIT_MFMA_TFLOPS if res["bf16"] else PEAK_FP32_MFMA_TFLOPS
+    t_min = max(fwd_bytes / (PEAK_HBM_GBPS * 1e9), fwd_flops / (mfma_peak * 1e12))
+    return roof, {
+        "alg_bytes_per_rank": fwd_bytes, "flops_per_rank": fwd_flops,
+        "hbm_frac": fwd_bytes / t_step / (PEAK_HBM_GBPS * 1e9),
+        "mfma_frac": fwd_flops / t_step / (mfma_peak * 1e12),
+        "binding_frac": t_min / t_step,
+    }
+
+
 def main():
     args = parse()
     env = dist_env()
@@ -162,258 +457,76 @@ def main():
     dev = torch.device("cuda", env.local_rank)
 
     from notorch_amd import _lib
-    from notorch_amd.data.synth import make_batch
-    from notorch_amd.nn import ChempropBlock, EmbeddedChempropBlock, GraphEmbedding, Sum
-    from notorch_amd.nn.gnn import _engine
 
     _lib.load()  # fail loudly if the HIP extension is missing
-    kind, n_mols, h, depth, sdtype = WORKLOADS[args.workload]
-    bf16 = sdtype == "bf16"
-    torch.manual_seed(0)
-    batch = make_batch(kind, n_mols, seed=1000 + env.rank)
-    G = batch.collate("nodes")
-    embedding = GraphEmbedding(42, 13, h)  # same RNG draws as two EmbeddingBag(42|13, h) in order
-    with torch.no_grad():
-        Xv, Xe = embedding.node(G.node_feats), embedding.edge(G.edge_feats)
-    block = ChempropBlock(hidden_dim=h, depth=depth).eval()
-    readout = Sum()
-    if bf16:  # bf16 storage: the CPU baseline runs the fp32 oracle on the same bf16-rounded values
-        block = block.to(torch.bfloat16)
-        embedding = embedding.to(torch.bfloat16)
-        Xv, Xe = Xv.to(torch.bfloat16), Xe.to(torch.bfloat16)
-    Ws = [l.linear.weight.detach().float().clone() for l in block._chemprop_layers()]
-    bs = [l.linear.bias.detach().float().clone() for l in block._chemprop_layers()]
-    block = block.to(dev)
-    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(dev)
-    Xv, Xe = Xv.float(), Xe.float()
-    V, E, B = G.num_nodes, G.num_edges, len(G)
-    torch.cuda.synchronize(dev)
+    res = run_workload(args.workload, args, env, dev, headline=True)
+    job = res["jobs"][0]
+    fresh = embedded = e2e = None
+    if not args.no_embedded and res["kind"] != "qm9v":
+        fresh = fresh_batch_leg(res, args, env, dev)
+        embedded = embedded_leg(res, args, env, dev)
+        if env.rank == 0:
+            e2e = end_to_end_leg(res, dev)
+    roof, fwd = summary(res, args, env, args.pmc_csv)
 
-    def step():
-        out = block(Gd)
-        return readout(out)
+    secondary = None
+    if not args.no_secondary and args.workload == "qm9-4096":
+        secondary = {}
+        for name in SECONDARY:
+            r2 = run_workload(name, args, env, dev, headline=False)
+            roof2, fwd2 = summary(r2, args, env)
+            secondary[name] = {
+                "config": f"{r2['n_mols']} {r2['kind']}-shaped molecules per GPU, depth={r2['depth']} "
+                          f"hidden={r2['h']}, {'bf16' if r2['bf16'] else 'f32'}",
+                "value": r2["rate"], "unit": "edge-messages/s", "ms_per_step": r2["secs"] / args.steps * 1e3,
+                "V_per_gpu": r2["jobs"][0].V, "E_per_gpu": r2["jobs"][0].E,
+                "roofline": roof2, "forward_roofline": fwd2,
+            }
+            del r2
 
-    with torch.no_grad():
-        for _ in range(args.warmup):
-            step()
-        events = []
-        _engine.UPDATE_EVENTS = events
-        if env.distributed:
-            dist.barrier()
-        torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize(dev)
-        if env.distributed:
-            dist.barrier()
-        elapsed = time.perf_counter() - t0
-        _engine.UPDATE_EVENTS = None
-
-    # Second, smaller measurement (not `value`): the whole encoder from the collated type indices,
-    # GraphEmbedding fused into the initial gather (EmbeddedChempropBlock) + Sum readout.
-    embedded = None
-    if not args.no_embedded:
-        Graw = batch.collate("nodes").to(dev)
-        embedded = {
-            "step": "GraphEmbedding + ChempropBlock + Sum from the collated integer type indices "
-                    "(EmbeddedChempropBlock; fused = embedding folded into the initial gather, "
-                    "unfused = nt_embed_bag kernels then the block)",
+    cpu = None
+    if not args.no_cpu_baseline and env.world_size == 1 and env.rank == 0:
+        cpu = cpu_baseline(job, res["embedding"], args.cpu_seconds)
+    if env.rank == 0:
+        sharded = res["kind"] == "qm9v"
+        line = {
+            "metric": METRIC,
+            "value": res["rate"],
             "unit": "edge-messages/s",
+            "n_gpus": env.world_size,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": res["secs"] / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong" if sharded else "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if res["bf16"] else "f32",
+            "mfma_numerics": res["info"].get("numerics", "?"),
+            "data": f"synthetic (seeded {res['kind']}-shaped molecules, random-init EmbeddingBag + weights)",
+            "config": {
+                "workload": (f"{args.workload}: {res['n_mols']} qm9-shaped molecules in {N_SHARDS} edge-balanced "
+                             f"shards, rank r runs shards r, r+N, ...; D-MPNN depth={res['depth']} hidden={res['h']}"
+                             if sharded else
+                             f"{args.workload}: {res['n_mols']} {res['kind']}-shaped molecules per GPU, D-MPNN "
+                             f"depth={res['depth']} hidden={res['h']}")
+                + ", ChempropBlock + Sum readout, reference collate (rev offset by nodes)",
+                "molecules_per_gpu": sum(j.B for j in res["jobs"]),
+                "V_per_gpu": sum(j.V for j in res["jobs"]),
+                "E_per_gpu": sum(j.E for j in res["jobs"]),
+                "shards_on_rank0": len(res["jobs"]) if sharded else None,
+                "hidden": res["h"],
+                "depth": res["depth"],
+                "parallelism": f"molecule-sharded x{env.world_size}, no collective on the forward path",
+            },
+            "roofline": roof,
+            "forward_roofline": fwd,
+            "secondary": secondary,
+            "fresh_batch": fresh,
+            "embedded_encoder": embedded,
+            "end_to_end": e2e,
+            "cpu_baseline": cpu,
         }
-        for fuse in (True, False):
-            enc = EmbeddedChempropBlock(embedding, block, fuse=fuse).eval().to(dev)
-            with torch.no_grad():
-                for _ in range(max(2, args.warmup // 2)):
-                    readout(enc(Graw))
-                if env.distributed:
-                    dist.barrier()
-                torch.cuda.synchronize(dev)
-                t1 = time.perf_counter()
-                for _ in range(args.steps):
-                    readout(enc(Graw))
-                torch.cuda.synchronize(dev)
-                if env.distributed:
-                    dist.barrier()
-                e_el = time.perf_counter() - t1
-            _, e_secs, e_rate = aggregate_throughput(E * depth * args.steps, e_el, device=dev)
-            tag = "fused" if fuse else "unfused"
-            embedded[f"{tag}_ms_per_step"] = e_secs / args.steps * 1e3
-            embedded[f"{tag}_value"] = e_rate
-
-    # Third (reported separately, never `value`): end to end from host Graph objects —
-    # native collate on the host, H2D copy (pageable), then the fused embedded encoder + readout.
-    end_to_end = None
-    if not args.no_embedded and env.rank == 0:
-        from notorch_amd.data.models.graph import BatchedGraph
-
-        graphs = batch.to_graphs()
-        enc = EmbeddedChempropBlock(embedding, block, fuse=True).eval().to(dev)
-        parts = {"collate": [], "h2d": [], "device": []}
-        with torch.no_grad():
-            for it in range(6):
-                torch.cuda.synchronize(dev)
-                t_a = time.perf_counter()
-                Gh = BatchedGraph.from_graphs(graphs)
-                t_b = time.perf_counter()
-                Gdev = Gh.to(dev)
-                torch.cuda.synchronize(dev)
-                t_c = time.perf_counter()
-                readout(enc(Gdev))
-                torch.cuda.synchronize(dev)
-                t_d = time.perf_counter()
-                if it:  # the first pass builds caches
-                    parts["collate"].append(t_b - t_a)
-                    parts["h2d"].append(t_c - t_b)
-                    parts["device"].append(t_d - t_c)
-        med = {k: statistics.median(v) * 1e3 for k, v in parts.items()}
-        total = sum(med.values())
-        end_to_end = {
-            "step": f"{B} host Graphs -> BatchedGraph.from_graphs (native collate) -> .to(device) "
-                    "(pageable H2D) -> EmbeddedChempropBlock + Sum; rank 0, median of 5",
-            "collate_ms": med["collate"], "h2d_ms": med["h2d"], "device_ms": med["device"],
-            "total_ms": total, "value": E * depth / (total * 1e-3), "unit": "edge-messages/s",
-        }
-
-    from notorch_amd import kernels as K
-
-    lay = getattr(Gd, "_nt_layout", None)
-    used_fused = bool(
-        lay is not None and _engine._fused_enabled() and K.fused_supported(V, E, h, Gd.edge_feats.dtype)
-        and _engine.fused_plan(lay, V, E) is not None
-    )
-    upd_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
-    units, secs, rate = aggregate_throughput(E * depth * args.steps, elapsed, device=dev)
-    if env.rank != 0:
-        if env.distributed:
-            dist.destroy_process_group()
-        return
-
-    flops_upd = 2 * E * h * h
-    upd_bytes = update_bytes(V, E, h)
-    variant = os.environ.get("NT_UPDATE_KERNEL", "as")
-    fused = used_fused
-    persistent = (not fused and not bf16 and _engine._fused_enabled()
-                  and K.fused_supported(V, E, h, Gd.edge_feats.dtype))
-    traffic = read_pmc_traffic(args.pmc_csv) if args.pmc_csv else None
-    if bf16:
-        # native bf16 MFMA (16x16x32, K padded to 32, N to 16); HBM bytes at 2 B per element
-        kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
-        upd_bytes = update_bytes(V, E, h, b=2)
-        bf16_flops = 2 * E * kp * np_
-        t_hbm = upd_bytes / (PEAK_HBM_GBPS * 1e9)
-        t_mfma = bf16_flops / (PEAK_BF16_MFMA_TFLOPS * 1e12)
-        bound = "hbm" if t_hbm >= t_mfma else "mfma"
-        if bound == "hbm":
-            achieved, peak, unit = upd_bytes / (upd_ms * 1e-3) / 1e9, PEAK_HBM_GBPS, "GB/s"
-        else:
-            achieved, peak, unit = bf16_flops / (upd_ms * 1e-3) / 1e12, PEAK_BF16_MFMA_TFLOPS, "TFLOP/s"
-        kname = "nt_dmpnn_update (update_bf16_kernel: 64-edge tiles, bf16 16x16x32 MFMA, fp32 accumulate)"
-        extra = {
-            "mfma_bf16_tflops": bf16_flops / (upd_ms * 1e-3) / 1e12,
-            "mfma_bf16_frac": bf16_flops / (upd_ms * 1e-3) / 1e12 / PEAK_BF16_MFMA_TFLOPS,
-            "hbm_frac": upd_bytes / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
-            "t_min_us": max(t_hbm, t_mfma) * 1e6,
-        }
-        x6 = False
-    elif fused or persistent or (h % 4 == 0 and 97 <= h <= 512 and variant[0] in "axp"):
-        # bf16x6 fp32 emulation: 6 bf16 MFMA products per fp32 product.  Fused / as16 kernels run
-        # v_mfma_f32_16x16x32_bf16 (K padded to 32, N to 16); x6 runs 32x32x16 (K to 16, N to 32).
-        if fused or persistent or variant[0] == "a":
-            kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
-        else:
-            kp, np_ = 16 * ((h + 15) // 16), 32 * ((h + 31) // 32)
-        if fused:
-            upd_bytes = fused_bytes(V, E, h)
-            fk = os.environ.get("NT_FUSED_KERNEL", "pk")
-            kname = ("nt_dmpnn_update_fused (update_%s_kernel: persistent producer/consumer, "
-                     "bf16x6 16x16x32 MFMA, aggregation of the next layer fused)" % ("ps" if fk == "ps" else "pk"))
-        elif persistent:
-            kname = ("nt_dmpnn_update_fused without tile plan (update_pk_kernel, bf16x6 16x16x32 MFMA; "
-                     "hub graph: aggregation by the chunked segment reduce)")
-        else:
-            kname = f"nt_dmpnn_update (bf16x6 variant {variant})"
-        bf16_flops = 6 * 2 * E * kp * np_
-        t_hbm = upd_bytes / (PEAK_HBM_GBPS * 1e9)
-        t_mfma = bf16_flops / (PEAK_BF16_MFMA_TFLOPS * 1e12)
-        bound = "hbm" if t_hbm >= t_mfma else "mfma"
-        if bound == "hbm":
-            achieved, peak, unit = upd_bytes / (upd_ms * 1e-3) / 1e9, PEAK_HBM_GBPS, "GB/s"
-        else:
-            achieved, peak, unit = bf16_flops / (upd_ms * 1e-3) / 1e12, PEAK_BF16_MFMA_TFLOPS, "TFLOP/s"
-        extra = {
-            "mfma_bf16_tflops": bf16_flops / (upd_ms * 1e-3) / 1e12,
-            "mfma_bf16_frac": bf16_flops / (upd_ms * 1e-3) / 1e12 / PEAK_BF16_MFMA_TFLOPS,
-            "hbm_frac": upd_bytes / (upd_ms * 1e-3) / 1e9 / PEAK_HBM_GBPS,
-            "fp32_equiv_tflops": flops_upd / (upd_ms * 1e-3) / 1e12,
-            "t_min_us": max(t_hbm, t_mfma) * 1e6,
-        }
-        x6 = True
-    else:
-        x6 = False
-        bound = "mfma"
-        achieved, peak, unit = flops_upd / (upd_ms * 1e-3) / 1e12, PEAK_FP32_MFMA_TFLOPS, "TFLOP/s"
-        kname = "nt_dmpnn_update (fp32 16x16x4 MFMA, variant %s)" % variant
-        extra = {"alg_hbm_gbps": upd_bytes / (upd_ms * 1e-3) / 1e9}
-    fwd_bytes, fwd_flops = forward_bytes_flops(V, E, B, h, depth, b=2 if bf16 else 4)
-    t_step = secs / args.steps
-    mfma_peak = PEAK_BF16_MFMA_TFLOPS if bf16 else PEAK_FP32_MFMA_TFLOPS
-    t_min = max(fwd_bytes / (PEAK_HBM_GBPS * 1e9), fwd_flops / (mfma_peak * 1e12))
-    line = {
-        "metric": METRIC,
-        "value": rate,
-        "unit": "edge-messages/s",
-        "n_gpus": env.world_size,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": t_step * 1e3,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16" if bf16 else "f32",
-        "mfma_numerics": ("bf16 MFMA, fp32 accumulate" if bf16 else
-                          "bf16x6 split (fp32-accurate)" if x6 else "fp32 MFMA"),
-        "data": f"synthetic (seeded {kind}-shaped molecules per rank, random-init EmbeddingBag + weights)",
-        "config": {
-            "workload": f"{args.workload}: {n_mols} {kind}-shaped molecules per GPU, D-MPNN depth={depth} "
-            f"hidden={h}, ChempropBlock + Sum readout, reference collate (rev offset by nodes)",
-            "molecules_per_gpu": n_mols,
-            "V_per_gpu": V,
-            "E_per_gpu": E,
-            "hidden": h,
-            "depth": depth,
-            "parallelism": f"molecule-sharded x{env.world_size}, no collective on the forward path",
-        },
-        "roofline": {
-            "kernel": kname,
-            "bound": bound,
-            "achieved": achieved,
-            "peak": peak,
-            "unit": unit,
-            "frac": achieved / peak,
-            "traffic": traffic,
-            "launch_ms": upd_ms,
-            "launches_timed": len(events),
-            "alg_bytes_per_launch": upd_bytes,
-            "flops_per_launch_fp32": flops_upd,
-            "alg_hbm_gbps": upd_bytes / (upd_ms * 1e-3) / 1e9,
-            **extra,
-        },
-        "embedded_encoder": embedded,
-        "end_to_end": end_to_end,
-        "forward_roofline": {
-            "alg_bytes": fwd_bytes,
-            "flops": fwd_flops,
-            "hbm_frac": fwd_bytes / t_step / (PEAK_HBM_GBPS * 1e9),
-            "mfma_frac": fwd_flops / t_step / (mfma_peak * 1e12),
-            "binding_frac": t_min / t_step,
-        },
-    }
-    if not args.no_cpu_baseline and env.world_size == 1:
-        line["cpu_baseline"] = cpu_baseline(G, Xv, Xe, Ws, bs, depth, args.cpu_seconds)
-    else:
-        line["cpu_baseline"] = None
-    print(json.dumps(line), flush=True)
+        print(json.dumps(line), flush=True)
     if env.distributed:
         dist.destroy_process_group()
 

@@ -12,7 +12,11 @@ import ctypes
 import os
 import threading
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libnotorch_amd.so")
+_LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
+# NT_LIB=diag loads the diagnostic build (make DIAG=1: A/B kernel variants selectable by NT_*
+# environment variables, ablation / stamp builds); the default is the shipping library.
+DIAG = os.environ.get("NT_LIB", "") == "diag"
+LIB_PATH = os.path.join(_LIB_DIR, "libnotorch_amd_diag.so" if DIAG else "libnotorch_amd.so")
 ABI_VERSION = 1
 
 NT_F32, NT_BF16 = 0, 1

@@ -26,15 +26,21 @@ __global__ void csr_keys_kernel(const int64_t* __restrict__ idx, int64_t n, int6
   }
 }
 
-// seg_ptr[s] = first position p with keys[p] >= s  (lower bound), for s in [0, nseg].
+// seg_ptr[s] = first position p with keys[p] >= s  (lower bound), for s in [0, nseg]: one thread
+// per segment, binary search in the sorted keys.  (A thread per position filling the empty
+// segments after it was serial in the length of an empty run: the rev_index CSR of a compat-mode
+// batch has tens of thousands of empty segments in one run, 264 us per build.)
 __global__ void csr_bounds_kernel(const uint32_t* __restrict__ keys, int64_t n, int64_t nseg,
                                   int32_t* __restrict__ seg_ptr) {
-  for (int64_t p = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; p <= n;
-       p += (int64_t)gridDim.x * blockDim.x) {
-    int64_t lo = (p == 0) ? -1 : (int64_t)keys[p - 1];
-    int64_t hi = (p == n) ? nseg : (int64_t)keys[p];
-    if (hi > nseg) hi = nseg;
-    for (int64_t s = lo + 1; s <= hi; ++s) seg_ptr[s] = (int32_t)p;
+  for (int64_t s = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; s <= nseg;
+       s += (int64_t)gridDim.x * blockDim.x) {
+    int64_t lo = 0, hi = n;  // first p in [0, n] with keys[p] >= s
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if ((int64_t)keys[mid] < s) lo = mid + 1;
+      else hi = mid;
+    }
+    seg_ptr[s] = (int32_t)lo;
   }
 }
 
@@ -88,7 +94,7 @@ extern "C" int nt_csr_build(const int64_t* idx, int64_t n, int64_t nseg, int32_t
   while (end_bit < 32 && ((uint64_t)nseg >> end_bit) != 0) ++end_bit;  // bits to hold sentinel nseg
   NT_HIP(hipcub::DeviceRadixSort::SortPairs(ws, temp_bytes, keys_in, keys_out, vals_in, perm, (int)n,
                                             0, end_bit, stream));
-  csr_bounds_kernel<<<grid_for(n + 1, 256), 256, 0, stream>>>(keys_out, n, nseg, seg_ptr);
+  csr_bounds_kernel<<<grid_for(nseg + 1, 256), 256, 0, stream>>>(keys_out, n, nseg, seg_ptr);
   NT_LAUNCH_CHECK();
   return NT_OK;
 }

@@ -279,8 +279,11 @@ template <int KS, int ACT>
 int launch_as(const UpdateArgs& a) {
   const int64_t grid = (a.E + kRows - 1) / kRows;
   NT_REQUIRE(grid < (int64_t(1) << 31), NT_EINVAL, "too many edges");
+  auto kern = update_as_kernel<KS, ACT>;
+#ifdef NT_DIAG
   const char* dg = getenv("NT_AS_DIAG");
-  auto kern = (dg && dg[0] == '1') ? update_as_kernel<KS, ACT, true> : update_as_kernel<KS, ACT>;
+  if (dg && dg[0] == '1') kern = update_as_kernel<KS, ACT, true>;
+#endif
   kern<<<(unsigned)grid, kThreads, 0, a.stream>>>(
       (const float4*)a.H, (const float4*)a.S, a.src, a.rev, (const uint4*)a.Wp,
       (const float4*)a.b, a.V, a.E, (int)(a.h / 4), (int)((a.h + 15) / 16), a.residual, a.act,
@@ -327,6 +330,7 @@ int launch_update_as(const UpdateArgs& a) {
 }  // namespace nt
 
 // Debug-only (not part of include/notorch_amd.h): read (and optionally reset) the stamp sums of the
+#ifdef NT_DIAG
 // diagnostic as16 build (NT_AS_DIAG=1).
 extern "C" __attribute__((visibility("default"))) int nt_debug_as_stamps(unsigned long long* out7,
                                                                          int reset) {
@@ -341,3 +345,4 @@ extern "C" __attribute__((visibility("default"))) int nt_debug_as_stamps(unsigne
   }
   return 0;
 }
+#endif  // NT_DIAG

@@ -42,8 +42,12 @@ constexpr int kWaves = 4;
 //                      | pc (producer/consumer bf16x6)
 //                      | glds | ring | stream | tile (exact fp32 MFMA)
 static char update_kernel_choice() {
+#ifdef NT_DIAG
   const char* v = getenv("NT_UPDATE_KERNEL");
   return (v && v[0]) ? v[0] : 'a';
+#else
+  return 'a';  // shipping build: as16 (h <= 304), x6 (h <= 512), fp32 MFMA tile kernel
+#endif
 }
 
 struct UpdateGeom {
@@ -266,6 +270,7 @@ __global__ void __launch_bounds__(kThreads, 2) dmpnn_update_f32(
 // MFMAs for real tiles (no padding tiles).  Epilogue: per 16-row tile, each wave stages its
 // C fragments in a wave-private LDS slab and stores whole 16-B row pieces (+bias +residual).
 // ------------------------------------------------------------------------------------------
+#ifdef NT_DIAG  // A/B-only streamed variant (make DIAG=1)
 #ifndef NT_STREAM_WAVES
 #define NT_STREAM_WAVES 2  // min waves per SIMD the streamed kernel is register-allocated for
 #endif
@@ -439,6 +444,8 @@ static int launch_stream(const float* H, const float* S, const int64_t* src, con
   return NT_OK;
 }
 
+#endif  // NT_DIAG
+
 template <int BM, int CPW, int ACT, bool VEC>
 static int launch_update(const float* H, const float* S, const int64_t* src, const int64_t* rev,
                          const float4* Wp, const float* b, int64_t V, int64_t E, int h,
@@ -463,6 +470,7 @@ static int dispatch_act_vec(const float* H, const float* S, const int64_t* src, 
                             const float4* Wp, const float* b, int64_t V, int64_t E, int h,
                             const UpdateGeom& g, int residual, int act, float alpha, float* H_out,
                             bool vec, hipStream_t stream) {
+#ifdef NT_DIAG
   if (vec && update_kernel_choice() == 's') {
     return act == NT_ACT_RELU
                ? launch_stream<CPW, NT_ACT_RELU>(H, S, src, rev, Wp, b, V, E, h, g, residual, act,
@@ -470,6 +478,7 @@ static int dispatch_act_vec(const float* H, const float* S, const int64_t* src, 
                : launch_stream<CPW, -1>(H, S, src, rev, Wp, b, V, E, h, g, residual, act, alpha,
                                         H_out, stream);
   }
+#endif
   if (act == NT_ACT_RELU) {
     return vec ? launch_update<BM, CPW, NT_ACT_RELU, true>(H, S, src, rev, Wp, b, V, E, h, g,
                                                            residual, act, alpha, H_out, stream)
@@ -586,18 +595,21 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
     return launch_update_as(a);
   }
+#ifdef NT_DIAG
   if (vec && choice == 'p' && pc_supported(h)) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, (const char*)Wp + f32_image_bytes(h),
                  (const float*)b, V, E, h, g.KB, g.NT, residual, act, act_alpha, (float*)H_out,
                  stream};
     return launch_update_pc(a);
   }
+#endif
   if (vec && (choice == 'x' || choice == 'p' || choice == 'a') && x6_supported(h)) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, (const char*)Wp + f32_image_bytes(h),
                  (const float*)b, V, E, h, g.KB, g.NT, residual, act, act_alpha, (float*)H_out,
                  stream};
     return launch_update_x6(a);
   }
+#ifdef NT_DIAG
   if (vec && choice == 'r' && g.NT <= 24) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
@@ -608,6 +620,7 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
     return launch_update_glds(a);
   }
+#endif
   // 64-edge tiles while two workgroups still fit one CU's LDS (h <= 304), else 32-edge tiles.
   if (lds_bytes<64>(g) <= 80 * 1024)
     return dispatch_cpw<64>((const float*)H, (const float*)S, src, rev, (const float4*)Wp,

@@ -17,6 +17,8 @@
 //   * Epilogue: accumulators staged per wave through LDS in column groups of <= 10 tiles, then
 //     bias + residual + store as 16-B row pieces.
 // Roofline: MFMA-bound (2 h^2 flop per edge vs ~16 h bytes per edge, 51 flop/B at h = 300).
+// A/B-only kernel: compiled into the diagnostic library (make DIAG=1) only.
+#ifdef NT_DIAG
 #include "common.hpp"
 #include "update.hpp"
 
@@ -438,3 +440,4 @@ int launch_update_glds(const UpdateArgs& a) {
 }
 
 }  // namespace nt
+#endif  // NT_DIAG

@@ -17,6 +17,8 @@
 //   * one workgroup barrier per K-step; every ring slot is its own __shared__ object so hipcc
 //     places no vmcnt drain in front of reads of the current slot.
 // Workgroup = 12 waves (768 lanes), 128 edges x all h columns, 1 workgroup per CU (3 waves/SIMD).
+// A/B-only kernel: compiled into the diagnostic library (make DIAG=1) only.
+#ifdef NT_DIAG
 #include <stdlib.h>
 
 #include <type_traits>
@@ -458,3 +460,4 @@ extern "C" __attribute__((visibility("default"))) int nt_debug_pc_stamps(unsigne
   }
   return 0;
 }
+#endif  // NT_DIAG

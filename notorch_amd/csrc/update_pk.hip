@@ -603,12 +603,14 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
 
 template <int KS, int ACT, int AACT, bool SUMONLY>
 int launch_pk(const Args& a, int grid, hipStream_t stream) {
-  // NT_PK_CW=1: consumers store H' (measured slower at config 2: 157 vs 143 us; the consumers, not
-  // the producers, are the critical role), kept for A/B
+  auto kern = update_pk_kernel<KS, ACT, AACT, SUMONLY>;
+#ifdef NT_DIAG
+  // A/B builds (make DIAG=1): NT_PK_CW=1 consumers store H' (measured slower at config 2: 157 vs
+  // 143 us), NT_PK_PF=4 the full next-step prefetch, NT_PK_DIAG=1 stamps, NT_PK_ABL=m ablations
+  // (timing only: outputs are wrong)
   const char* cw = getenv("NT_PK_CW");
-  auto kern = (cw && cw[0] == '1') ? update_pk_kernel<KS, ACT, AACT, SUMONLY, false, 0, true>
-                                   : update_pk_kernel<KS, ACT, AACT, SUMONLY>;
-  const char* pf = getenv("NT_PK_PF");  // NT_PK_PF=4: the full next-step prefetch, for A/B
+  if (cw && cw[0] == '1') kern = update_pk_kernel<KS, ACT, AACT, SUMONLY, false, 0, true>;
+  const char* pf = getenv("NT_PK_PF");
   if (pf && pf[0] == '4') kern = update_pk_kernel<KS, ACT, AACT, SUMONLY, false, 0, false, 4>;
   if constexpr (KS == 10 && ACT == NT_ACT_RELU && SUMONLY) {
     const char* d = getenv("NT_PK_DIAG");
@@ -622,6 +624,7 @@ int launch_pk(const Args& a, int grid, hipStream_t stream) {
     if (m == 9) kern = update_pk_kernel<KS, ACT, AACT, SUMONLY, false, 9>;
     if (m == 15) kern = update_pk_kernel<KS, ACT, AACT, SUMONLY, false, 15>;
   }
+#endif
   kern<<<grid, kThreads, 0, stream>>>(a);
   NT_LAUNCH_CHECK();
   return NT_OK;
@@ -669,12 +672,13 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
   a.aalpha = aalpha;
   a.O4 = (float4*)u.H_out;
   a.SO4 = (float4*)S_out;
+  a.prio = 0;  // age arbitration (consumer priority measured +-1%: A/B only)
+#ifdef NT_DIAG
   {
-    // default 0 (age arbitration): consumer priority was ~1% ahead before the finish rows were
-    // batched, and ~1% behind after (A/B in tools/pk_ab.sh); kept selectable
     const char* pr = getenv("NT_PK_PRIO");
     a.prio = pr && pr[0] ? atoi(pr) : 0;
   }
+#endif
   if (a.ntiles == 0) return NT_OK;
   const int grid = a.ntiles < cu_count() ? a.ntiles : cu_count();
   const int KS = (int)((u.h + 31) / 32);
@@ -705,6 +709,7 @@ extern "C" __attribute__((visibility("default"))) int nt_debug_pk_timeouts(unsig
   return 0;
 }
 
+#ifdef NT_DIAG
 extern "C" __attribute__((visibility("default"))) int nt_debug_pk_stamps(unsigned long long* out9,
                                                                          int reset) {
   if (hipMemcpyFromSymbol(out9, HIP_SYMBOL(nt::g_pk_stamps), 9 * sizeof(unsigned long long), 0,
@@ -718,3 +723,4 @@ extern "C" __attribute__((visibility("default"))) int nt_debug_pk_stamps(unsigne
   }
   return 0;
 }
+#endif  // NT_DIAG

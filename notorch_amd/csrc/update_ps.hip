@@ -42,6 +42,7 @@
 
 namespace nt {
 
+#ifdef NT_DIAG  // the A/B persistent "ps" kernel (make DIAG=1)
 // Diagnostic build (NT_PS_ABL=16): cycles summed over waves.  Producers: [0] finish, [1] wait B3,
 // [2] gather, [3] wait B1+B2; consumers: [4] steps before B3, [5] wait B3, [6] steps after,
 // [7] wait B1, [8] staging + B2; [9] producer waves, [10] consumer waves.
@@ -515,6 +516,11 @@ __global__ void __launch_bounds__(kThreads, 1) update_ps_kernel(Args a) {
   }
 }
 
+}  // namespace
+#endif  // NT_DIAG
+
+namespace {
+
 // tile_ptr[k] = dst_ptr[first v with dst_ptr[v] >= k L], k < ntiles; tile_ptr[ntiles] = E.
 __global__ void tile_plan_kernel(const int32_t* __restrict__ dst_ptr, int64_t V, int64_t E, int L,
                                  int ntiles, int32_t* __restrict__ tile_ptr) {
@@ -546,6 +552,7 @@ __global__ void dst_sorted_kernel(const int32_t* __restrict__ dst_ptr, int64_t V
 int cu_count();
 namespace {
 
+#ifdef NT_DIAG
 template <int KS, int ACT, int AACT, bool SUMONLY>
 int launch_ps(const Args& a, hipStream_t stream) {
   const int grid = a.ntiles < cu_count() ? a.ntiles : cu_count();
@@ -583,6 +590,7 @@ int dispatch_ps(const Args& a, int ks, hipStream_t stream, std::integer_sequence
   return rc;
 }
 
+#endif  // NT_DIAG
 }  // namespace
 
 int cu_count() {
@@ -642,6 +650,7 @@ int launch_update_ps(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
   const bool fused = tile_ptr != nullptr;
   NT_REQUIRE(fused == (S_out != nullptr), NT_EINVAL, "S_out must be given exactly with a tile plan");
   NT_REQUIRE(!fused || (perm && dsts), NT_EINVAL, "fused mode needs perm and dst_sorted");
+#ifdef NT_DIAG
   // kernel choice (A/B): NT_FUSED_KERNEL = pk (default: K-slice ring of pre-split A) | ps
   const char* fk = getenv("NT_FUSED_KERNEL");
   if (!(fk && fk[0] == 'p' && fk[1] == 's'))
@@ -683,9 +692,13 @@ int launch_update_ps(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
   if (relu && sum && aact == NT_ACT_IDENTITY)
     return dispatch_ps<NT_ACT_RELU, NT_ACT_IDENTITY, true>(a, KS, u.stream, Seq{});
   return dispatch_ps<-1, -1, false>(a, KS, u.stream, Seq{});
+#else
+  return launch_update_pk(u, tile_ptr, ntiles, perm, dsts, reduce, aact, aalpha, S_out);
+#endif
 }
 }  // namespace nt
 
+#ifdef NT_DIAG
 // Debug-only (not part of include/notorch_amd.h): read (and optionally reset) the stamp sums of the
 // diagnostic ps build (NT_PS_ABL=16).
 extern "C" __attribute__((visibility("default"))) int nt_debug_ps_stamps(unsigned long long* out11,
@@ -701,3 +714,4 @@ extern "C" __attribute__((visibility("default"))) int nt_debug_ps_stamps(unsigne
   }
   return 0;
 }
+#endif  // NT_DIAG

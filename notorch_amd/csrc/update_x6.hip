@@ -469,8 +469,12 @@ int launch_x6(const UpdateArgs& a) {
 //   "a" = 64 rows, 2-slot rings   "b" = 128 rows, 2-slot rings
 //   "c" = 128 rows, 3-slot S/H ring   "d" = 128 rows, 3-slot S/H and W rings
 static char x6_cfg() {
+#ifdef NT_DIAG
   const char* v = getenv("NT_X6_CFG");
   return (v && v[0]) ? v[0] : 'a';
+#else
+  return 'a';
+#endif
 }
 
 // static LDS bytes of a configuration (must stay <= 160 KiB)
@@ -484,6 +488,7 @@ constexpr int x6_lds_bytes() {
 
 template <int NT32, int ACT>
 int launch_x6_cfg(const UpdateArgs& a) {
+#ifdef NT_DIAG
   if constexpr (ACT == NT_ACT_RELU && X6Geom<NT32, 4>::kFits) {
     const char c = x6_cfg();
     if (c == 'b') return launch_x6<NT32, 4, 2, 2, ACT>(a);
@@ -501,6 +506,7 @@ int launch_x6_cfg(const UpdateArgs& a) {
       if (c == 's') return launch_x6<NT32, 2, 2, 2, ACT, 8>(a);
     }
   }
+#endif
   return launch_x6<NT32, 2, 2, 2, ACT>(a);
 }
 
@@ -543,6 +549,7 @@ int launch_update_x6(const UpdateArgs& a) {
 }  // namespace nt
 
 // Debug-only (not part of include/notorch_amd.h): read (and optionally reset) the stamp sums of the
+#ifdef NT_DIAG
 // diagnostic x6 build selected with NT_UPDATE_KERNEL=x6 NT_X6_CFG=s.
 extern "C" __attribute__((visibility("default"))) int nt_debug_x6_stamps(unsigned long long* out5,
                                                                          int reset) {
@@ -557,3 +564,4 @@ extern "C" __attribute__((visibility("default"))) int nt_debug_x6_stamps(unsigne
   }
   return 0;
 }
+#endif  // NT_DIAG

@@ -21,6 +21,7 @@ bit for bit; ``rev_offset="edges"`` is the corrected collate.
 """
 from __future__ import annotations
 
+import weakref
 from copy import copy
 from dataclasses import InitVar, dataclass, field
 from typing import Iterable, Literal, Optional
@@ -59,10 +60,34 @@ class DeviceLayout:
     plan: object = None
     # backward CSRs (src -> nodes, rev_index -> edges), built lazily by _engine.backward_layout
     bwd: object = None
+    # host-computed statistics the collate ships with the CSR, so a fresh batch needs no
+    # device -> host sync: (max, min) in-degree, largest molecule, (min, max) type index of the
+    # node / edge feature columns when they are integer type matrices
+    deg_range: Optional[tuple] = None
+    mol_max: Optional[int] = None
+    type_range: Optional[tuple] = None
+    # chunk plan of the dst CSR (hubs) and of the molecule CSR (large molecules): tensors or False
+    dst_chunks: object = None
+    mol_chunks: object = None
+    type_src: object = None  # (weakref node_feats, weakref edge_feats) type_range was taken from
+
+    def __getstate__(self):
+        # weak references do not pickle (DataLoader workers ship collated graphs): mark the type
+        # statistics as describing the owning graph's features; Graph.__setstate__ re-binds them
+        st = dict(self.__dict__)
+        if st.get("type_src") is not None:
+            st["type_src"] = "owner"
+        return st
 
     def to(self, device, edge_index: Tensor, batch_node_index: Optional[Tensor]) -> "DeviceLayout":
         mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731
-        return DeviceLayout(
+
+        def mv_plan(p):  # (tensors and ints) tuples or False / None
+            if not p:
+                return p
+            return tuple(x.to(device, non_blocking=True) if isinstance(x, Tensor) else x for x in p)
+
+        new = DeviceLayout(
             mv(self.dst_ptr),
             mv(self.dst_perm),
             mv(self.mol_ptr),
@@ -71,6 +96,12 @@ class DeviceLayout:
             batch_node_index,
             self.validated,
         )
+        new.plan = mv_plan(self.plan)
+        new.deg_range, new.mol_max, new.type_range = self.deg_range, self.mol_max, self.type_range
+        new.dst_chunks = mv_plan(self.dst_chunks)
+        if self.mol_chunks is not None and new.mol_ptr is not None:
+            new.mol_chunks = (new.mol_ptr, mv_plan(self.mol_chunks[1]))
+        return new
 
 
 @dataclass(repr=False, eq=False)
@@ -102,18 +133,36 @@ class Graph(UpdateMixin):
         return self._device
 
     def to(self, device):
+        types_ok = self._layout_types_ok()
         self._device = device
         self.node_feats = self.node_feats.to(device)
         self.edge_feats = self.edge_feats.to(device)
         self.edge_index = self.edge_index.to(device)
         self.rev_index = self.rev_index.to(device)
-        self._move_layout(device)
+        self._move_layout(device, types_ok)
         return self
 
-    def _move_layout(self, device):
+    def __setstate__(self, state):
+        self.__dict__.update(state)
+        lay = state.get("_nt_layout")
+        if lay is not None and lay.type_src == "owner":
+            lay.type_src = (weakref.ref(self.node_feats), weakref.ref(self.edge_feats),
+                            (self.node_feats._version, self.edge_feats._version))
+
+    def _layout_types_ok(self) -> bool:
+        lay = getattr(self, "_nt_layout", None)
+        return lay is not None and lay.type_range is not None and _same_types(lay, self.node_feats, self.edge_feats)
+
+    def _move_layout(self, device, types_ok: bool = False):
         lay = getattr(self, "_nt_layout", None)
         if lay is not None and device is not None:
-            self._nt_layout = lay.to(device, self.edge_index, getattr(self, "batch_node_index", None))
+            moved = lay.to(device, self.edge_index, getattr(self, "batch_node_index", None))
+            if types_ok:  # the statistics described the tensors just moved: re-bind them
+                moved.type_src = (weakref.ref(self.node_feats), weakref.ref(self.edge_feats),
+                                  (self.node_feats._version, self.edge_feats._version))
+            else:
+                moved.type_range = None
+            self._nt_layout = moved
 
     @property
     def A(self) -> Tensor:
@@ -162,6 +211,7 @@ class BatchedGraph(Graph):
         return self._size
 
     def to(self, device):
+        types_ok = self._layout_types_ok()
         self._device = device
         self.node_feats = self.node_feats.to(device)
         self.edge_feats = self.edge_feats.to(device)
@@ -169,7 +219,7 @@ class BatchedGraph(Graph):
         self.rev_index = self.rev_index.to(device)
         self.batch_node_index = self.batch_node_index.to(device)
         self.batch_edge_index = self.batch_edge_index.to(device)
-        self._move_layout(device)
+        self._move_layout(device, types_ok)
         return self
 
     @classmethod
@@ -221,7 +271,8 @@ class BatchedGraph(Graph):
             batch_edge_index=batch_edge_index,
             size=B,
         )
-        BG._nt_layout = host_layout(edge_index, rev_index, len(node_feats), batch_node_index, B)
+        BG._nt_layout = host_layout(edge_index, rev_index, len(node_feats), batch_node_index, B,
+                                    node_feats, edge_feats)
         if Gs[-1].device is not None:  # reference passes device_=G.device of the last graph
             BG.to(Gs[-1].device)
         return BG
@@ -287,6 +338,7 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
     # (reference quirk): leave such batches to the device-side check
     lay.validated = E == 0 or int(rev_index.max()) < E
     lay.mol_ptr, lay.mol_perm, lay.batch_node_index = mol_ptr, None, bni
+    host_stats(lay, dst_ptr.numpy(), E, mol_ptr.numpy(), node_out, edge_out)
     BG._nt_layout = lay
     if Gs[-1].device is not None:  # reference passes device_=G.device of the last graph
         BG.to(Gs[-1].device)
@@ -299,6 +351,8 @@ def host_layout(
     num_nodes: int,
     batch_node_index: Optional[Tensor] = None,
     num_graphs: Optional[int] = None,
+    node_feats: Optional[Tensor] = None,
+    edge_feats: Optional[Tensor] = None,
 ) -> DeviceLayout:
     """Build the CSR layout on the host (numpy stable argsort == ascending edge id per node)."""
     ei = edge_index.detach().cpu().numpy()
@@ -338,4 +392,89 @@ def host_layout(
             lay.mol_ptr = torch.from_numpy(mol_ptr)
             lay.mol_perm = None if sorted_ else torch.from_numpy(np.argsort(b, kind="stable").astype(np.int32))
             lay.batch_node_index = batch_node_index
+    host_stats(lay, dst_ptr, E, None if lay.mol_ptr is None else lay.mol_ptr.numpy(), node_feats, edge_feats)
     return lay
+
+
+# ---- host-side plans (numpy restatements of the device planners; same arrays, no device sync) ----
+MAX_FUSED_IN_DEGREE = 32  # nt_dmpnn_tile_plan's limit (larger in-degrees take the unfused path)
+LONG_SEGMENT = 64  # segments longer than this aggregate through the chunked reduce
+CHUNK_ROWS = 32  # rows per chunk of nt_segment_reduce_chunked
+
+
+def host_tile_plan(dst_ptr: np.ndarray, E: int, max_in_degree: int):
+    """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) exactly as nt_dmpnn_tile_plan builds them:
+    tile k starts at dst_ptr[first v with dst_ptr[v] >= k L], L = 65 - max(max_in_degree, 1)."""
+    L = 65 - max(int(max_in_degree), 1)
+    ntiles = (E + L - 1) // L if E > 0 else 0
+    tile_ptr = np.empty(ntiles + 1, dtype=np.int32)
+    if ntiles:
+        v = np.searchsorted(dst_ptr, np.arange(ntiles, dtype=np.int64) * L, side="left")
+        tile_ptr[:ntiles] = dst_ptr[v]
+    tile_ptr[ntiles] = E
+    counts = np.diff(dst_ptr.astype(np.int64))
+    dsts = np.repeat(np.arange(len(counts), dtype=np.int32), counts)
+    return torch.from_numpy(tile_ptr), ntiles, torch.from_numpy(dsts)
+
+
+def host_chunk_plan(seg_ptr: np.ndarray, chunk: int = CHUNK_ROWS):
+    """(chunk_pos[nchunks+1], nchunks, chunk_ptr[nseg+1]) exactly as kernels.chunk_plan builds them."""
+    sp = seg_ptr.astype(np.int64)
+    n = sp[1:] - sp[:-1]
+    nch = (n + chunk - 1) // chunk
+    chunk_ptr = np.zeros(len(n) + 1, dtype=np.int64)
+    np.cumsum(nch, out=chunk_ptr[1:])
+    nchunks = int(chunk_ptr[-1])
+    seg_of = np.repeat(np.arange(len(n)), nch)
+    k_in_seg = np.arange(nchunks) - chunk_ptr[seg_of]
+    chunk_pos = np.empty(nchunks + 1, dtype=np.int32)
+    chunk_pos[:nchunks] = sp[seg_of] + k_in_seg * chunk
+    chunk_pos[nchunks] = seg_ptr[-1]
+    return torch.from_numpy(chunk_pos), nchunks, torch.from_numpy(chunk_ptr.astype(np.int32))
+
+
+def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional[np.ndarray],
+               node_feats: Optional[Tensor] = None, edge_feats: Optional[Tensor] = None) -> None:
+    """Fill the layout's host statistics and plans from the host CSR (one O(V + E) pass)."""
+    deg = np.diff(dst_ptr.astype(np.int64))
+    lay.deg_range = (int(deg.max()), int(deg.min())) if deg.size else (0, 0)
+    V = len(deg)
+    maxdeg, mindeg = lay.deg_range
+    if E > 0 and V > 0 and maxdeg <= MAX_FUSED_IN_DEGREE:
+        tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg)
+        lay.plan = (tile_ptr, ntiles, dsts, mindeg == 0)
+    elif E > 0 and V > 0:
+        lay.plan = False
+    lay.dst_chunks = host_chunk_plan(dst_ptr) if maxdeg > LONG_SEGMENT else False
+    if mol_ptr is not None:
+        n = np.diff(mol_ptr.astype(np.int64))
+        lay.mol_max = int(n.max()) if n.size else 0
+        if lay.mol_ptr is not None:
+            lay.mol_chunks = (lay.mol_ptr, host_chunk_plan(mol_ptr) if lay.mol_max > LONG_SEGMENT else False)
+    if node_feats is not None and edge_feats is not None:
+        lay.type_src = (weakref.ref(node_feats), weakref.ref(edge_feats), (node_feats._version, edge_feats._version))
+    tr = []
+    for X in (node_feats, edge_feats):
+        if X is not None and X.dim() == 2 and X.dtype == torch.int64 and X.device.type == "cpu":
+            tr.append((int(X.min()), int(X.max())) if X.numel() else (0, -1))
+        else:
+            tr.append(None)
+    lay.type_range = tuple(tr)
+
+
+def _same_types(lay: DeviceLayout, node_feats: Tensor, edge_feats: Tensor) -> bool:
+    """Whether lay.type_range describes exactly these feature tensors (same objects, unmodified)."""
+    src = lay.type_src
+    if not isinstance(src, tuple):
+        return False
+    return src[0]() is node_feats and src[1]() is edge_feats and src[2] == (node_feats._version, edge_feats._version)
+
+
+def types_in_range(lay: Optional[DeviceLayout], node_types: Tensor, edge_types: Tensor, num_node_types: int,
+                   num_edge_types: int) -> Optional[bool]:
+    """Host answer to "are all type indices inside the tables?" from the collate's statistics:
+    True / False, or None when the layout carries no statistics for these tensors."""
+    if lay is None or lay.type_range is None or not _same_types(lay, node_types, edge_types):
+        return None
+    (n0, n1), (e0, e1) = lay.type_range
+    return n0 >= 0 and n1 < num_node_types and e0 >= 0 and e1 < num_edge_types

@@ -197,8 +197,71 @@ class SynthMolBatch:
             batch_edge_index=bei,
             size=B,
         )
-        BG._nt_layout = host_layout(edge_index, rev_index, self.num_nodes, bni, B)
+        BG._nt_layout = host_layout(edge_index, rev_index, self.num_nodes, bni, B, BG.node_feats,
+                                    BG.edge_feats)
         return BG
+
+
+def _types(rng: np.random.Generator, V: int, Nb: int) -> tuple[np.ndarray, np.ndarray]:
+    a_off = np.cumsum((0,) + ATOM_TYPE_SIZES[:-1])
+    b_off = np.cumsum((0,) + BOND_TYPE_SIZES[:-1])
+    atom_types = np.stack(
+        [o + rng.integers(s, size=V) for o, s in zip(a_off, ATOM_TYPE_SIZES)], axis=1
+    ).astype(np.int64)
+    bond_types = np.stack(
+        [o + rng.integers(s, size=Nb) for o, s in zip(b_off, BOND_TYPE_SIZES)], axis=1
+    ).astype(np.int64).reshape(Nb, 2)
+    return atom_types, bond_types
+
+
+def make_qm9_batch_vectorized(num_mols: int, seed: int = 0, ring_tries: int = 30) -> SynthMolBatch:
+    """The QM9 generator of ``make_batch("qm9", ...)`` vectorised over molecules (same
+    distribution, a different random stream), for million-molecule batches (BASELINE config 4):
+    every step draws for all molecules at once.
+
+    * n_atoms in {9, 8, 7} w.p. {.90, .08, .02};
+    * spanning tree: atom i (1 <= i < n) bonds to a uniformly drawn earlier atom of degree < 4;
+    * ring closures: k in {0,1,2,3} w.p. {.15, .30, .35, .20}; up to ``ring_tries`` draws of a
+      random atom pair, accepted while fewer than k were added, u != v, both degrees < 4 and the
+      pair not bonded yet.
+    Bonds of a molecule are listed tree bonds first (in atom order), then ring closures."""
+    rng = np.random.default_rng(seed)
+    B = int(num_mols)
+    N = 9
+    n = rng.choice(np.array([9, 8, 7]), size=B, p=[0.90, 0.08, 0.02]).astype(np.int64)
+    deg = np.zeros((B, N), dtype=np.int64)
+    adj = np.zeros((B, N, N), dtype=bool)
+    rows = np.arange(B)
+    cand_u = np.zeros((B, N - 1 + ring_tries), dtype=np.int64)
+    cand_v = np.zeros((B, N - 1 + ring_tries), dtype=np.int64)
+    keep = np.zeros((B, N - 1 + ring_tries), dtype=bool)
+    for i in range(1, N):
+        active = i < n
+        scores = rng.random((B, i))
+        scores[deg[:, :i] >= 4] = -1.0
+        j = scores.argmax(1)
+        cand_u[:, i - 1], cand_v[:, i - 1], keep[:, i - 1] = j, i, active
+        a = rows[active]
+        deg[a, j[active]] += 1
+        deg[a, i] += 1
+        adj[a, j[active], i] = adj[a, i, j[active]] = True
+    k = rng.choice(np.array([0, 1, 2, 3]), size=B, p=[0.15, 0.30, 0.35, 0.20])
+    added = np.zeros(B, dtype=np.int64)
+    for t in range(ring_tries):
+        u = rng.integers(0, n)
+        v = rng.integers(0, n)
+        ok = (added < k) & (u != v) & (deg[rows, u] < 4) & (deg[rows, v] < 4) & ~adj[rows, u, v]
+        c = N - 1 + t
+        cand_u[:, c], cand_v[:, c], keep[:, c] = u, v, ok
+        a = rows[ok]
+        deg[a, u[ok]] += 1
+        deg[a, v[ok]] += 1
+        adj[a, u[ok], v[ok]] = adj[a, v[ok], u[ok]] = True
+        added += ok
+    n_bonds = keep.sum(1).astype(np.int64)
+    bonds = np.stack([cand_u[keep], cand_v[keep]], axis=1).astype(np.int64)
+    atom_types, bond_types = _types(rng, int(n.sum()), len(bonds))
+    return SynthMolBatch(n, n_bonds, bonds, atom_types, bond_types)
 
 
 def make_batch(kind: Kind, num_mols: int, seed: int = 0) -> SynthMolBatch:
@@ -213,13 +276,5 @@ def make_batch(kind: Kind, num_mols: int, seed: int = 0) -> SynthMolBatch:
     n_atoms = np.asarray(n_atoms, dtype=np.int64)
     n_bonds = np.asarray(n_bonds, dtype=np.int64)
     bonds_arr = np.asarray(bonds, dtype=np.int64).reshape(-1, 2)
-    V, Nb = int(n_atoms.sum()), len(bonds_arr)
-    a_off = np.cumsum((0,) + ATOM_TYPE_SIZES[:-1])
-    b_off = np.cumsum((0,) + BOND_TYPE_SIZES[:-1])
-    atom_types = np.stack(
-        [o + rng.integers(s, size=V) for o, s in zip(a_off, ATOM_TYPE_SIZES)], axis=1
-    ).astype(np.int64)
-    bond_types = np.stack(
-        [o + rng.integers(s, size=Nb) for o, s in zip(b_off, BOND_TYPE_SIZES)], axis=1
-    ).astype(np.int64).reshape(Nb, 2)
+    atom_types, bond_types = _types(rng, int(n_atoms.sum()), len(bonds_arr))
     return SynthMolBatch(n_atoms, n_bonds, bonds_arr, atom_types, bond_types)

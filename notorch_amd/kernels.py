@@ -43,6 +43,16 @@ def _stream(device: torch.device) -> int:
     return torch.cuda.current_stream(device).cuda_stream
 
 
+def _run(dev: torch.device, fn, *args) -> None:
+    """Call a C-ABI entry point with ``dev`` as the current HIP device (the library queries the
+    current device for its CU count and kernel attributes; the launch goes to dev's stream)."""
+    if dev.index is not None and dev.index != torch.cuda.current_device():
+        with torch.cuda.device(dev):
+            check(fn(*args))
+    else:
+        check(fn(*args))
+
+
 def _require_device(*ts: Tensor | None) -> torch.device:
     dev = None
     for t in ts:
@@ -143,11 +153,8 @@ def csr_build(idx: Tensor, nseg: int, *, check_bounds: bool = True) -> tuple[Ten
     ws_bytes = lib.nt_csr_workspace_bytes(n, nseg)
     ws = torch.empty(ws_bytes, dtype=torch.uint8, device=dev)
     err = torch.zeros(1, dtype=torch.int32, device=dev)
-    check(
-        lib.nt_csr_build(
-            _ptr(idx), n, nseg, _ptr(seg_ptr), _ptr(perm), _ptr(ws), ws_bytes, _ptr(err), _stream(dev)
-        )
-    )
+    _run(dev, lib.nt_csr_build,
+         _ptr(idx), n, nseg, _ptr(seg_ptr), _ptr(perm), _ptr(ws), ws_bytes, _ptr(err), _stream(dev))
     if check_bounds and n > 0 and int(err.item()) != 0:
         raise IndexError(f"index out of range for a scatter into {nseg} rows")
     return seg_ptr, perm
@@ -181,12 +188,9 @@ def dmpnn_init(
     if seg_ptr is not None:
         S = torch.empty(V, h, dtype=Xv.dtype, device=dev)
     lib = _lib.load()
-    check(
-        lib.nt_dmpnn_init(
-            _ptr(Xv), _ptr(Xe), _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h, act[0], act[1],
-            reduce_code(reduce), code, _ptr(H0), _ptr(S), _stream(dev),
-        )
-    )
+    _run(dev, lib.nt_dmpnn_init,
+         _ptr(Xv), _ptr(Xe), _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h, act[0], act[1],
+         reduce_code(reduce), code, _ptr(H0), _ptr(S), _stream(dev))
     return H0, S
 
 
@@ -213,12 +217,9 @@ def segment_reduce(
     if out is None:
         out = torch.empty(nseg, h, dtype=X.dtype, device=dev)
     lib = _lib.load()
-    check(
-        lib.nt_segment_reduce(
-            _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce), act[0], act[1], code,
-            _ptr(out), _stream(dev),
-        )
-    )
+    _run(dev, lib.nt_segment_reduce,
+         _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce), act[0], act[1], code,
+         _ptr(out), _stream(dev))
     return out
 
 
@@ -267,10 +268,9 @@ def segment_reduce_chunked(
     else:
         _require_feat("out", out, X.dtype)
     partial = torch.empty(max(nchunks, 1), h, dtype=torch.float32, device=dev)
-    check(_lib.load().nt_segment_reduce_chunked(
-        _ptr(X), _ptr(perm), _ptr(chunk_pos), nchunks, _ptr(chunk_ptr), _ptr(seg_ptr), nseg, h,
-        reduce_code(reduce), act[0], act[1], code, _ptr(partial), _ptr(out), _stream(dev),
-    ))
+    _run(dev, _lib.load().nt_segment_reduce_chunked,
+         _ptr(X), _ptr(perm), _ptr(chunk_pos), nchunks, _ptr(chunk_ptr), _ptr(seg_ptr), nseg, h,
+         reduce_code(reduce), act[0], act[1], code, _ptr(partial), _ptr(out), _stream(dev))
     return out
 
 
@@ -294,7 +294,7 @@ def pack_weights(W: Tensor) -> Tensor:
         raise ValueError(f"ChempropLayer weight must be square, got {tuple(W.shape)}")
     Wp = torch.empty(L, packed_weight_numel(h, W.dtype), dtype=torch.float32, device=dev)
     lib = _lib.load()
-    check(lib.nt_dmpnn_pack_weight(_ptr(W3), L, h, code, _ptr(Wp), _stream(dev)))
+    _run(dev, lib.nt_dmpnn_pack_weight, _ptr(W3), L, h, code, _ptr(Wp), _stream(dev))
     return Wp[0] if W.dim() == 2 else Wp
 
 
@@ -331,12 +331,9 @@ def dmpnn_update(
     else:
         _require_feat("out", out, H.dtype)
     lib = _lib.load()
-    check(
-        lib.nt_dmpnn_update(
-            _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
-            act[0], act[1], code, _ptr(out), _stream(dev),
-        )
-    )
+    _run(dev, lib.nt_dmpnn_update,
+         _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
+         act[0], act[1], code, _ptr(out), _stream(dev))
     return out
 
 
@@ -359,11 +356,8 @@ def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int) -> tuple[Tensor, int,
     ntiles = int(lib.nt_dmpnn_tile_count(E, max_in_degree))
     tile_ptr = torch.empty(ntiles + 1, dtype=torch.int32, device=dev)
     dsts = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
-    check(
-        lib.nt_dmpnn_tile_plan(
-            _ptr(dst_ptr), V, E, max_in_degree, _ptr(tile_ptr), ntiles, _ptr(dsts), _stream(dev)
-        )
-    )
+    _run(dev, lib.nt_dmpnn_tile_plan,
+         _ptr(dst_ptr), V, E, max_in_degree, _ptr(tile_ptr), ntiles, _ptr(dsts), _stream(dev))
     return tile_ptr, ntiles, dsts
 
 
@@ -420,13 +414,10 @@ def dmpnn_update_fused(
         perm = None
         S_out = None
     lib = _lib.load()
-    check(
-        lib.nt_dmpnn_update_fused(
-            _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
-            act[0], act[1], _ptr(tile_ptr), ntiles, _ptr(perm), _ptr(dsts), reduce_code(reduce),
-            agg_act[0], agg_act[1], code, _ptr(out), _ptr(S_out), _stream(dev),
-        )
-    )
+    _run(dev, lib.nt_dmpnn_update_fused,
+         _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
+         act[0], act[1], _ptr(tile_ptr), ntiles, _ptr(perm), _ptr(dsts), reduce_code(reduce),
+         agg_act[0], agg_act[1], code, _ptr(out), _ptr(S_out), _stream(dev))
     return out, S_out
 
 
@@ -447,9 +438,8 @@ def dmpnn_message(H: Tensor, S: Tensor, src: Tensor, rev: Tensor, *,
         out = torch.empty_like(H)
     else:
         _require_feat("out", out, H.dtype)
-    check(_lib.load().nt_dmpnn_message(
-        _ptr(H), _ptr(S), _ptr(src), _ptr(rev), V, E, h, act[0], act[1], code, _ptr(out), _stream(dev)
-    ))
+    _run(dev, _lib.load().nt_dmpnn_message,
+         _ptr(H), _ptr(S), _ptr(src), _ptr(rev), V, E, h, act[0], act[1], code, _ptr(out), _stream(dev))
     return out
 
 
@@ -477,11 +467,10 @@ def dmpnn_edge_backward(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor, dst
         out = torch.empty_like(H)
     else:
         _require_feat("out", out, H.dtype)
-    check(_lib.load().nt_dmpnn_edge_backward(
-        _ptr(G if residual else None), _ptr(H), _ptr(dA), _ptr(dS), _ptr(dst), _ptr(rev_ptr),
-        _ptr(rev_perm), _ptr(dst_ptr), V, E, h, int(residual), act[0], act[1], reduce_code(reduce),
-        code, _ptr(out), _stream(dev),
-    ))
+    _run(dev, _lib.load().nt_dmpnn_edge_backward,
+         _ptr(G if residual else None), _ptr(H), _ptr(dA), _ptr(dS), _ptr(dst), _ptr(rev_ptr),
+         _ptr(rev_perm), _ptr(dst_ptr), V, E, h, int(residual), act[0], act[1], reduce_code(reduce),
+         code, _ptr(out), _stream(dev))
     return out
 
 
@@ -504,9 +493,8 @@ def gather_rows(X: Tensor, idx: Tensor, *, base: Tensor | None = None, seg_ptr: 
         out = torch.empty(n, h, dtype=X.dtype, device=dev)
     else:
         _require_feat("out", out, X.dtype)
-    check(_lib.load().nt_gather_rows(
-        _ptr(base), _ptr(X), _ptr(idx), _ptr(seg_ptr), n, nseg, h, code, _ptr(out), _stream(dev)
-    ))
+    _run(dev, _lib.load().nt_gather_rows,
+         _ptr(base), _ptr(X), _ptr(idx), _ptr(seg_ptr), n, nseg, h, code, _ptr(out), _stream(dev))
     return out
 
 
@@ -533,7 +521,8 @@ def embed_bag(table: Tensor, idx: Tensor, *, validate: bool = True, out: Tensor 
     n, k = idx.shape
     if out is None:
         out = torch.empty(n, h, dtype=table.dtype, device=dev)
-    check(_lib.load().nt_embed_bag(_ptr(table), ntypes, _ptr(idx), n, k, h, code, _ptr(out), _stream(dev)))
+    _run(dev, _lib.load().nt_embed_bag,
+         _ptr(table), ntypes, _ptr(idx), n, k, h, code, _ptr(out), _stream(dev))
     return out
 
 
@@ -568,11 +557,10 @@ def dmpnn_init_embed(
         raise ValueError("src must have one entry per edge")
     H0 = torch.empty(E, h, dtype=node_table.dtype, device=dev)
     S = None if seg_ptr is None else torch.empty(V, h, dtype=node_table.dtype, device=dev)
-    check(_lib.load().nt_dmpnn_init_embed(
-        _ptr(node_table), node_table.shape[0], _ptr(node_types), kv, _ptr(edge_table),
-        edge_table.shape[0], _ptr(edge_types), ke, _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h,
-        act[0], act[1], reduce_code(reduce), code, _ptr(H0), _ptr(S), _stream(dev),
-    ))
+    _run(dev, _lib.load().nt_dmpnn_init_embed,
+         _ptr(node_table), node_table.shape[0], _ptr(node_types), kv, _ptr(edge_table),
+         edge_table.shape[0], _ptr(edge_types), ke, _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h,
+         act[0], act[1], reduce_code(reduce), code, _ptr(H0), _ptr(S), _stream(dev))
     return H0, S
 
 
@@ -601,10 +589,9 @@ def node_scores(X: Tensor, *, a: Tensor | None = None, a_bias: Tensor | None = N
             raise ValueError("SDPAttention scores need batch_node_index")
         _require_i64("batch_node_index", node_seg)
     s = torch.empty(n, dtype=torch.float32, device=dev)
-    check(_lib.load().nt_node_scores(
-        _ptr(X), n, h, _ptr(a), _ptr(a_bias), _ptr(Q), _ptr(node_seg), float(sqrt_key), code,
-        _ptr(s), _stream(dev),
-    ))
+    _run(dev, _lib.load().nt_node_scores,
+         _ptr(X), n, h, _ptr(a), _ptr(a_bias), _ptr(Q), _ptr(node_seg), float(sqrt_key), code,
+         _ptr(s), _stream(dev))
     return s
 
 
@@ -618,9 +605,8 @@ def softmax_pool(X: Tensor, scores: Tensor, seg_ptr: Tensor, perm: Tensor | None
         raise ValueError("seg_ptr must be int32 of length nseg + 1")
     h = X.shape[1]
     out = torch.empty(nseg, h, dtype=X.dtype, device=dev)
-    check(_lib.load().nt_softmax_pool(
-        _ptr(X), _ptr(scores), _ptr(seg_ptr), _ptr(perm), nseg, h, code, _ptr(out), _stream(dev)
-    ))
+    _run(dev, _lib.load().nt_softmax_pool,
+         _ptr(X), _ptr(scores), _ptr(seg_ptr), _ptr(perm), nseg, h, code, _ptr(out), _stream(dev))
     return out
 
 
@@ -644,8 +630,7 @@ def dropout_residual(Y: Tensor, p: float, seed: int, offset: int = 0, *, base: T
         _require_feat("out", out, Y.dtype)
         if out.shape != Y.shape or not out.is_contiguous():
             raise ValueError("out must be a contiguous tensor shaped like Y")
-    check(_lib.load().nt_dropout_residual(
-        _ptr(base), _ptr(Y), Y.numel(), float(p), int(seed) & (2**64 - 1), int(offset), code, _ptr(out),
-        _stream(dev),
-    ))
+    _run(dev, _lib.load().nt_dropout_residual,
+         _ptr(base), _ptr(Y), Y.numel(), float(p), int(seed) & (2**64 - 1), int(offset), code, _ptr(out),
+         _stream(dev))
     return out

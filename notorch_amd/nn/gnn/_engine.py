@@ -45,6 +45,30 @@ _IDENTITY = (NT_ACT_IDENTITY, 0.0)
 # Optional per-launch timer for the dominant kernel (bench.py sets it): a list that receives
 # (start, end) torch.cuda.Event pairs recorded on the launch stream around every nt_dmpnn_update.
 UPDATE_EVENTS: Optional[list] = None
+# What the last layer-update launch ran (bench.py's roofline): kernel, numerics, padded MFMA shape.
+LAST_UPDATE_INFO: dict = {}
+
+
+def _note_update(kind: str, dtype: torch.dtype, h: int) -> None:
+    kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
+    if dtype == torch.bfloat16:
+        info = dict(kernel="update_bf16_kernel (64-edge tiles, bf16 16x16x32 MFMA, fp32 accumulate)",
+                    kernel_short="update_bf16", numerics="bf16 storage, bf16 MFMA, fp32 accumulate",
+                    products=1)
+    elif kind == "fused":
+        info = dict(kernel="update_pk_kernel (persistent producer/consumer, bf16x6 16x16x32 MFMA, "
+                           "aggregation of the next layer fused)", kernel_short="update_pk",
+                    numerics="fp32 via bf16x6 split (6 bf16 MFMA products, fp32 accumulate)", products=6)
+    elif kind == "persistent":
+        info = dict(kernel="update_pk_kernel without tile plan (hub graph: aggregation by the chunked "
+                           "segment reduce)", kernel_short="update_pk",
+                    numerics="fp32 via bf16x6 split (6 bf16 MFMA products, fp32 accumulate)", products=6)
+    else:
+        info = dict(kernel="nt_dmpnn_update (unfused fp32 update kernel)", kernel_short="update",
+                    numerics="fp32 via bf16x6 split", products=6)
+    info.update(fused=kind == "fused", kpad=kp, npad=np_)
+    LAST_UPDATE_INFO.clear()
+    LAST_UPDATE_INFO.update(info)
 
 
 # ------------------------------------------------------------------------------------ layouts
@@ -282,6 +306,7 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
     persistent = (drop is None and _fused_enabled() and H.dtype == torch.float32
                   and K.fused_supported(V, E, h, H.dtype))
     timer = UPDATE_EVENTS
+    _note_update("persistent" if persistent else "unfused", H.dtype, h)
     for l in range(d):
         if keep_states:
             states.append((H, S))
@@ -318,6 +343,7 @@ def _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual
     spare_H: Optional[Tensor] = None
     spare_S: Optional[Tensor] = None
     timer = UPDATE_EVENTS
+    _note_update("fused", H.dtype, H.shape[1])
     for l in range(d):
         last = l == d - 1
         if keep_states:

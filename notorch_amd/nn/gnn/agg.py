@@ -84,7 +84,9 @@ def _softmax_pool_torch(X: Tensor, scores: Tensor, bni: Tensor, B: int) -> Tenso
 
 
 class _AttentionReadout(Aggregation):
-    def _pool(self, G, scores_fn, torch_scores_fn) -> Tensor:
+    def _pool(self, G, scores_fn, torch_scores_fn, extra=()) -> Tensor:
+        """``extra``: tensors the scores depend on besides X and the module's parameters (the
+        SDPAttention query Q, passed by keyword): their requires_grad selects the autograd path too."""
         X = G.node_feats
         if X.device.type != "cuda":
             raise RuntimeError(
@@ -93,7 +95,8 @@ class _AttentionReadout(Aggregation):
         X = X.contiguous()
         B = len(G)
         needs_grad = torch.is_grad_enabled() and (
-            X.requires_grad or any(p.requires_grad for p in self.parameters()))
+            X.requires_grad or any(p.requires_grad for p in self.parameters())
+            or any(t.requires_grad for t in extra))
         if needs_grad:
             return _softmax_pool_torch(X, torch_scores_fn(X), G.batch_node_index, B)
         mol_ptr, mol_perm = _engine.mol_layout(G)
@@ -131,4 +134,5 @@ class SDPAttention(_AttentionReadout):
             lambda X: K.node_scores(X, Q=Q.contiguous(), node_seg=bni.contiguous(),
                                     sqrt_key=self.sqrt_key_dim),
             lambda X: (torch.einsum("vd,vd->v", Q[bni], X) / self.sqrt_key_dim).float(),
+            extra=(Q,),
         )

@@ -24,6 +24,7 @@ import torch.nn as nn
 
 from notorch_amd import kernels as K
 from notorch_amd._lib import NT_ACT_IDENTITY
+from notorch_amd.data.models.graph import types_in_range
 from notorch_amd.data.synth import DEFAULT_NUM_ATOM_TYPES, DEFAULT_NUM_BOND_TYPES
 from notorch_amd.nn.gnn import _engine
 from notorch_amd.nn.gnn.chemprop import ChempropBlock
@@ -57,8 +58,13 @@ class GraphEmbedding(nn.Module):
 
     def forward(self, G):
         if self._use_kernel(G):
-            Xv = K.embed_bag(self.node.weight.detach(), G.node_feats.contiguous())
-            Xe = K.embed_bag(self.edge.weight.detach(), G.edge_feats.contiguous())
+            nt_, et_ = G.node_feats.contiguous(), G.edge_feats.contiguous()
+            ok = types_in_range(getattr(G, "_nt_layout", None), nt_, et_, self.num_node_types,
+                                self.num_edge_types)
+            if ok is False:
+                raise IndexError("type index out of range for the embedding tables")
+            Xv = K.embed_bag(self.node.weight.detach(), nt_, validate=ok is None)
+            Xe = K.embed_bag(self.edge.weight.detach(), et_, validate=ok is None)
             return G.update(node_feats=Xv, edge_feats=Xe)
         return G.update(node_feats=self.node(G.node_feats), edge_feats=self.edge(G.edge_feats))
 
@@ -105,10 +111,16 @@ class EmbeddedChempropBlock(nn.Module):
         lay = _engine.dst_layout(G)
         node_types, edge_types = G.node_feats.contiguous(), G.edge_feats.contiguous()
         seen = getattr(lay, "embed_checked", None)
+        # the check is against these table sizes: a smaller table must re-validate the indices
+        key = (node_types._version, edge_types._version, emb.node.num_embeddings, emb.edge.num_embeddings)
         validate = not (
-            seen is not None and seen[0]() is node_types and seen[1]() is edge_types
-            and seen[2] == (node_types._version, edge_types._version)
+            seen is not None and seen[0]() is node_types and seen[1]() is edge_types and seen[2] == key
         )
+        if validate:  # the collate's host statistics answer without a device -> host sync
+            ok = types_in_range(lay, node_types, edge_types, emb.node.num_embeddings, emb.edge.num_embeddings)
+            if ok is False:
+                raise IndexError("type index out of range for the embedding tables")
+            validate = ok is None
         node, H = _engine.block_forward_embedded(
             emb.node.weight.detach(), node_types, emb.edge.weight.detach(), edge_types,
             G.edge_index[0].contiguous(), G.rev_index.contiguous(), lay,
@@ -116,6 +128,5 @@ class EmbeddedChempropBlock(nn.Module):
             residual, validate=validate,
         )
         # type indices validated for these tensors: no host sync on the next call
-        lay.embed_checked = (weakref.ref(node_types), weakref.ref(edge_types),
-                             (node_types._version, edge_types._version))
+        lay.embed_checked = (weakref.ref(node_types), weakref.ref(edge_types), key)
         return G.update(node_feats=node, edge_feats=H)

@@ -72,6 +72,11 @@ def test_collate_is_picklable():
     G = make_batch("qm9", 4, seed=5).collate("nodes")
     G2 = pickle.loads(pickle.dumps(G))
     assert torch.equal(G2.edge_index, G.edge_index) and len(G2) == 4
+    from notorch_amd.data.models.graph import types_in_range
+
+    # the shipped statistics still describe the unpickled features (DataLoader workers)
+    assert types_in_range(G2._nt_layout, G2.node_feats, G2.edge_feats, 42, 13) is True
+    assert G2._nt_layout.plan[1] == G._nt_layout.plan[1]
 
 
 def test_native_collate_matches_device_path_and_layout():
@@ -105,3 +110,39 @@ def test_native_collate_float_features_and_errors():
     mixed = [Gs[0], Graph(Gs[1].node_feats.float(), Gs[1].edge_feats, Gs[1].edge_index, Gs[1].rev_index)]
     with pytest.raises(RuntimeError, match="differ"):
         BatchedGraph.from_graphs(mixed)
+
+
+def test_host_plans_ship_with_the_collate():
+    """The collate ships the statistics and plans a fresh batch needs (no device -> host sync):
+    in-degree range, tile plan (tiles cut at node boundaries, <= 64 rows, every node's in-edges in
+    one tile), chunk plans for hubs, molecule size, type-index ranges."""
+    import numpy as np
+
+    from notorch_amd.data.models.graph import BatchedGraph, types_in_range
+    from notorch_amd.data.synth import make_batch
+
+    b = make_batch("qm9", 300, seed=4)
+    for G in (b.collate("nodes"), BatchedGraph.from_graphs(b.to_graphs(), rev_offset="edges")):
+        lay = G._nt_layout
+        dst_ptr = lay.dst_ptr.numpy().astype(np.int64)
+        deg = np.diff(dst_ptr)
+        assert lay.deg_range == (deg.max(), deg.min())
+        tile_ptr, ntiles, dsts, zero_fill = lay.plan
+        tp = tile_ptr.numpy()
+        assert tp[0] == 0 and tp[-1] == G.num_edges and len(tp) == ntiles + 1
+        assert (np.diff(tp) <= 64).all() and (np.diff(tp) >= 0).all()
+        assert np.isin(tp, dst_ptr).all()  # cuts only at node boundaries
+        assert (dsts.numpy() == np.repeat(np.arange(G.num_nodes), deg)).all()
+        assert zero_fill == (deg.min() == 0)
+        assert lay.dst_chunks is False
+        assert lay.mol_max == int(np.bincount(G.batch_node_index.numpy()).max())
+        assert types_in_range(lay, G.node_feats, G.edge_feats, 42, 13) is True
+        assert types_in_range(lay, G.node_feats, G.edge_feats, 41, 13) is False
+        G.node_feats[0, 0] = 5  # in-place edit: the statistics no longer describe the tensor
+        assert types_in_range(lay, G.node_feats, G.edge_feats, 42, 13) is None
+    P = make_batch("polymer", 2, seed=1).collate("nodes")
+    lay = P._nt_layout
+    assert lay.plan is False and lay.deg_range[0] > 32
+    chunk_pos, nchunks, chunk_ptr = lay.dst_chunks
+    assert chunk_pos.numel() == nchunks + 1 and int(chunk_ptr[-1]) == nchunks
+    assert (np.diff(chunk_pos.numpy()) <= 32).all()

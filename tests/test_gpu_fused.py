@@ -219,6 +219,8 @@ def test_fused_kernel_variants_and_no_spin_timeouts(variant, monkeypatch):
     from notorch_amd import _lib
 
     K = _K()
+    if variant == "ps" and not _lib.DIAG:
+        pytest.skip("the ps kernel is an A/B variant: diagnostic library only (NT_LIB=diag)")
     monkeypatch.setenv("NT_FUSED_KERNEL", variant)
     lib = _lib.load()
     fn = lib.nt_debug_pk_timeouts
@@ -246,3 +248,44 @@ def test_fused_kernel_variants_and_no_spin_timeouts(variant, monkeypatch):
     torch.cuda.synchronize()
     assert fn(ctypes.byref(cnt), 1) == 0
     assert cnt.value == 0, "a pk ring spin gave up"
+
+
+def test_host_plans_equal_device_planners():
+    """The collate's host tile / chunk plans are the arrays nt_dmpnn_tile_plan and
+    kernels.chunk_plan build on the device (the engine uses them without a sync)."""
+    from notorch_amd.data.synth import make_batch
+
+    K = _K()
+    for kind, n in (("qm9", 500), ("zinc", 64)):
+        G = make_batch(kind, n, seed=3).collate("nodes")
+        lay = G._nt_layout
+        tile_ptr, ntiles, dsts, _ = lay.plan
+        d_tile_ptr, d_ntiles, d_dsts = K.tile_plan(lay.dst_ptr.to(DEV), G.num_edges, lay.deg_range[0])
+        assert d_ntiles == ntiles
+        assert torch.equal(d_tile_ptr.cpu(), tile_ptr) and torch.equal(d_dsts.cpu(), dsts)
+    P = make_batch("polymer", 2, seed=2).collate("nodes")
+    lay = P._nt_layout
+    for host, seg_ptr in ((lay.dst_chunks, lay.dst_ptr), (lay.mol_chunks[1], lay.mol_ptr)):
+        dev = K.chunk_plan(seg_ptr.to(DEV))
+        assert dev[1] == host[1]
+        assert torch.equal(dev[0].cpu(), host[0]) and torch.equal(dev[2].cpu(), host[2])
+
+
+def test_forward_on_a_non_current_device():
+    """Every launch runs under a device guard (kernels._run): a block on cuda:1 while cuda:0 is
+    current gives the same result as on cuda:0 (skipped on one-GPU boxes)."""
+    from notorch_amd.nn import ChempropBlock
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs two visible GPUs")
+    G = _graph("qm9", 64, seed=12)
+    h = 300
+    torch.manual_seed(0)
+    Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
+    blk = ChempropBlock(hidden_dim=h, depth=3).eval()
+    outs = []
+    for dev in ("cuda:0", "cuda:1"):
+        with torch.cuda.device(0), torch.no_grad():
+            b = blk.to(dev)
+            outs.append(b(G.update(node_feats=Xv, edge_feats=Xe).to(dev)).edge_feats.cpu())
+    assert torch.equal(outs[0], outs[1])

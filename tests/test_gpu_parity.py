@@ -120,7 +120,8 @@ def test_update_kernel(h, residual):
 @pytest.mark.parametrize("variant", ["as", "x6", "pc", "glds"])
 @pytest.mark.parametrize("h", [300, 296, 256, 100, 36])
 def test_update_kernel_variants(variant, h, monkeypatch):
-    """Every selectable update kernel (NT_UPDATE_KERNEL) against the fp64 restatement."""
+    """Every selectable update kernel (NT_UPDATE_KERNEL, diagnostic library) against the fp64
+    restatement; the shipping library runs its fixed dispatch for every variant name."""
     K = _K()
     monkeypatch.setenv("NT_UPDATE_KERNEL", variant)
     G = _graph_tensors("qm9", 37, seed=h + 1)

@@ -87,3 +87,21 @@ def test_gated_gradients():
     ro(G.update(node_feats=Xd).to(DEV)).pow(2).sum().backward()
     assert_parity(Xd.grad, ref_dX, 1e-5, "dX")
     assert_parity(ro.a.weight.grad, ref_dW, 1e-5, "da")
+
+
+def test_sdpa_query_gradient_with_frozen_encoder():
+    """a learned query with a frozen encoder (X without grad) must still get dL/dQ."""
+    from notorch_amd.nn import SDPAttention
+
+    G = _graph("qm9", 32, seed=5)
+    h = 24
+    torch.manual_seed(4)
+    X = torch.randn(G.num_nodes, h, dtype=torch.float64)
+    Q = torch.randn(len(G), h, dtype=torch.float64)
+    Qr = Q.clone().requires_grad_(True)
+    dmpnn_ref.readout_sdpa(X, G.batch_node_index, len(G), Qr, h ** 0.5).pow(2).sum().backward()
+    Qd = Q.float().to(DEV).requires_grad_(True)
+    out = SDPAttention(h)(G.update(node_feats=X.float()).to(DEV), Q=Qd)
+    assert out.grad_fn is not None
+    out.pow(2).sum().backward()
+    assert_parity(Qd.grad, Qr.grad, 1e-5, "dQ")
