@@ -1,6 +1,10 @@
 """Copy the judged parts of a gpurun profile directory into profiles/<round>/ and write a summary.
 
 Usage: python tools/save_profile.py gpurun_out/prof_r1b profiles/r1 [bench.json ...]
+
+Also writes PMC.json: HBM bytes per launch of the dominant kernel (FETCH_SIZE x2 + WRITE_SIZE,
+bench.read_pmc_traffic) with the commit it was taken at; bench.py reads the newest one for
+roofline.traffic when it runs without --pmc-csv.
 """
 import collections
 import csv
@@ -8,7 +12,11 @@ import glob
 import json
 import os
 import shutil
+import subprocess
 import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 src, dst = sys.argv[1], sys.argv[2]
 os.makedirs(dst, exist_ok=True)
@@ -35,5 +43,21 @@ for b in sys.argv[3:]:
     d = json.loads(txt)
     shutil.copy(b, os.path.join(dst, os.path.basename(b)))
     lines += [f"## bench line ({os.path.basename(b)})", "", "```json", json.dumps(d, indent=1), "```", ""]
+fetch = glob.glob(f"{src}/fetch/*counter_collection.csv")
+write = glob.glob(f"{src}/write/*counter_collection.csv")
+if fetch and write:
+    from bench import read_pmc_traffic
+
+    kern = os.environ.get("NT_PROFILE_KERNEL", "update_pk")
+    traffic = read_pmc_traffic(f"{fetch[0]},{write[0]}", kern)
+    if traffic is not None:
+        commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True,
+                                text=True).stdout.strip()
+        pmc = {"kernel": kern, "traffic_per_launch": traffic, "commit": commit, "time": time.time(),
+               "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE in separate passes; "
+                         "FETCH_SIZE x2 (gfx950 wide-load correction) + WRITE_SIZE, KB -> B, "
+                         "mean per dispatch"}
+        json.dump(pmc, open(os.path.join(dst, "PMC.json"), "w"), indent=1)
+        lines += [f"## HBM traffic per launch of `{kern}`: {traffic / 1e6:.1f} MB (PMC.json)", ""]
 open(os.path.join(dst, "SUMMARY.md"), "w").write("\n".join(lines))
 print("wrote", dst)
