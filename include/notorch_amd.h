@@ -282,6 +282,15 @@ NT_API int nt_gather_rows(const void* base, const void* X, const int64_t* idx, c
 NT_API int nt_dropout_residual(const void* base, const void* Y, int64_t n, float p, uint64_t seed,
                                uint64_t offset, int dtype, void* out, void* stream);
 
+/* Device status word of the calling device (no reference counterpart: the reference's ops cannot
+ * hang).  The persistent fp32 update kernel hands work between its waves through bounded LDS waits;
+ * a wait that gives up sets this word (sticky) and the launch's outputs are invalid.
+ * nt_device_status enqueues on `stream` a copy of the word into *host_out (caller-owned, pinned for
+ * an asynchronous copy); the wrapper raises on a nonzero word at its next call.
+ * nt_device_status_reset clears it (stream-ordered). */
+NT_API int nt_device_status(uint32_t* host_out, void* stream);
+NT_API int nt_device_status_reset(void* stream);
+
 #ifdef __cplusplus
 }
 #endif

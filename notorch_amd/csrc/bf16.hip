@@ -23,7 +23,8 @@
 
 namespace nt {
 
-int cu_count();  // update_ps.hip
+int cu_count();   // update_ps.hip
+int xcd_count();  // update_ps.hip
 
 namespace {
 
@@ -223,7 +224,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     const bf16_t* __restrict__ H, const bf16_t* __restrict__ S, const int64_t* __restrict__ src,
     const int64_t* __restrict__ rev, const uint4* __restrict__ Wp, const bf16_t* __restrict__ bias,
     int64_t V, int64_t E, int h, int KS, int NTn, int residual, int act, float alpha,
-    bf16_t* __restrict__ out, BfAgg agg, int ntiles) {
+    bf16_t* __restrict__ out, BfAgg agg, int ntiles, int nxcd) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   __shared__ int64_t soff[kM], qoff[kM], erow[kM];
   __shared__ int nstart[kM + 1], nnode[kM], nseg;
@@ -273,14 +274,23 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     cs = (s >= 0 && s < V) ? (int)s : -1;
     cq = (q >= 0 && q < E) ? (int)q : -1;
   };
-  if (w == 0 && (int)blockIdx.x < ntiles) {
-    stage_a(blockIdx.x);
+  // XCD-aware walk (as update_pk.hip): blocks b and b + nxcd share an XCD; each XCD takes one
+  // contiguous 1/nxcd of the tiles, so rows shared by neighbouring tiles stay in its L2.
+  int t_first = blockIdx.x, t_step = G, t_end = ntiles;
+  if (nxcd > 1 && G % nxcd == 0) {
+    const int x = (int)blockIdx.x % nxcd, chunk = (ntiles + nxcd - 1) / nxcd;
+    t_first = x * chunk + (int)blockIdx.x / nxcd;
+    t_step = G / nxcd;
+    t_end = min(ntiles, x * chunk + chunk);
+  }
+  if (w == 0 && t_first < t_end) {
+    stage_a(t_first);
     stage_b();
     stage_c();
   }
 
-  for (int t = blockIdx.x; t < ntiles; t += G) {
-    const bool has_next = t + G < ntiles;
+  for (int t = t_first; t < t_end; t += t_step) {
+    const bool has_next = t + t_step < t_end;
     if (w == 0) {  // publish this tile's indices (the previous tile's epilogue ended with a barrier)
       erow[lane] = ce;
       soff[lane] = cs >= 0 ? (int64_t)cs * h : -1;
@@ -298,7 +308,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
           nstart[__popcll(m)] = cn;
         }
       }
-      if (has_next) stage_a(t + G);
+      if (has_next) stage_a(t + t_step);
     }
     // B fragments of the first k step, in flight during the gather
     uint4 bcur[NW];
@@ -528,7 +538,7 @@ int launch_upd(const void* H, const void* S, const int64_t* src, const int64_t* 
   const int64_t g = grid < slots ? grid : slots;
   kern<<<(unsigned)g, kThreads, lds, stream>>>(
       (const bf16_t*)H, (const bf16_t*)S, src, rev, (const uint4*)Wp, (const bf16_t*)b, V, E, (int)h,
-      KS, NTn, residual, act, alpha, (bf16_t*)H_out, agg, (int)grid);
+      KS, NTn, residual, act, alpha, (bf16_t*)H_out, agg, (int)grid, xcd_count());
   NT_LAUNCH_CHECK();
   return NT_OK;
 }

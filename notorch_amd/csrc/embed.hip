@@ -13,9 +13,13 @@
 // (kv + ke) int64 type indices per edge instead of the Xv[src] and Xe rows (2 rows per edge), and
 // the embedding's own V + E row writes disappear: (E + V) rows written in total instead of
 // (2E + 2V) written + 2E read.
+#include <algorithm>
+
 #include "rows.hpp"
 
 namespace nt {
+int cu_count();  // update_ps.hip
+
 namespace {
 
 template <typename T, bool VEC>
@@ -109,15 +113,32 @@ __global__ void __launch_bounds__(256) init_embed_aggregate(
 // and 2 bond columns, transforms/graph.py:32-43): a node's in-edges are taken 4 at a time and every
 // index load of the 4 (perm -> src -> type rows) is issued before the first table row is summed,
 // so the three dependent index latencies are paid once per 4 edges instead of once per edge.
-template <typename T, bool VEC, int R, int ACT, int KV, int KE>
-__global__ void __launch_bounds__(256) init_embed_aggregate_k(
+//
+// LDS = true: both tables are first copied into LDS (a few tens of KiB: 42 x h and 13 x h), so the
+// nine table-row reads per edge are LDS reads instead of L2 round trips (the tables do not fit the
+// 32 KiB L1).  1024-thread workgroups, two per CU (kTabB of LDS each), grid-stride over the nodes.
+constexpr int kTabB = 72 * 1024;
+constexpr int kLdsThreads = 1024;
+
+template <typename T, bool VEC, int R, int ACT, int KV, int KE, bool LDS = false>
+__global__ void __launch_bounds__(LDS ? kLdsThreads : 256, LDS ? 2 : 1) init_embed_aggregate_k(
     EmbedArgs a, const int64_t* __restrict__ src, const int32_t* __restrict__ seg_ptr,
     const int32_t* __restrict__ perm, int64_t V, int64_t h, int act, float alpha,
     T* __restrict__ H0, T* __restrict__ S) {
   constexpr int N = Piece<T, VEC>::N;
-  constexpr int U = 4;
+  constexpr int U = LDS ? 2 : 4;  // LDS rows are cheap: fewer edges in flight, more waves
   const T* Tv = (const T*)a.Tv;
   const T* Te = (const T*)a.Te;
+  if constexpr (LDS) {
+    __shared__ uint4 tab[kTabB / 16];
+    const int64_t nvq = a.nv * h * (int64_t)sizeof(T) / 16, neq = a.ne * h * (int64_t)sizeof(T) / 16;
+    const uint4* gv = (const uint4*)a.Tv;
+    const uint4* ge = (const uint4*)a.Te;
+    for (int64_t i = threadIdx.x; i < nvq + neq; i += blockDim.x) tab[i] = i < nvq ? gv[i] : ge[i - nvq];
+    __syncthreads();
+    Tv = (const T*)tab;
+    Te = (const T*)(tab + nvq);
+  }
   const int64_t hw = h / N;
   const int64_t total = V * hw;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
@@ -128,7 +149,10 @@ __global__ void __launch_bounds__(256) init_embed_aggregate_k(
 #pragma unroll
     for (int i = 0; i < N; ++i) r[i].init();
     for (int32_t j = b; j < en; j += U) {
-      int64_t e[U], sv[U], tv[U][KV], te[U][KE];
+      // type indices narrowed to int32 once in range-checked form (a type index is < 2^31 or it is
+      // invalid anyway): half the registers of int64, so the kernel keeps 8 waves per SIMD
+      int64_t e[U], sv[U];
+      int tv[U][KV], te[U][KE];
 #pragma unroll
       for (int u = 0; u < U; ++u) e[u] = j + u < en ? (int64_t)perm[j + u] : -1;
 #pragma unroll
@@ -136,9 +160,15 @@ __global__ void __launch_bounds__(256) init_embed_aggregate_k(
 #pragma unroll
       for (int u = 0; u < U; ++u) {
 #pragma unroll
-        for (int q = 0; q < KV; ++q) tv[u][q] = e[u] >= 0 ? a.vtypes[sv[u] * KV + q] : -1;
+        for (int q = 0; q < KV; ++q) {
+          const int64_t x = e[u] >= 0 ? a.vtypes[sv[u] * KV + q] : -1;
+          tv[u][q] = (x >= 0 && x < a.nv) ? (int)x : -1;
+        }
 #pragma unroll
-        for (int q = 0; q < KE; ++q) te[u][q] = e[u] >= 0 ? a.etypes[e[u] * KE + q] : -1;
+        for (int q = 0; q < KE; ++q) {
+          const int64_t x = e[u] >= 0 ? a.etypes[e[u] * KE + q] : -1;
+          te[u][q] = (x >= 0 && x < a.ne) ? (int)x : -1;
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -150,15 +180,15 @@ __global__ void __launch_bounds__(256) init_embed_aggregate_k(
         // an invalid index (the host validates, so never in practice) contributes +0.0f
 #pragma unroll
         for (int q = 0; q < KV; ++q) {
-          const bool ok = tv[u][q] >= 0 && tv[u][q] < a.nv;
-          Piece<T, VEC>::load(Tv + (ok ? tv[u][q] : 0) * h + c, y);
+          const bool ok = tv[u][q] >= 0;
+          Piece<T, VEC>::load(Tv + (int64_t)(ok ? tv[u][q] : 0) * h + c, y);
 #pragma unroll
           for (int i = 0; i < N; ++i) xv[i] += ok ? y[i] : 0.f;
         }
 #pragma unroll
         for (int q = 0; q < KE; ++q) {
-          const bool ok = te[u][q] >= 0 && te[u][q] < a.ne;
-          Piece<T, VEC>::load(Te + (ok ? te[u][q] : 0) * h + c, y);
+          const bool ok = te[u][q] >= 0;
+          Piece<T, VEC>::load(Te + (int64_t)(ok ? te[u][q] : 0) * h + c, y);
 #pragma unroll
           for (int i = 0; i < N; ++i) xe[i] += ok ? y[i] : 0.f;
         }
@@ -207,9 +237,17 @@ int launch_init_embed(const EmbedArgs& a, const int64_t* src, const int32_t* seg
   if (V == 0) return NT_OK;
   const int grid = grid_for(V * (h / N), 256, 256 * 32);
   const bool k72 = a.kv == 7 && a.ke == 2;
+  // tables in LDS when both fit (fp32 h <= 327, bf16 h <= 655 at the reference's 42 + 13 types)
+  const bool lds = k72 && VEC && (a.nv + a.ne) * h * (int64_t)sizeof(T) <= kTabB &&
+                   (a.nv * h * (int64_t)sizeof(T)) % 16 == 0;
+  const int grid_lds = (int)std::min<int64_t>((V * (h / N) + kLdsThreads - 1) / kLdsThreads,
+                                              2 * (int64_t)cu_count());
 #define NT_IE(R_, A_)                                                                            \
   do {                                                                                           \
-    if (k72)                                                                                     \
+    if (lds)                                                                                     \
+      init_embed_aggregate_k<T, VEC, R_, A_, 7, 2, true><<<grid_lds, kLdsThreads, 0, stream>>>(  \
+          a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S);                               \
+    else if (k72)                                                                                \
       init_embed_aggregate_k<T, VEC, R_, A_, 7, 2><<<grid, 256, 0, stream>>>(                    \
           a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S);                               \
     else                                                                                         \

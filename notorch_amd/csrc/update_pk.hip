@@ -29,7 +29,9 @@
 
 namespace nt {
 
-__device__ unsigned int g_pk_timeout;  // set when a bounded spin gave up (debug getter below)
+// Device status word: set (sticky) when a bounded spin gave up; read by nt_device_status, which
+// the wrapper enqueues after every forward and checks at its next call.
+__device__ unsigned int g_pk_timeout;
 // diagnostic build (NT_PK_DIAG=1): per-wave cycle sums.  Consumers: [0] ready waits, [1] stage_free
 // waits, [2] whole loop; producers: [3] freed waits, [4] stage_ready waits, [5] finish, [6] whole
 // loop; [7] consumer waves, [8] producer waves.
@@ -105,6 +107,7 @@ struct Args {
   float4* O4;
   float4* SO4;
   int prio;  // NT_PK_PRIO: 1 = producers at s_setprio 1, 2 = consumers (A/B; 0 = none)
+  int nxcd;  // XCDs of the device (xcd_count()): blocks b and b + nxcd share an L2
 };
 
 // ------------------------------------------------------------------------------ LDS counters
@@ -345,15 +348,16 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
   int* emap = flags + kFlagInts;  // [kEmaps][64]: edge of every row of tile i in emap[i % kEmaps]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // XCD-aware tile walk: workgroups are dispatched round-robin over the 8 XCDs (XCD = blockIdx % 8),
-  // so give each XCD one contiguous eighth of the tile plan.  Neighbouring tiles share S / H rows
-  // (molecules straddle tile cuts), which then stay in that XCD's L2.
+  // XCD-aware tile walk: workgroups are dispatched round-robin over the nxcd XCDs (blocks b and
+  // b + nxcd share one), so give each XCD one contiguous 1/nxcd of the tile plan.  Neighbouring
+  // tiles share S / H rows (molecules straddle tile cuts), which then stay in that XCD's L2.
   int t0 = (int)blockIdx.x, tstride = (int)gridDim.x, nt;
-  if ((gridDim.x & 7) == 0) {
-    const int x = (int)blockIdx.x & 7, chunk = (a.ntiles + 7) >> 3;
+  const int nx = a.nxcd;
+  if (nx > 1 && (int)gridDim.x % nx == 0) {
+    const int x = (int)blockIdx.x % nx, chunk = (a.ntiles + nx - 1) / nx;
     const int lo = x * chunk, hi = min(a.ntiles, lo + chunk);
-    t0 = lo + ((int)blockIdx.x >> 3);
-    tstride = (int)gridDim.x >> 3;
+    t0 = lo + (int)blockIdx.x / nx;
+    tstride = (int)gridDim.x / nx;
     nt = hi > t0 ? (hi - t0 + tstride - 1) / tstride : 0;
   } else {
     nt = (a.ntiles - t0 + tstride - 1) / tstride;
@@ -643,7 +647,8 @@ int dispatch_pk(const Args& a, int ks, int grid, hipStream_t stream,
 
 }  // namespace
 
-int cu_count();  // update_ps.hip
+int cu_count();   // update_ps.hip
+int xcd_count();  // update_ps.hip
 
 int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntiles,
                      const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
@@ -672,6 +677,7 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
   a.aalpha = aalpha;
   a.O4 = (float4*)u.H_out;
   a.SO4 = (float4*)S_out;
+  a.nxcd = xcd_count();
   a.prio = 0;  // age arbitration (consumer priority measured +-1%: A/B only)
 #ifdef NT_DIAG
   {
@@ -694,14 +700,37 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
 
 }  // namespace nt
 
+extern "C" __attribute__((visibility("default"))) int nt_device_status(uint32_t* host_out,
+                                                                      void* stream) {
+  nt::clear_error();
+  NT_REQUIRE(host_out != nullptr, NT_EINVAL, "NULL status pointer");
+  if (hipMemcpyFromSymbolAsync(host_out, HIP_SYMBOL(nt::g_pk_timeout), sizeof(unsigned), 0,
+                               hipMemcpyDeviceToHost, nt::as_stream(stream)) != hipSuccess) {
+    nt::set_error("nt_device_status: hipMemcpyFromSymbolAsync failed");
+    return NT_EHIP;
+  }
+  return NT_OK;
+}
+
+extern "C" __attribute__((visibility("default"))) int nt_device_status_reset(void* stream) {
+  nt::clear_error();
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(nt::g_pk_timeout)) != hipSuccess ||
+      hipMemsetAsync(p, 0, sizeof(unsigned), nt::as_stream(stream)) != hipSuccess) {
+    nt::set_error("nt_device_status_reset: hipMemsetAsync failed");
+    return NT_EHIP;
+  }
+  return NT_OK;
+}
+
 // Debug-only (not part of include/notorch_amd.h): bounded-spin give-ups of the pk kernel.
 extern "C" __attribute__((visibility("default"))) int nt_debug_pk_timeouts(unsigned* out,
                                                                            int reset) {
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(nt::g_pk_timeout), sizeof(unsigned), 0,
                           hipMemcpyDeviceToHost) != hipSuccess)
     return 2;
-  if (reset) {
-    unsigned z = 0;
+  if (reset) {  // 1: clear; 2: set (tests of the wrapper's status check)
+    unsigned z = reset == 2 ? 1u : 0u;
     if (hipMemcpyToSymbol(HIP_SYMBOL(nt::g_pk_timeout), &z, sizeof(z), 0, hipMemcpyHostToDevice) !=
         hipSuccess)
       return 2;

@@ -593,6 +593,20 @@ int dispatch_ps(const Args& a, int ks, hipStream_t stream, std::integer_sequence
 #endif  // NT_DIAG
 }  // namespace
 
+// XCDs (XCCs) of the current device: blocks b and b + xcd_count() share an XCD's L2 (dispatch is
+// round-robin over the XCDs, MI355X_MICROARCH.md); 1 on a part or partition mode with one XCD.
+int xcd_count() {
+  static int n[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1;
+  if (n[dev] == 0) {
+    int c = 0;
+    if (hipDeviceGetAttribute(&c, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess || c <= 0) c = 1;
+    n[dev] = c;
+  }
+  return n[dev];
+}
+
 int cu_count() {
   static int n[64] = {0};
   int dev = 0;

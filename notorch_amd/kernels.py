@@ -32,6 +32,10 @@ __all__ = [
     "dmpnn_init_embed",
     "node_scores",
     "softmax_pool",
+    "watch_device_status",
+    "check_device_status",
+    "reset_device_status",
+    "DeviceStatusError",
 ]
 
 
@@ -634,3 +638,62 @@ def dropout_residual(Y: Tensor, p: float, seed: int, offset: int = 0, *, base: T
          _ptr(base), _ptr(Y), Y.numel(), float(p), int(seed) & (2**64 - 1), int(offset), code, _ptr(out),
          _stream(dev))
     return out
+
+
+# ------------------------------------------------------------------------------------ status word
+class DeviceStatusError(RuntimeError):
+    """A bounded wait inside the persistent update kernel gave up: outputs are invalid."""
+
+
+_STATUS: dict = {}  # device index -> (pinned uint32[1], torch.cuda.Event)
+
+
+def _status_error(dev: torch.device) -> DeviceStatusError:
+    return DeviceStatusError(
+        f"notorch_amd: a bounded producer/consumer wait in update_pk_kernel gave up on {dev}; the "
+        "outputs of the forward(s) since the last status check are invalid "
+        "(reset with notorch_amd.kernels.reset_device_status)")
+
+
+def watch_device_status(dev: torch.device) -> None:
+    """Called after every forward that ran the persistent kernel: raise if an EARLIER forward on
+    this device set the status word (checked without a host sync once its copy has landed), then
+    enqueue an asynchronous copy of the word into pinned host memory for the next call."""
+    if torch.cuda.is_current_stream_capturing():
+        return  # no queries / copies inside a hipGraph capture: replays are checked by check_device_status
+    ent = _STATUS.get(dev.index)
+    if ent is None:
+        ent = (torch.zeros(1, dtype=torch.int32).pin_memory(), torch.cuda.Event())
+        _STATUS[dev.index] = ent
+        fresh = True
+    else:
+        fresh = False
+    host, ev = ent
+    if not fresh and ev.query() and int(host[0]) != 0:
+        raise _status_error(dev)
+    _run(dev, _lib.load().nt_device_status, host.data_ptr(), _stream(dev))
+    ev.record(torch.cuda.current_stream(dev))
+
+
+def check_device_status(dev: torch.device | str | int = "cuda") -> None:
+    """Synchronous check (syncs dev's current stream): raise DeviceStatusError if the status word
+    is set."""
+    dev = torch.device(dev) if not isinstance(dev, int) else torch.device("cuda", dev)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    host = torch.zeros(1, dtype=torch.int32).pin_memory()
+    _run(dev, _lib.load().nt_device_status, host.data_ptr(), _stream(dev))
+    torch.cuda.current_stream(dev).synchronize()
+    if int(host[0]) != 0:
+        raise _status_error(dev)
+
+
+def reset_device_status(dev: torch.device | str | int = "cuda") -> None:
+    dev = torch.device(dev) if not isinstance(dev, int) else torch.device("cuda", dev)
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    _run(dev, _lib.load().nt_device_status_reset, _stream(dev))
+    ent = _STATUS.get(dev.index)
+    if ent is not None:
+        torch.cuda.current_stream(dev).synchronize()
+        ent[0].zero_()

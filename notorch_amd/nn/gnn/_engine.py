@@ -333,6 +333,8 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
             spare = H  # H_l is dead once H_{l+1} exists: reuse its buffer for H_{l+2}
         H = Hn
     node = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, _IDENTITY, chunks)
+    if persistent:
+        K.watch_device_status(H.device)
     return node, H, states
 
 
@@ -364,6 +366,8 @@ def _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual
             spare_H = H
             spare_S = S
         H, S = Hn, Sn
+    if H.dtype == torch.float32:  # the persistent kernel's bounded waits (bf16 has none)
+        K.watch_device_status(H.device)
     return S, H, states
 
 

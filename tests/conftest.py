@@ -25,3 +25,14 @@ def pytest_collection_modifyitems(config, items):
         for item in items:
             if "gpu" in item.keywords:
                 item.add_marker(skip)
+
+
+@pytest.fixture(autouse=True)
+def _device_status_clean(request):
+    """Every GPU test ends with the persistent kernel's status word clear (no bounded wait gave
+    up anywhere in the test): kernels.check_device_status syncs and raises otherwise."""
+    yield
+    if "gpu" in request.keywords and _gpu_available():
+        from notorch_amd import kernels
+
+        kernels.check_device_status()

@@ -47,11 +47,13 @@ def test_embed_bag_out_of_range_raises():
 
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("h", [256, 300, 13])
-def test_init_embed_bit_identical_to_unfused(dtype, h):
+@pytest.mark.parametrize("h,n", [(256, 48), (300, 48), (13, 48), (512, 48), (300, 3000), (512, 1500)])
+def test_init_embed_bit_identical_to_unfused(dtype, h, n):
+    """Fused embedding init == embed_bag + nt_dmpnn_init, bit for bit: tables staged in LDS (fp32
+    h <= 327, bf16 h <= 655), read from L2 otherwise (fp32 h = 512), scalar pieces (h = 13)."""
     from notorch_amd import kernels as K
 
-    G = _graph("zinc", 48, seed=2)
+    G = _graph("zinc", n, seed=2)
     torch.manual_seed(1)
     Tv = torch.randn(42, h).to(dtype).to(DEV)
     Te = torch.randn(13, h).to(dtype).to(DEV)
@@ -64,6 +66,11 @@ def test_init_embed_bit_identical_to_unfused(dtype, h):
     assert torch.equal(H0, H0_ref) and torch.equal(S, S_ref)
     H0b, none = K.dmpnn_init_embed(Tv, nt, Te, et, src)
     assert none is None and torch.equal(H0b, H0_ref)
+    relu = K.act_code(torch.nn.ReLU())
+    for reduce in ("mean", "max"):
+        H0_ref, S_ref = K.dmpnn_init(Xv, Xe, src, seg_ptr, perm, act=relu, reduce=reduce)
+        H0, S = K.dmpnn_init_embed(Tv, nt, Te, et, src, seg_ptr, perm, act=relu, reduce=reduce)
+        assert torch.equal(H0, H0_ref) and torch.equal(S, S_ref), reduce
 
 
 def _modules(h, depth, dtype=torch.float32, **opts):

@@ -289,3 +289,78 @@ def test_forward_on_a_non_current_device():
             b = blk.to(dev)
             outs.append(b(G.update(node_feats=Xv, edge_feats=Xe).to(dev)).edge_feats.cpu())
     assert torch.equal(outs[0], outs[1])
+
+
+def test_device_status_word_raises_on_next_forward():
+    """A set status word (what a give-up of a bounded ring wait leaves) makes the next forward
+    raise DeviceStatusError, and the synchronous check raises too; a reset clears both."""
+    import ctypes
+
+    from notorch_amd import _lib
+    from notorch_amd import kernels as K
+    from notorch_amd.nn import ChempropBlock
+
+    lib = _lib.load()
+    fn = lib.nt_debug_pk_timeouts
+    fn.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.c_int]
+    cnt = ctypes.c_uint(0)
+    G = _graph("qm9", 32, seed=3)
+    torch.manual_seed(0)
+    Gd = G.update(node_feats=torch.randn(G.num_nodes, 64), edge_feats=torch.randn(G.num_edges, 64)).to(DEV)
+    blk = ChempropBlock(hidden_dim=64, depth=2).eval().to(DEV)
+    with torch.no_grad():
+        blk(Gd)
+        torch.cuda.synchronize()
+        K.check_device_status()
+        assert fn(ctypes.byref(cnt), 2) == 0  # simulate a give-up
+        blk(Gd)  # copies the (set) word
+        torch.cuda.synchronize()
+        with pytest.raises(K.DeviceStatusError):
+            blk(Gd)
+        with pytest.raises(K.DeviceStatusError):
+            K.check_device_status()
+        K.reset_device_status()
+        blk(Gd)
+        blk(Gd)
+    K.check_device_status()
+
+
+def _n_for_tiles(pred, lo, hi, step=1):
+    """Smallest molecule count in [lo, hi) whose fused tile plan's ntiles satisfies pred."""
+    for n in range(lo, hi, step):
+        _, _, (_, ntiles, _), _ = _plan(_graph("qm9", n, seed=11))
+        if pred(ntiles):
+            return n, ntiles
+    pytest.skip("no batch size in range gives the wanted tile count")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("case", ["grid_eq_ntiles_mult8", "ragged_over_cus"])
+def test_xcd_walk_branches(dtype, case):
+    """Both branches of the XCD-aware tile walk (update_pk.hip / bf16.hip): (a) grid == ntiles with
+    ntiles % 8 == 0 (one tile per block, XCD chunks of ntiles / 8), (b) more tiles than resident
+    blocks with ntiles % 8 != 0 (ragged per-XCD chunks, several tiles per block)."""
+    K = _K()
+    slots = torch.cuda.get_device_properties(0).multi_processor_count * (2 if dtype == torch.bfloat16 else 1)
+    if case == "grid_eq_ntiles_mult8":
+        n, ntiles = _n_for_tiles(lambda t: t % 8 == 0 and 16 <= t <= slots, 20, 400)
+    else:
+        n, ntiles = _n_for_tiles(lambda t: t % 8 != 0 and t > slots + 3, 4 * slots, 8 * slots, 7)
+    G = _graph("qm9", n, seed=11)
+    h = 64
+    g = torch.Generator().manual_seed(n)
+    H, S = torch.randn(G.num_edges, h, generator=g), torch.randn(G.num_nodes, h, generator=g)
+    lin = nn.Linear(h, h)
+    W, b = lin.weight.detach(), lin.bias.detach()
+    if dtype == torch.bfloat16:
+        H, S, W, b = (x.to(torch.bfloat16).float() for x in (H, S, W, b))
+    _, perm, plan, zf = _plan(G)
+    relu = K.act_code(nn.ReLU())
+    Hn, Sn = K.dmpnn_update_fused(H.to(dtype).to(DEV), S.to(dtype).to(DEV), G.edge_index[0].to(DEV),
+                                  G.rev_index.to(DEV), K.pack_weights(W.to(dtype).to(DEV)),
+                                  b.to(dtype).to(DEV), residual=True, act=relu, plan=plan, perm=perm,
+                                  agg_act=relu, zero_fill=zf)
+    rH, rS = _ref_layer(G, H, S, W, b, True, torch.relu, "sum", torch.relu)
+    tol = FP32_NORM_TOL if dtype == torch.float32 else 2e-2
+    assert_parity(Hn.float(), rH, tol, f"{case} H ntiles={ntiles}")
+    assert_parity(Sn.float(), rS, tol, f"{case} S ntiles={ntiles}")
