@@ -43,7 +43,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 
 constexpr int kRows = 64;
-constexpr int kThreads = 512;
+constexpr int kPW = 4;                        // producer waves (the last kPW waves)
+__host__ __device__ constexpr int threads_for(int cw) { return (cw + kPW) * 64; }
 constexpr int kR = 6;                         // ring slots
 constexpr int kLCap = 6;                      // slices a producer keeps loading ahead (4 before)
 constexpr int kPartB = kRows * 4 * 16;        // one bf16 part of a slice: 4096 B
@@ -331,16 +332,19 @@ __device__ __forceinline__ void finish_tile(const Args& a, int t, const float* _
 // PF: rows of the next step's A fragments prefetched during the current step (of 4); the other rows
 // are read after the step's MFMAs.  PF = 2 frees 24 VGPRs, which removes the scratch spills the
 // full prefetch (PF = 4) caused inside the consumers' MFMA loop.
+// CW: consumer (MFMA) waves, 4 (one per SIMD) or 8 (two per SIMD: one wave's MFMAs cover its
+// partner's ring waits, fragment reads and W / residual load latency; consumer-only time at
+// config 2 108 -> 87 us).  PF = 0 and 5 producer slices in flight keep 3 waves per SIMD (168 VGPRs).
 template <int KS, int ACT, int AACT, bool SUMONLY, bool D = false, int ABL = 0, bool CWR = false,
-          int PF = 2>
-__global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
+          int PF = 0, int CW = 8>
+__global__ void __launch_bounds__(threads_for(CW), 1) update_pk_kernel(Args a) {
   unsigned long long st[4] = {0, 0, 0, 0};
   const unsigned long long t_begin = D ? pk_now() : 0;
   int gave_up = 0;
   auto report = [&]() {
     if (gave_up && (threadIdx.x & 63) == 0) atomicOr(&g_pk_timeout, 1u);
   };
-  constexpr int CT = (KS + 1) / 2;
+  constexpr int CT = (2 * KS + CW - 1) / CW;  // column tiles of the busiest consumer wave
   __shared__ __attribute__((aligned(16))) uint4 smem[kLdsB / 16];
   char* ring = reinterpret_cast<char*>(smem);
   float* stage = reinterpret_cast<float*>(ring + kR * kSliceB);
@@ -368,16 +372,17 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
   auto tile_of = [&](int i) { return t0 + i * tstride; };
   const int G = nt * KS;
 
-  if (a.prio == 1 && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  if (a.prio == 2 && wave < 4) __builtin_amdgcn_s_setprio(1);
-  if (wave >= 4) {
+  if (a.prio == 1 && wave >= CW) __builtin_amdgcn_s_setprio(1);
+  if (a.prio == 2 && wave < CW) __builtin_amdgcn_s_setprio(1);
+  if (wave >= CW) {
     // =============================================================== producers
-    const int pw = wave - 4;
+    const int pw = wave - CW;
     const int row = 16 * pw + (lane >> 2), kg = lane & 3;
     // Slice loads run L slices ahead of the LDS writes (a register ring, loop unrolled by L), so
     // each slice's gather latency overlaps L consumer steps.  Slice g + L belongs to the tile of
     // slice g or the next one (L < KS): rs_cur / rs_nxt, rotated when slice g starts a tile.
-    constexpr int L = KS == 1 ? 1 : (KS - 1 < kLCap ? KS - 1 : kLCap);
+    constexpr int LC = CW == 8 ? 5 : kLCap;  // 3 waves per SIMD: a 168-VGPR budget
+    constexpr int L = KS == 1 ? 1 : (KS - 1 < LC ? KS - 1 : LC);
     int e_cur = row_edge(a, tile_of(0), row);
     int e_nxt = nt > 1 ? row_edge(a, tile_of(1), row) : -1;
     RowSrc rs_cur = row_src(a, e_cur);
@@ -388,7 +393,7 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
       if (u < G) load_slice(a, pick_src(u / KS == 0, rs_cur, rs_nxt), u % KS, kg, q[u]);
     int fin = 0;  // next tile to finish: before slice (fin + 1) KS + kR - 1 is produced
     auto finish_next = [&]() {
-      wait_ge<D>(flags + kStageReady, 4 * (fin + 1), gave_up, &st[1]);  // consumers staged tile fin
+      wait_ge<D>(flags + kStageReady, CW * (fin + 1), gave_up, &st[1]);  // consumers staged tile fin
       const unsigned long long tf = D ? pk_now() : 0;
       if constexpr ((ABL & 1) == 0) {
         if (!CWR || a.SO4 != nullptr) finish_tile<AACT, SUMONLY, CWR>(a, tile_of(fin), stage, pw, lane);
@@ -416,7 +421,7 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
           if (s == 0 && kg == 0) emap[(i % kEmaps) * 64 + row] = e_cur;
           while (fin < nt && (fin + 1) * KS + (kR - 1) <= g) finish_next();
           const int slot = g % kR;
-          wait_ge<D>(flags + kFreed + slot, 4 * (g / kR), gave_up, &st[0]);
+          wait_ge<D>(flags + kFreed + slot, CW * (g / kR), gave_up, &st[0]);
           write_slice<ACT>(a, q[u], ring + slot * kSliceB, row, kg);
           signal(flags + kReady + slot, lane);
           const int gl = g + L;  // refill this register slot with slice g + L
@@ -443,7 +448,7 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
 
   // ================================================================= consumers
   const int g16 = lane >> 4, fr = lane & 15;
-  const int nc = (a.nt16 - wave + 3) / 4;
+  const int nc = (a.nt16 - wave + CW - 1) / CW;
   const int wbytes = KS * a.nt16 * 3 * 1024;
   const auto wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.Wb, (short)0, wbytes, 0x00020000);
   const int wvoff = lane * 16;
@@ -453,13 +458,13 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
     constexpr int NC = decltype(nc_tag)::value;
     f32x4 acc[4][CT];
     uint4 bw[NC][3];
-    bf16x8 af[4][3], an[PF][3];
+    bf16x8 af[4][3], an[PF > 0 ? PF : 1][3];
     auto load_w = [&](int ks, int j) {
       const int base = __builtin_amdgcn_readfirstlane(ks * step_bytes + wave * 3 * 1024);
 #pragma unroll
       for (int p = 0; p < 3; ++p)
         bw[j][p] = __builtin_bit_cast(
-            uint4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff, base + (4 * j * 3 + p) * 1024, 0));
+            uint4, __builtin_amdgcn_raw_buffer_load_b128(wrsrc, wvoff, base + (CW * j * 3 + p) * 1024, 0));
     };
     auto read_row = [&](int g, int rt, bf16x8 (&dst)[3]) {
       const char* base = ring + (g % kR) * kSliceB;
@@ -477,7 +482,7 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
     for (int i = 0; i < nt; ++i) {
       // The MFMA runs transposed (A operand = W fragment, B operand = edge fragment), so an
       // accumulator holds 4 consecutive output columns of one edge: C/D lane (fr, g16), register q
-      // = edge row 16 rt + fr, column 16 (wave + 4 j) + 4 g16 + q.  They start at the residual row
+      // = edge row 16 rt + fr, column 16 (wave + CW j) + 4 g16 + q.  They start at the residual row
       // pieces H[e] (one 16-B load each; rows past the tile read row 0 and are never stored);
       // slice (i, 0) is published, so tile i's row -> edge map is visible.
       const int hh = 4 * a.hv;
@@ -490,7 +495,7 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
           const int64_t e = er >= 0 ? er : 0;
 #pragma unroll
           for (int j = 0; j < CT; ++j) {
-            int col = 16 * (wave + 4 * j) + 4 * g16;
+            int col = 16 * (wave + CW * j) + 4 * g16;
             col = col < hh ? col : 0;
             if constexpr ((ABL & 4) != 0) {
               acc[rt][j] = f32x4{(float)e, 0.f, 0.f, 0.f};
@@ -559,7 +564,7 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
         const bool stage_it = !CWR || a.SO4 != nullptr;
 #pragma unroll
         for (int j = 0; j < NC; ++j) {
-          const int col = 16 * (wave + 4 * j) + 4 * g16;
+          const int col = 16 * (wave + CW * j) + 4 * g16;
           const float4 bj = (bf && col < hh) ? *reinterpret_cast<const float4*>(bf + col)
                                              : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
@@ -608,7 +613,14 @@ __global__ void __launch_bounds__(kThreads, 1) update_pk_kernel(Args a) {
 template <int KS, int ACT, int AACT, bool SUMONLY>
 int launch_pk(const Args& a, int grid, hipStream_t stream) {
   auto kern = update_pk_kernel<KS, ACT, AACT, SUMONLY>;
+  int threads = threads_for(8);
 #ifdef NT_DIAG
+  // NT_PK_NCW=4: one consumer wave per SIMD (the round-1 layout), for A/B
+  const char* ncw = getenv("NT_PK_NCW");
+  if (ncw && ncw[0] == '4') {
+    kern = update_pk_kernel<KS, ACT, AACT, SUMONLY, false, 0, false, 2, 4>;
+    threads = threads_for(4);
+  }
   // A/B builds (make DIAG=1): NT_PK_CW=1 consumers store H' (measured slower at config 2: 157 vs
   // 143 us), NT_PK_PF=4 the full next-step prefetch, NT_PK_DIAG=1 stamps, NT_PK_ABL=m ablations
   // (timing only: outputs are wrong)
@@ -629,7 +641,7 @@ int launch_pk(const Args& a, int grid, hipStream_t stream) {
     if (m == 15) kern = update_pk_kernel<KS, ACT, AACT, SUMONLY, false, 15>;
   }
 #endif
-  kern<<<grid, kThreads, 0, stream>>>(a);
+  kern<<<grid, threads, 0, stream>>>(a);
   NT_LAUNCH_CHECK();
   return NT_OK;
 }
