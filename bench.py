@@ -79,6 +79,12 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-embedded", action="store_true", help="skip embedded / fresh / end-to-end legs")
     p.add_argument("--no-secondary", action="store_true", help="skip the config-3 / config-5 keys")
+    p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                   help="process group for the bench bookkeeping (nccl = RCCL; gloo only to rehearse "
+                   "the N>1 path with --same-device on a one-GPU box)")
+    p.add_argument("--same-device", action="store_true",
+                   help="every rank on cuda:0 (rehearsal of the N>1 code path on one GPU; not a "
+                   "scaling measurement)")
     p.add_argument("--pmc-csv", default=None,
                    help="comma-separated rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs of the "
                    "same command (tools/profile.sh) to fill roofline.traffic")
@@ -280,6 +286,7 @@ def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
     except AttributeError:
         visible = os.cpu_count() or 1
     share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, visible)
+    thread_counts = sorted({1, share, visible})
 
     def one():
         with torch.inference_mode():
@@ -288,11 +295,13 @@ def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
 
     res = {}
     prev = torch.get_num_threads()
-    for P in sorted({1, share}):
+    for P in thread_counts:
         torch.set_num_threads(P)
-        one()  # warm-up
+        over = P > share  # more threads than the box gives this process: one timed run suffices
+        if not over:
+            one()  # warm-up
         times, t_start = [], time.perf_counter()
-        while (time.perf_counter() - t_start < budget_s and len(times) < 200) or len(times) < 3:
+        while (time.perf_counter() - t_start < budget_s and len(times) < 200) or len(times) < (1 if over else 3):
             t0 = time.perf_counter()
             one()
             times.append(time.perf_counter() - t0)
@@ -307,13 +316,15 @@ def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
         "kind": "port",
         "by_threads": {str(p): {"value": E * job.depth / m, "ms": m * 1e3, "runs": n} for p, (m, n) in res.items()},
         "sample": f"oracle/dmpnn_ref.py (ATen CPU restatement of chemprop.py+agg.py) on {sample} "
-        f"(V={G.num_nodes}, E={E}), fp32, torch.set_num_threads(P) for P in {sorted(res)} (P = 1 and "
-        f"the box's per-GPU CPU share, OMP_NUM_THREADS={share}); median of runs within {budget_s:.0f} s "
-        f"each after 1 warm-up; host cpus visible {visible}",
+        f"(V={G.num_nodes}, E={E}), fp32, torch.set_num_threads(P) for P in {sorted(res)} (P = 1, "
+        f"the box's per-GPU CPU share OMP_NUM_THREADS={share}, and every CPU in sched_getaffinity = "
+        f"{visible}); median of runs within {budget_s:.0f} s each after 1 warm-up; value and cores = "
+        f"the fastest P",
     }
 
 
 WS_BS = None  # (weights, biases) of the headline block on the host, for the CPU baseline
+BOOK_DEV = None  # device of the bookkeeping all-reduce tensors (the GPU under RCCL, cpu under gloo)
 
 
 # --------------------------------------------------------------------------- main
@@ -341,10 +352,11 @@ def run_workload(name, args, env, dev, headline):
     _engine.UPDATE_EVENTS = None
     info = dict(_engine.LAST_UPDATE_INFO)
     E_rank = sum(j.E for j in jobs)
-    units, secs, rate = aggregate_throughput(E_rank * depth * args.steps, elapsed, device=dev)
+    units, secs, rate = aggregate_throughput(E_rank * depth * args.steps, elapsed, device=BOOK_DEV)
     res = {"jobs": jobs, "embedding": embedding, "block": block, "readout": readout, "events": events,
            "info": info, "units": units, "secs": secs, "rate": rate, "batch": batch, "ranges": ranges,
-           "name": name, "kind": kind, "h": h, "depth": depth, "bf16": bf16, "n_mols": n_mols}
+           "name": name, "kind": kind, "h": h, "depth": depth, "bf16": bf16, "n_mols": n_mols,
+           "steps": args.steps}
     if headline:
         global WS_BS
         layers = block._chemprop_layers()
@@ -385,7 +397,7 @@ def embedded_leg(res, args, env, dev):
     for fuse in (True, False):
         enc = EmbeddedChempropBlock(res["embedding"], res["block"], fuse=fuse).eval()
         el = timed_steps(lambda: res["readout"](enc(Graw)), args.steps, max(2, args.warmup // 2), env, dev)
-        _, e_secs, e_rate = aggregate_throughput(job.E * job.depth * args.steps, el, device=dev)
+        _, e_secs, e_rate = aggregate_throughput(job.E * job.depth * args.steps, el, device=BOOK_DEV)
         tag = "fused" if fuse else "unfused"
         out[f"{tag}_ms_per_step"] = e_secs / args.steps * 1e3
         out[f"{tag}_value"] = e_rate
@@ -424,6 +436,41 @@ def end_to_end_leg(res, dev):
             "total_ms": total, "value": job.E * job.depth / (total * 1e-3), "unit": "edge-messages/s"}
 
 
+def pipeline_leg(res, dev, workers, n_batches=24, warm=4):
+    """Steady-state host feed: per-molecule Graphs -> DataLoader workers (native collate, CSR and
+    tile plan) -> pinned batches -> H2D on a side stream overlapped with the previous batch's
+    EmbeddedChempropBlock + Sum (notorch_amd.data.loader.graph_loader)."""
+    from notorch_amd.data.loader import graph_loader
+    from notorch_amd.nn import EmbeddedChempropBlock
+
+    job = res["jobs"][0]
+    graphs = job.batch.to_graphs()
+    B = len(graphs)
+    dataset = graphs * n_batches  # the same molecules every batch (references, no copies)
+    enc = EmbeddedChempropBlock(res["embedding"], res["block"], fuse=True).eval()
+    loader = graph_loader(dataset, B, dev, num_workers=workers)
+    with torch.no_grad():
+        it = iter(loader)
+        for _ in range(warm):
+            res["readout"](enc(next(it)))
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        n = 0
+        for G in it:
+            res["readout"](enc(G))
+            n += 1
+        torch.cuda.synchronize(dev)
+        t = (time.perf_counter() - t0) / max(n, 1)
+    del loader, it
+    device_ms = res["secs"] / res["steps"] / len(res["jobs"]) * 1e3
+    return {"step": f"{B} host Graphs per batch -> DataLoader({workers} workers, native collate, "
+                    "pin_memory) -> side-stream non_blocking H2D overlapped with the previous batch's "
+                    "EmbeddedChempropBlock + Sum; steady state over "
+                    f"{n} batches after {warm}", "workers": workers, "ms_per_batch": t * 1e3,
+            "device_step_ms": device_ms, "ratio_to_device_step": t * 1e3 / device_ms,
+            "value": job.E * job.depth / t, "unit": "edge-messages/s"}
+
+
 def summary(res, args, env, pmc_csv=None):
     jobs = res["jobs"]
     info = res["info"]
@@ -451,10 +498,15 @@ def summary(res, args, env, pmc_csv=None):
 def main():
     args = parse()
     env = dist_env()
+    dev = torch.device("cuda", 0 if args.same_device else env.local_rank)
     if env.distributed:
-        torch.cuda.set_device(env.local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", env.local_rank))
-    dev = torch.device("cuda", env.local_rank)
+        torch.cuda.set_device(dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    global BOOK_DEV
+    BOOK_DEV = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     from notorch_amd import _lib
 
@@ -467,6 +519,12 @@ def main():
         embedded = embedded_leg(res, args, env, dev)
         if env.rank == 0:
             e2e = end_to_end_leg(res, dev)
+            try:
+                share = len(os.sched_getaffinity(0))
+            except AttributeError:
+                share = os.cpu_count() or 4
+            share = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or share, share, 16)
+            e2e["pipelined"] = pipeline_leg(res, dev, workers=max(4, share - 2))
     roof, fwd = summary(res, args, env, args.pmc_csv)
 
     secondary = None

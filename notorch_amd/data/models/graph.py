@@ -22,6 +22,8 @@ bit for bit; ``rev_offset="edges"`` is the corrected collate.
 from __future__ import annotations
 
 import weakref
+from itertools import repeat
+from operator import attrgetter
 from copy import copy
 from dataclasses import InitVar, dataclass, field
 from typing import Iterable, Literal, Optional
@@ -79,13 +81,22 @@ class DeviceLayout:
             st["type_src"] = "owner"
         return st
 
-    def to(self, device, edge_index: Tensor, batch_node_index: Optional[Tensor]) -> "DeviceLayout":
-        mv = lambda t: None if t is None else t.to(device, non_blocking=True)  # noqa: E731
+    def tensors(self) -> list:
+        """Every tensor the layout owns (CSR arrays, plans, chunk plans)."""
+        out = [t for t in (self.dst_ptr, self.dst_perm, self.mol_ptr, self.mol_perm) if t is not None]
+        for p in (self.plan, self.dst_chunks, self.mol_chunks[1] if self.mol_chunks else None):
+            if p:
+                out += [x for x in p if isinstance(x, Tensor)]
+        return out
+
+    def map_tensors(self, fn, edge_index: Tensor, batch_node_index: Optional[Tensor]) -> "DeviceLayout":
+        """A copy of the layout with fn applied to every tensor it owns (device moves, pinning)."""
+        mv = lambda t: None if t is None else fn(t)  # noqa: E731
 
         def mv_plan(p):  # (tensors and ints) tuples or False / None
             if not p:
                 return p
-            return tuple(x.to(device, non_blocking=True) if isinstance(x, Tensor) else x for x in p)
+            return tuple(fn(x) if isinstance(x, Tensor) else x for x in p)
 
         new = DeviceLayout(
             mv(self.dst_ptr),
@@ -102,6 +113,9 @@ class DeviceLayout:
         if self.mol_chunks is not None and new.mol_ptr is not None:
             new.mol_chunks = (new.mol_ptr, mv_plan(self.mol_chunks[1]))
         return new
+
+    def to(self, device, edge_index: Tensor, batch_node_index: Optional[Tensor]) -> "DeviceLayout":
+        return self.map_tensors(lambda t: t.to(device, non_blocking=True), edge_index, batch_node_index)
 
 
 @dataclass(repr=False, eq=False)
@@ -132,15 +146,47 @@ class Graph(UpdateMixin):
     def device(self):
         return self._device
 
-    def to(self, device):
+    def to(self, device, non_blocking: bool = False):
+        """Move in place (reference graph.py:41-43).  non_blocking: asynchronous copies from pinned
+        host memory (pin_memory()), ordered on the current stream."""
         types_ok = self._layout_types_ok()
         self._device = device
-        self.node_feats = self.node_feats.to(device)
-        self.edge_feats = self.edge_feats.to(device)
-        self.edge_index = self.edge_index.to(device)
-        self.rev_index = self.rev_index.to(device)
+        self.node_feats = self.node_feats.to(device, non_blocking=non_blocking)
+        self.edge_feats = self.edge_feats.to(device, non_blocking=non_blocking)
+        self.edge_index = self.edge_index.to(device, non_blocking=non_blocking)
+        self.rev_index = self.rev_index.to(device, non_blocking=non_blocking)
         self._move_layout(device, types_ok)
         return self
+
+    def _feature_tensors(self) -> list:
+        return [self.node_feats, self.edge_feats, self.edge_index, self.rev_index]
+
+    def tensors(self) -> list:
+        """Every tensor of the graph and of its kernel layout."""
+        lay = getattr(self, "_nt_layout", None)
+        return self._feature_tensors() + (lay.tensors() if lay is not None else [])
+
+    def pin_memory(self):
+        """Copy of the graph with every host tensor (features, indices, CSR layout, plans) in pinned
+        memory, so .to(device, non_blocking=True) is an asynchronous DMA.  torch's DataLoader calls
+        this on collated batches when pin_memory=True."""
+        types_ok = self._layout_types_ok()
+        other = copy(self)
+        for name in self._field_names():
+            setattr(other, name, getattr(self, name).pin_memory())
+        lay = getattr(self, "_nt_layout", None)
+        if lay is not None:
+            moved = lay.map_tensors(Tensor.pin_memory, other.edge_index, getattr(other, "batch_node_index", None))
+            if types_ok:
+                moved.type_src = (weakref.ref(other.node_feats), weakref.ref(other.edge_feats),
+                                  (other.node_feats._version, other.edge_feats._version))
+            else:
+                moved.type_range = None
+            other._nt_layout = moved
+        return other
+
+    def _field_names(self) -> list:
+        return ["node_feats", "edge_feats", "edge_index", "rev_index"]
 
     def __setstate__(self, state):
         self.__dict__.update(state)
@@ -210,17 +256,19 @@ class BatchedGraph(Graph):
     def __len__(self) -> int:
         return self._size
 
-    def to(self, device):
+    def to(self, device, non_blocking: bool = False):
         types_ok = self._layout_types_ok()
         self._device = device
-        self.node_feats = self.node_feats.to(device)
-        self.edge_feats = self.edge_feats.to(device)
-        self.edge_index = self.edge_index.to(device)
-        self.rev_index = self.rev_index.to(device)
-        self.batch_node_index = self.batch_node_index.to(device)
-        self.batch_edge_index = self.batch_edge_index.to(device)
+        for name in self._field_names():
+            setattr(self, name, getattr(self, name).to(device, non_blocking=non_blocking))
         self._move_layout(device, types_ok)
         return self
+
+    def _field_names(self) -> list:
+        return ["node_feats", "edge_feats", "edge_index", "rev_index", "batch_node_index", "batch_edge_index"]
+
+    def _feature_tensors(self) -> list:
+        return [getattr(self, n) for n in self._field_names()]
 
     @classmethod
     def from_graphs(cls, Gs: Iterable[Graph], rev_offset: RevOffset = "nodes") -> "BatchedGraph":
@@ -237,7 +285,7 @@ class BatchedGraph(Graph):
             raise ValueError("from_graphs needs at least one graph")
         if rev_offset not in ("nodes", "edges"):
             raise ValueError(f"rev_offset must be 'nodes' or 'edges', got {rev_offset!r}")
-        if all(G.edge_index.device.type == "cpu" and G.node_feats.device.type == "cpu" for G in Gs):
+        if all(map(attrgetter("edge_index.is_cpu"), Gs)) and all(map(attrgetter("node_feats.is_cpu"), Gs)):
             return _native_collate(cls, Gs, rev_offset)
         return cls._from_graphs_device(Gs, rev_offset)
 
@@ -293,22 +341,30 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
     def _c(x):  # contiguous int64 view, without a call per graph in the common case
         return x if (x.dtype is i64 and x.is_contiguous()) else x.to(i64).contiguous()
 
-    nf, ef, ei, rv, nn_, ne_ = [], [], [], [], [], []
-    for G in Gs:  # one pass: the per-graph Python cost is what bounds this collate
-        x, y, z, r = G.node_feats, G.edge_feats, G.edge_index, G.rev_index
-        nf.append(x if x.is_contiguous() else x.contiguous())
-        ef.append(y if y.is_contiguous() else y.contiguous())
-        ei.append(_c(z))
-        rv.append(_c(r))
-        nn_.append(x.shape[0])
-        ne_.append(y.shape[0])
+    # per-graph work through C-level map() over the tensors' own methods: the per-graph Python cost
+    # is what bounds this collate (the copies and the CSR are one C++ pass)
+    T = Tensor
+    nf = list(map(attrgetter("node_feats"), Gs))
+    ef = list(map(attrgetter("edge_feats"), Gs))
+    ei = list(map(attrgetter("edge_index"), Gs))
+    rv = list(map(attrgetter("rev_index"), Gs))
+    if not all(map(T.is_contiguous, nf)):
+        nf = [x.contiguous() for x in nf]
+    if not all(map(T.is_contiguous, ef)):
+        ef = [y.contiguous() for y in ef]
+    if not (all(map(T.is_contiguous, ei)) and {z.dtype for z in ei} == {i64}):
+        ei = [_c(z) for z in ei]
+    if not (all(map(T.is_contiguous, rv)) and {r.dtype for r in rv} == {i64}):
+        rv = [_c(r) for r in rv]
+    nn_ = list(map(T.size, nf, repeat(0)))  # Tensor.size(0): C-level (len() goes through Python)
+    ne_ = list(map(T.size, ef, repeat(0)))
     nd, ed = nf[0], ef[0]
     nrow, erow = nd.shape[1:], ed.shape[1:]
-    if any(x.dtype != nd.dtype or x.shape[1:] != nrow for x in nf):
+    if len({(x.dtype, x.shape[1:]) for x in nf}) != 1:
         raise RuntimeError("from_graphs: node_feats of the graphs differ in dtype or row shape")
-    if any(x.dtype != ed.dtype or x.shape[1:] != erow for x in ef):
+    if len({(x.dtype, x.shape[1:]) for x in ef}) != 1:
         raise RuntimeError("from_graphs: edge_feats of the graphs differ in dtype or row shape")
-    if any(z.numel() != 2 * n or r.numel() != n for z, r, n in zip(ei, rv, ne_)):
+    if list(map(T.numel, ei)) != [2 * n for n in ne_] or list(map(T.numel, rv)) != ne_:
         raise RuntimeError("from_graphs: edge_index / rev_index do not match edge_feats")
     n_nodes = torch.tensor(nn_, dtype=i64)
     n_edges = torch.tensor(ne_, dtype=i64)
@@ -322,7 +378,12 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
     dst_ptr = torch.empty(V + 1, dtype=torch.int32)
     dst_perm = torch.empty(E, dtype=torch.int32)
     mol_ptr = torch.empty(B + 1, dtype=torch.int32)
-    ptrs = lambda ts: (ctypes.c_void_p * B)(*[t.data_ptr() for t in ts])  # noqa: E731
+    def ptrs(ts):  # array of the B data pointers, passed as one pointer
+        a = np.fromiter(map(T.data_ptr, ts), dtype=np.uint64, count=B)
+        keep.append(a)
+        return a.ctypes.data
+
+    keep: list = []
     lib = _lib.load()
     _lib.check(lib.nt_collate_graphs(
         B, ptrs(nf), n_nodes.data_ptr(), nd[0].numel() * nd.element_size() if nd.dim() else nd.element_size(),
@@ -336,7 +397,7 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
     lay = DeviceLayout(dst_ptr, dst_perm, edge_index=edge_index, validated=True)
     # rev_offset="nodes" can push rev_index past E only for graphs with fewer edges than nodes
     # (reference quirk): leave such batches to the device-side check
-    lay.validated = E == 0 or int(rev_index.max()) < E
+    lay.validated = E == 0 or int(rev_index.numpy().max()) < E  # numpy: no intra-op pool wake-up
     lay.mol_ptr, lay.mol_perm, lay.batch_node_index = mol_ptr, None, bni
     host_stats(lay, dst_ptr.numpy(), E, mol_ptr.numpy(), node_out, edge_out)
     BG._nt_layout = lay
@@ -456,7 +517,8 @@ def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional
     tr = []
     for X in (node_feats, edge_feats):
         if X is not None and X.dim() == 2 and X.dtype == torch.int64 and X.device.type == "cpu":
-            tr.append((int(X.min()), int(X.max())) if X.numel() else (0, -1))
+            xn = X.numpy()
+            tr.append((int(xn.min()), int(xn.max())) if X.numel() else (0, -1))
         else:
             tr.append(None)
     lay.type_range = tuple(tr)

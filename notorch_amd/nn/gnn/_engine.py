@@ -396,6 +396,98 @@ def _torch_block(Xv, Xe, edge_index, rev, weights, biases, act_mod, reduce, resi
     return _torch_scatter(H, dst, V, reduce), H
 
 
+# ------------------------------------------------------------------------------------ layerwise
+# Blocks the fused kernels do not take as one unit: an activation outside the kernels' codes (any
+# nn.Module, chemprop.py:17,24,37), or layers that differ in activation or dropout.  Every layer
+# runs unfused on the device: M = act(H) as the module's own elementwise op when it has no kernel
+# code, then the segment-reduce and update kernels on M with the identity activation
+# (S = scatter(M, dst), U = W (S[src] - M[rev]) + b), dropout by the hash kernel, residual add.
+def layer_act(act_mod: torch.nn.Module) -> Optional[tuple[int, float]]:
+    try:
+        return K.act_code(act_mod)
+    except NotImplementedError:
+        return None
+
+
+def block_forward_layerwise(Xv, Xe, src, rev, lay, acts, weights, biases, drops, reduce, residual):
+    """acts[l] = (module, kernel code or None); drops[l] = (p, seed) or None.  Returns (node, H_d)."""
+    V = Xv.shape[0]
+    H, _ = K.dmpnn_init(Xv, Xe, src)
+    chunks = dst_chunks(lay)
+    E, h = H.shape
+    for l, ((mod, code), W, b) in enumerate(zip(acts, weights, biases)):
+        if code is None:
+            M, code_l = mod(H).contiguous(), _IDENTITY
+        else:
+            M, code_l = H, code
+        S = _aggregate(M, lay.dst_ptr, lay.dst_perm, V, reduce, code_l, chunks)
+        Wp = pack_layer_weights([W])[0]
+        U = K.dmpnn_update(M, S, src, rev, Wp, None if b is None else b.detach(), residual=False, act=code_l)
+        if drops[l] is not None:
+            H = K.dropout_residual(U, drops[l][0], drops[l][1], dropout_offset(l, E, h),
+                                   base=H if residual else None, out=U)
+        else:
+            H = H + U if residual else U
+    node = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, _IDENTITY, chunks)
+    return node, H
+
+
+def _torch_block_layerwise(Xv, Xe, edge_index, rev, weights, biases, act_mods, reduce, residual, masks):
+    src, dst = edge_index[0], edge_index[1]
+    V = Xv.shape[0]
+    H = Xv[src] + Xe
+    for l, (W, b) in enumerate(zip(weights, biases)):
+        M = act_mods[l](H)
+        S = _torch_scatter(M, dst, V, reduce)
+        U = torch.nn.functional.linear(S[src] - M[rev], W, b)
+        if masks[l] is not None:
+            U = U * masks[l]
+        H = H + U if residual else U
+    return _torch_scatter(H, dst, V, reduce), H
+
+
+class LayerwiseBlockFunction(torch.autograd.Function):
+    """Kernel forward (block_forward_layerwise); backward by recomputing the same math in PyTorch
+    device ops under autograd (any activation module, per-layer dropout masks regenerated by the
+    hash kernel)."""
+
+    @staticmethod
+    def forward(ctx, Xv, Xe, edge_index, rev, lay, acts, drops, reduce, residual, nlayers, *params):
+        weights, biases = list(params[:nlayers]), list(params[nlayers:])
+        node, H = block_forward_layerwise(Xv, Xe, edge_index[0].contiguous(), rev, lay, acts, weights,
+                                          biases, drops, reduce, residual)
+        ctx.save_for_backward(Xv, Xe, edge_index, rev, *[p if p is not None else torch.empty(0) for p in params])
+        ctx.cfg = (acts, drops, reduce, residual, nlayers, [p is None for p in params])
+        return node, H
+
+    @staticmethod
+    def backward(ctx, dnode, dH):
+        acts, drops, reduce, residual, nlayers, is_none = ctx.cfg
+        Xv, Xe, edge_index, rev, *rest = ctx.saved_tensors
+        params = [None if n else p for p, n in zip(rest, is_none)]
+        need = ctx.needs_input_grad
+        with torch.enable_grad():
+            Xv_ = Xv.detach().requires_grad_(need[0])
+            Xe_ = Xe.detach().requires_grad_(need[1])
+            ps = [None if p is None else p.detach().requires_grad_(True) for p in params]
+            E, h = Xe.shape
+            masks = [None if d is None else K.dropout_residual(torch.ones_like(Xe), d[0], d[1], dropout_offset(l, E, h))
+                     for l, d in enumerate(drops)]
+            node, H = _torch_block_layerwise(Xv_, Xe_, edge_index, rev, ps[:nlayers], ps[nlayers:],
+                                             [a[0] for a in acts], reduce, residual, masks)
+            leaves = [t for t in [Xv_, Xe_] + ps if t is not None and t.requires_grad]
+            outs, grads = [], []
+            for o, g in ((node, dnode), (H, dH)):
+                if g is not None:
+                    outs.append(o)
+                    grads.append(g)
+            got = torch.autograd.grad(outs, leaves, grads, allow_unused=True)
+        it = iter(got)
+        res_inputs = [next(it) if need[0] else None, next(it) if need[1] else None]
+        res_params = [None if p is None else next(it) for p in ps]
+        return (*res_inputs, None, None, None, None, None, None, None, None, *res_params)
+
+
 def backward_layout(lay: DeviceLayout, src: Tensor, rev: Tensor, V: int, E: int) -> tuple:
     """(src_ptr, src_perm, rev_ptr, rev_perm): the CSRs of the two gathers' transposes (scatter by
     src into nodes, scatter by rev_index into edges), built once per graph and cached on its layout."""

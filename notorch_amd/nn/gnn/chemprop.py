@@ -86,14 +86,20 @@ class ChempropLayer(nn.Module):
         """U = Dropout(Linear(S[src] - act(H)[rev])), S = scatter(act(H), dst) — no residual here."""
         drop = _dropout([self])
         V = len(node_feats)
-        act = K.act_code(self.act)
-        if drop is not None or (torch.is_grad_enabled()
-                                and (edge_feats.requires_grad or self.linear.weight.requires_grad)):
-            # training through a standalone layer: route through the block function with depth 1
-            # and no residual, then subtract nothing (the block function returns H_1 = U).
+        act = _engine.layer_act(self.act)
+        if drop is not None or act is None or (
+                torch.is_grad_enabled() and (edge_feats.requires_grad or self.linear.weight.requires_grad)):
+            # training through a standalone layer (or an activation without a kernel code): route
+            # through the block function with depth 1 and no residual (it returns H_1 = U)
             lay = _engine.DeviceLayout(*self._csr(edge_index, rev_index, V), edge_index=edge_index, validated=True)
             Xv = torch.zeros(V, edge_feats.shape[1], device=edge_feats.device, dtype=edge_feats.dtype)
             # H0 = Xv[src] + Xe = edge_feats exactly (adding +0.0)
+            if act is None:
+                _, H = _engine.LayerwiseBlockFunction.apply(
+                    Xv, edge_feats, edge_index, rev_index.contiguous(), lay, [(self.act, None)], [drop],
+                    self.reduce, False, 1, self.linear.weight, self.linear.bias,
+                )
+                return H
             _, H = _engine.ChempropBlockFunction.apply(
                 Xv, edge_feats, edge_index, rev_index.contiguous(), lay, self.act, act, self.reduce,
                 False, 1, drop, self.linear.weight, self.linear.bias,
@@ -164,11 +170,6 @@ class ChempropBlock(nn.Module):
                 f"node_feats ({Xv.dtype}), edge_feats ({Xe.dtype}) and the layer weights must share "
                 "one dtype (float32, or bfloat16 after block.to(torch.bfloat16))"
             )
-        drop = _dropout(layers)
-        acts = {K.act_code(layer.act) for layer in layers}
-        if len(acts) > 1:
-            raise NotImplementedError("layers with different activations are not supported")
-        act = acts.pop() if acts else (NT_ACT_IDENTITY, 0.0)
         residual = bool(layers) and isinstance(self.layers[0], Residual)
         lay = _engine.dst_layout(G)
         Xv = Xv.contiguous()
@@ -179,6 +180,28 @@ class ChempropBlock(nn.Module):
         needs_grad = torch.is_grad_enabled() and (
             Xv.requires_grad or Xe.requires_grad or any(p.requires_grad for p in self.parameters())
         )
+        codes = [_engine.layer_act(layer.act) for layer in layers]
+        dps = [float(l.update[1].p) if l.training and l.update[1].p > 0 else None for l in layers]
+        uniform = all(c is not None for c in codes) and len(set(codes)) <= 1 and len(set(dps)) <= 1
+        if not uniform:
+            seed = _engine.draw_dropout_seed() if any(p is not None for p in dps) else 0
+            drops = [None if p is None else (p, seed) for p in dps]  # disjoint per-layer offsets
+            # an activation without a kernel code, or layers that differ in activation / dropout:
+            # the layer-by-layer device path (_engine.block_forward_layerwise)
+            acts = [(layer.act, c) for layer, c in zip(layers, codes)]
+            if needs_grad:
+                node, H = _engine.LayerwiseBlockFunction.apply(
+                    Xv, Xe, G.edge_index, rev, lay, acts, drops, self.reduce, residual, len(layers),
+                    *weights, *biases,
+                )
+            else:
+                node, H = _engine.block_forward_layerwise(
+                    Xv, Xe, G.edge_index[0].contiguous(), rev, lay, acts, weights, biases, drops,
+                    self.reduce, residual,
+                )
+            return G.update(node_feats=node, edge_feats=H)
+        drop = _dropout(layers)
+        act = codes[0] if codes else (NT_ACT_IDENTITY, 0.0)
         if needs_grad:
             node, H = _engine.ChempropBlockFunction.apply(
                 Xv, Xe, G.edge_index, rev, lay, layers[0].act if layers else nn.Identity(), act,

@@ -97,15 +97,13 @@ class EmbeddedChempropBlock(nn.Module):
             and emb.node.weight.dtype == emb.edge.weight.dtype
             and not any(l.training and l.update[1].p > 0 for l in blk._chemprop_layers())  # dropout
         )
-        if not fusable:
-            return blk(emb(G))
         layers = blk._chemprop_layers()
+        codes = [_engine.layer_act(l.act) for l in layers]
+        if not fusable or any(c is None for c in codes) or len(set(codes)) > 1:
+            return blk(emb(G))  # the block takes generic / mixed activations layer by layer
         if any(l.linear.weight.dtype != emb.node.weight.dtype for l in layers):
             raise RuntimeError("embedding tables and layer weights must share one dtype")
-        acts = {K.act_code(l.act) for l in layers}
-        if len(acts) > 1:
-            raise NotImplementedError("layers with different activations are not supported")
-        act = acts.pop() if acts else (NT_ACT_IDENTITY, 0.0)
+        act = codes[0] if codes else (NT_ACT_IDENTITY, 0.0)
         residual = bool(layers) and isinstance(blk.layers[0], Residual)
         # the layout needs V: give dst_layout a graph whose node_feats has V rows (the type matrix)
         lay = _engine.dst_layout(G)

@@ -328,6 +328,33 @@ def test_polymer_hubs_parity():
     assert_parity(out.node_feats, ref_n, what="node")
 
 
+@pytest.mark.parametrize("rev_offset", ["nodes", "edges"])
+def test_polymer_bench_config_parity(rev_offset):
+    """BASELINE config 5 exactly as bench.py runs it (16 polymer graphs of 1k-10k atoms, hubs of
+    in-degree up to ~512, seed 1000, h = 300, depth 3, default init), in the reference collate's
+    compat rev mode and in fixed mode: block outputs and the Sum readout against the oracle
+    (chemprop.py:81-88 with the scatter over hub segments at :39 / :86, agg.py:23-29)."""
+    from notorch_amd.data.synth import make_batch
+    from notorch_amd.nn import ChempropBlock, Sum
+
+    G = make_batch("polymer", 16, seed=1000).collate(rev_offset)
+    assert G.num_nodes > 40_000 and int(torch.bincount(G.edge_index[1]).max()) >= 100
+    h = 300
+    Xv, Xe = _embed(G, h, seed=0)
+    torch.manual_seed(0)
+    blk = ChempropBlock(hidden_dim=h, depth=3).eval()
+    Ws, bs = dmpnn_ref.block_params(blk)
+    ref_n, ref_e = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, Ws, bs)
+    ref_r = dmpnn_ref.readout(ref_n, G.batch_node_index, len(G), "sum")
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
+    with torch.no_grad():
+        out = blk.to(DEV)(Gd)
+        r = Sum()(out)
+    assert_parity(out.edge_feats, ref_e, what=f"edge {rev_offset}")
+    assert_parity(out.node_feats, ref_n, what=f"node {rev_offset}")
+    assert_parity(r, ref_r, what=f"readout {rev_offset}")
+
+
 def test_fixed_mode_batching_invariance_bitexact():
     """Fixed-rev collate: forward(batch) == concat(forward(shard_i)) bit for bit, at full size."""
     from notorch_amd.data.synth import make_batch

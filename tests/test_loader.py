@@ -1,0 +1,40 @@
+"""CPU: the host feed (notorch_amd.data.loader) — DataLoader workers running the
+native collate return exactly what BatchedGraph.from_graphs returns in the main process
+(transforms/graph.py:45 -> graph.py:186-223), including the shipped CSR layout and tile plan."""
+import pickle
+
+import torch
+
+from notorch_amd.data.loader import GraphCollator
+from notorch_amd.data.models.graph import BatchedGraph
+from notorch_amd.data.synth import make_batch
+
+
+def _same(a, b):
+    assert len(a) == len(b)
+    for x, y in zip(a.tensors(), b.tensors()):
+        assert x.dtype == y.dtype and torch.equal(x, y)
+    la, lb = a._nt_layout, b._nt_layout
+    assert la.deg_range == lb.deg_range and la.mol_max == lb.mol_max and la.type_range == lb.type_range
+    assert la.plan[1] == lb.plan[1] and la.plan[3] == lb.plan[3]
+
+
+def test_collator_in_workers_matches_main_process():
+    graphs = make_batch("qm9", 96, seed=3).to_graphs()
+    coll = GraphCollator("nodes")
+    pickle.loads(pickle.dumps(coll))
+    dl = torch.utils.data.DataLoader(graphs, batch_size=32, collate_fn=coll, num_workers=2)
+    got = list(dl)
+    assert len(got) == 3
+    for i, G in enumerate(got):
+        _same(G, BatchedGraph.from_graphs(graphs[32 * i:32 * (i + 1)], "nodes"))
+        # the statistics still describe the unpickled tensors (no re-validation needed)
+        assert G._layout_types_ok()
+
+
+def test_graph_tensors_cover_layout():
+    G = BatchedGraph.from_graphs(make_batch("qm9", 8, seed=1).to_graphs())
+    ts = G.tensors()
+    lay = G._nt_layout
+    for t in (lay.dst_ptr, lay.dst_perm, lay.mol_ptr, lay.plan[0], lay.plan[2], G.batch_edge_index):
+        assert any(t is u for u in ts)

@@ -53,3 +53,62 @@ def test_gloo_world2_sharding_and_aggregation():
     assert a0 == 0 and b0 == a1 and b1 == 64
     assert t0 == t1 == 3 * (e0 + e1)      # SUM of units
     assert s0 == s1 == 2.0                # MAX of times
+
+
+def _pipeline_worker(rank, world, port, out):
+    """One rank of a molecule-sharded forward: shard -> collate (fixed rev mode) -> .to(device) ->
+    embedding + D-MPNN block + Sum readout (the oracle restatement stands in for the device kernels:
+    there is no GPU here) -> readouts gathered to rank 0 (bookkeeping only, after the forward)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from notorch_amd.data.synth import make_batch
+    from oracle import dmpnn_ref
+
+    batch = make_batch("qm9", 48, seed=7)
+    a, b = edge_balanced_ranges(2 * batch.n_bonds, world)[rank]
+    G = batch.subset(a, b).collate("edges").to("cpu")
+    torch.manual_seed(0)
+    h = 32
+    emb_v, emb_e = torch.nn.EmbeddingBag(42, h, mode="sum"), torch.nn.EmbeddingBag(13, h, mode="sum")
+    blk_W = [torch.randn(h, h) / 6 for _ in range(3)]
+    blk_b = [torch.randn(h) * 0.1 for _ in range(3)]
+    with torch.no_grad():
+        Xv, Xe = emb_v(G.node_feats), emb_e(G.edge_feats)
+        node, _ = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, blk_W, blk_b)
+        r = dmpnn_ref.readout(node, G.batch_node_index, len(G), "sum")
+    sizes = [None] * world
+    dist.all_gather_object(sizes, (a, b, G.num_nodes, G.num_edges))
+    parts = [torch.zeros(sb - sa, h) for sa, sb, _, _ in sizes]
+    dist.all_gather(parts, r)
+    if rank == 0:
+        out["parts"] = torch.cat(parts).numpy()
+        out["sizes"] = sizes
+    dist.destroy_process_group()
+
+
+def test_gloo_world2_sharded_forward_pipeline():
+    """The N>1 path end to end on CPU (gloo, world 2): every rank runs its edge-balanced shard's
+    forward independently; the gathered readouts equal the whole batch's forward (fixed rev mode:
+    molecules are independent units), and the shards' collated sizes add up."""
+    from notorch_amd.data.synth import make_batch
+    from oracle import dmpnn_ref
+
+    mgr = mp.Manager()
+    out = mgr.dict()
+    port = 29600 + os.getpid() % 1000
+    mp.spawn(_pipeline_worker, args=(2, port, out), nprocs=2, join=True)
+    batch = make_batch("qm9", 48, seed=7)
+    G = batch.collate("edges")
+    torch.manual_seed(0)
+    h = 32
+    emb_v, emb_e = torch.nn.EmbeddingBag(42, h, mode="sum"), torch.nn.EmbeddingBag(13, h, mode="sum")
+    blk_W = [torch.randn(h, h) / 6 for _ in range(3)]
+    blk_b = [torch.randn(h) * 0.1 for _ in range(3)]
+    with torch.no_grad():
+        Xv, Xe = emb_v(G.node_feats), emb_e(G.edge_feats)
+        node, _ = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, blk_W, blk_b)
+        ref = dmpnn_ref.readout(node, G.batch_node_index, len(G), "sum").numpy()
+    sizes = out["sizes"]
+    assert sizes[0][0] == 0 and sizes[0][1] == sizes[1][0] and sizes[1][1] == 48
+    assert sizes[0][2] + sizes[1][2] == G.num_nodes and sizes[0][3] + sizes[1][3] == G.num_edges
+    np.testing.assert_allclose(out["parts"], ref, rtol=1e-5, atol=1e-5)
