@@ -282,6 +282,14 @@ NT_API int nt_gather_rows(const void* base, const void* X, const int64_t* idx, c
 NT_API int nt_dropout_residual(const void* base, const void* Y, int64_t n, float p, uint64_t seed,
                                uint64_t offset, int dtype, void* out, void* stream);
 
+/* Dense layer GEMM, the backward's dA = G W of nn.Linear (chemprop.py:26,41), trained through
+ * lightning_models/model.py:224-241 (the reference runs it as ATen addmm's autograd):
+ *   out[i] = X[i] W^T,  i < M,   Wp = nt_dmpnn_pack_weight image of W (h x h; pass the image of W^T
+ * for dA = G W).  The persistent bf16x6 MFMA layer kernel without gathers (fp32-accurate).
+ * fp32 only; h % 4 == 0, h <= 304; 16-byte aligned; out != X. */
+NT_API int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const void* Wp, int dtype,
+                                 void* out, void* stream);
+
 /* Device status word of the calling device (no reference counterpart: the reference's ops cannot
  * hang).  The persistent fp32 update kernel hands work between its waves through bounded LDS waits;
  * a wait that gives up sets this word (sticky) and the launch's outputs are invalid.

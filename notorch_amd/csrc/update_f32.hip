@@ -664,3 +664,24 @@ extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t
   return launch_update_ps(a, tile_ptr, ntiles, perm, dst_sorted, reduce, agg_act, agg_alpha,
                           (float*)S_out);
 }
+
+// out = X W^T (the layer GEMM alone: no gathers, no residual, no bias) on the persistent bf16x6
+// MFMA kernel in its dense mode (row e of A is X[e]); the backward's dA = G W passes the packed
+// image of W^T.
+extern "C" int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const void* Wp, int dtype,
+                                     void* out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul: fp32 only");
+  NT_REQUIRE(M >= 0 && M < (int64_t(1) << 31) && h > 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(ps_supported(h), NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul needs h % 4 == 0 and h <= 304");
+  if (M == 0) return NT_OK;
+  NT_REQUIRE(X && Wp && out, NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(X != out, NT_EINVAL, "out aliases X");
+  NT_REQUIRE(aligned16(X) && aligned16(out) && aligned16(Wp), NT_EINVAL, "pointers must be 16-byte aligned");
+  const UpdateGeom g = geom_for(h);
+  UpdateArgs a{(const float*)X, (const float*)X, nullptr, nullptr,
+               (const char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), nullptr, M, M, h,
+               g.KB, g.NT, 0, NT_ACT_IDENTITY, 0.f, (float*)out, as_stream(stream_)};
+  return launch_update_pk(a, nullptr, 0, nullptr, nullptr, NT_SUM, NT_ACT_IDENTITY, 0.f, nullptr);
+}

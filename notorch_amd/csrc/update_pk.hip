@@ -166,7 +166,8 @@ __device__ __forceinline__ int row_edge(const Args& a, int t, int row) {
 __device__ __forceinline__ RowSrc row_src(const Args& a, int e) {
   RowSrc rs{-1, -1};
   if (e >= 0) {
-    const int64_t s = a.src[e], q = a.rev[e];
+    // dense mode (nt_dmpnn_dense_matmul): no src -> row e itself, no rev -> nothing subtracted
+    const int64_t s = a.src ? a.src[e] : e, q = a.rev ? a.rev[e] : -1;
     rs.soff = (s >= 0 && s < a.V) ? (int)s * a.hv : -1;
     rs.qoff = (q >= 0 && q < a.E) ? (int)q * a.hv : -1;
   }
@@ -707,6 +708,8 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
     return dispatch_pk<NT_ACT_RELU, NT_ACT_RELU, true>(a, KS, grid, u.stream, Seq{});
   if (relu && sum && aact == NT_ACT_IDENTITY)
     return dispatch_pk<NT_ACT_RELU, NT_ACT_IDENTITY, true>(a, KS, grid, u.stream, Seq{});
+  if (u.act == NT_ACT_IDENTITY && !fused)  // dense mode (the backward's dA) and identity layers
+    return dispatch_pk<NT_ACT_IDENTITY, NT_ACT_IDENTITY, true>(a, KS, grid, u.stream, Seq{});
   return dispatch_pk<-1, -1, false>(a, KS, grid, u.stream, Seq{});
 }
 

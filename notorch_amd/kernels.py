@@ -32,6 +32,7 @@ __all__ = [
     "dmpnn_init_embed",
     "node_scores",
     "softmax_pool",
+    "dense_matmul",
     "watch_device_status",
     "check_device_status",
     "reset_device_status",
@@ -423,6 +424,20 @@ def dmpnn_update_fused(
          act[0], act[1], _ptr(tile_ptr), ntiles, _ptr(perm), _ptr(dsts), reduce_code(reduce),
          agg_act[0], agg_act[1], code, _ptr(out), _ptr(S_out), _stream(dev))
     return out, S_out
+
+
+def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None) -> Tensor:
+    """X @ W^T for the packed image Wp of W (fp32, h % 4 == 0, h <= 304): the layer GEMM alone on
+    the bf16x6 MFMA kernel.  With Wp = pack_weights(W.t()) it is the backward's dA = G @ W."""
+    dev = _require_device(X, Wp, out)
+    _require_f32("X", X)
+    M, h = X.shape
+    if Wp.numel() != packed_weight_numel(h, X.dtype):
+        raise ValueError("Wp is not a packed fp32 weight image for this hidden size")
+    if out is None:
+        out = torch.empty_like(X)
+    _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_F32, _ptr(out), _stream(dev))
+    return out
 
 
 # ------------------------------------------------------------------------------------ backward

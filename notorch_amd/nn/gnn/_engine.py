@@ -545,7 +545,10 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
         dWs[l] = _weight_grad(Gu, A)
         dbs[l] = Gu.sum(0)
         del A
-        dA = torch.mm(Gu, W)
+        if Gu.dtype == torch.float32 and K.fused_supported(V, E, h, Gu.dtype):
+            dA = K.dense_matmul(Gu.contiguous(), K.pack_weights(W.t().contiguous()))  # bf16x6 MFMA
+        else:
+            dA = torch.mm(Gu, W)
         del Gu
         dS = K.segment_reduce(dA, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY)
         G = K.dmpnn_edge_backward(G, H_l, dA, dS, dst, rev_ptr, rev_perm, lay.dst_ptr,

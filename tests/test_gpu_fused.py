@@ -364,3 +364,15 @@ def test_xcd_walk_branches(dtype, case):
     tol = FP32_NORM_TOL if dtype == torch.float32 else 2e-2
     assert_parity(Hn.float(), rH, tol, f"{case} H ntiles={ntiles}")
     assert_parity(Sn.float(), rS, tol, f"{case} S ntiles={ntiles}")
+
+
+@pytest.mark.parametrize("h,M", [(300, 77_000), (300, 1), (100, 1000), (64, 4097), (4, 3)])
+def test_dense_matmul_x6(h, M):
+    """nt_dmpnn_dense_matmul (the backward's dA = G W, chemprop.py:41 under autograd): the
+    persistent kernel's dense mode against fp64, fp32 contract."""
+    K = _K()
+    g = torch.Generator().manual_seed(M + h)
+    X, W = torch.randn(M, h, generator=g), torch.randn(h, h, generator=g) / h ** 0.5
+    out = K.dense_matmul(X.to(DEV), K.pack_weights(W.t().contiguous().to(DEV)))
+    ref = X.double() @ W.double()
+    assert_parity(out, ref, FP32_NORM_TOL, f"dense h={h} M={M}")
