@@ -282,6 +282,26 @@ NT_API int nt_gather_rows(const void* base, const void* X, const int64_t* idx, c
 NT_API int nt_dropout_residual(const void* base, const void* Y, int64_t n, float p, uint64_t seed,
                                uint64_t offset, int dtype, void* out, void* stream);
 
+/* Backward of the max / min scatters (torch_scatter scatter_max / scatter_min at chemprop.py:39,86
+ * and agg.py:45; trained through lightning_models/model.py:224-241): the gradient of an output
+ * element goes to its arg, the FIRST row of the segment (ascending CSR order) holding the extreme.
+ *   nt_segment_arg:             arg[v][c] = that row of act(X) over segment v (seg_ptr / perm as
+ *                               nt_segment_reduce), -1 for an empty segment; reduce = NT_MAX | NT_MIN
+ *   nt_dmpnn_edge_backward_arg: nt_dmpnn_edge_backward with the dS term masked by arg (reduce of the
+ *                               layer's aggregation = max | min): (arg[dst e][c] == e ? dS[dst e][c] : 0)
+ *   nt_gather_rows_arg:         out[i] = (base ? base[i] : 0) + (arg[idx i] == i ? X[idx i] : 0)
+ * fp32 only. */
+NT_API int nt_segment_arg(const void* X, const int32_t* seg_ptr, const int32_t* perm, int64_t nseg,
+                          int64_t h, int reduce, int act, float act_alpha, int dtype, int32_t* arg,
+                          void* stream);
+NT_API int nt_dmpnn_edge_backward_arg(const void* G, const void* H, const void* dA, const void* dS,
+                                      const int32_t* arg, const int64_t* dst, const int32_t* rev_ptr,
+                                      const int32_t* rev_perm, int64_t V, int64_t E, int64_t h,
+                                      int residual, int act, float act_alpha, int dtype, void* G_out,
+                                      void* stream);
+NT_API int nt_gather_rows_arg(const void* base, const void* X, const int64_t* idx, const int32_t* arg,
+                              int64_t n, int64_t h, int dtype, void* out, void* stream);
+
 /* Dense layer GEMM, the backward's dA = G W of nn.Linear (chemprop.py:26,41), trained through
  * lightning_models/model.py:224-241 (the reference runs it as ATen addmm's autograd):
  *   out[i] = X[i] W^T,  i < M,   Wp = nt_dmpnn_pack_weight image of W (h x h; pass the image of W^T

@@ -99,6 +99,13 @@ SIGNATURES: dict[str, tuple] = {
     "nt_gather_rows": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp]),
     "nt_dropout_residual": (_c_int, [_vp, _vp, _c_i64, ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64,
                                      _c_int, _vp, _vp]),
+    "nt_segment_arg": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp]),
+    "nt_dmpnn_edge_backward_arg": (
+        _c_int,
+        [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp,
+         _vp],
+    ),
+    "nt_gather_rows_arg": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_int, _vp, _vp]),
     "nt_dmpnn_dense_matmul": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, _vp]),
     "nt_device_status": (_c_int, [_vp, _vp]),
     "nt_device_status_reset": (_c_int, [_vp]),

@@ -135,6 +135,80 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const T* __restrict__ 
   }
 }
 
+// ------------------------------------------------------------------------------ max / min
+// torch_scatter's scatter_max / scatter_min (chemprop.py:39,86; agg.py:45) send the whole gradient
+// of an output element to its arg: the FIRST row of the segment, in the CSR's ascending-row order,
+// whose value is the extreme (CPU reducer: strict > / <).  Empty segments have no arg (-1).
+template <int ACT, bool MAXR>
+__global__ void __launch_bounds__(256) segment_arg_kernel(const float* __restrict__ X,
+                                                          const int32_t* __restrict__ seg_ptr,
+                                                          const int32_t* __restrict__ perm,
+                                                          int64_t nseg, int64_t h, int act, float alpha,
+                                                          int32_t* __restrict__ arg) {
+  const int64_t total = nseg * h;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = t / h, c = t - v * h;
+    const int32_t b = seg_ptr[v], en = seg_ptr[v + 1];
+    int32_t best_r = -1;
+    float best = 0.f;
+    for (int32_t j = b; j < en; ++j) {
+      const int32_t r = perm ? perm[j] : j;
+      const float x = act_t<ACT>(X[(int64_t)r * h + c], act, alpha);
+      if (best_r < 0 || (MAXR ? x > best : x < best)) {
+        best = x;
+        best_r = r;
+      }
+    }
+    arg[t] = best_r;
+  }
+}
+
+__device__ __forceinline__ float4 arg_mask(float4 x, int4 a, int64_t e) {
+  return make_float4(a.x == e ? x.x : 0.f, a.y == e ? x.y : 0.f, a.z == e ? x.z : 0.f, a.w == e ? x.w : 0.f);
+}
+__device__ __forceinline__ float arg_mask(float x, int a, int64_t e) { return a == e ? x : 0.f; }
+
+// edge backward with the dS term routed through the arg: dS[dst e] reaches row e only where e is
+// the arg of (dst e, column)
+template <typename T, typename TI, int ACT>
+__global__ void __launch_bounds__(256) edge_backward_arg_kernel(
+    const T* __restrict__ G, const T* __restrict__ H, const T* __restrict__ dA,
+    const T* __restrict__ dS, const TI* __restrict__ arg, const int64_t* __restrict__ dst,
+    const int32_t* __restrict__ rev_ptr, const int32_t* __restrict__ rev_perm, int64_t E, int64_t hw,
+    int residual, int act, float alpha, T* __restrict__ Gout) {
+  const int64_t total = E * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / hw, c = t - e * hw;
+    const int64_t v = dst[e];
+    T dm = arg_mask(dS[v * hw + c], arg[v * hw + c], e);
+    const int32_t b = rev_ptr[e], en = rev_ptr[e + 1];
+    for (int32_t j = b; j < en; ++j) dm = dm - dA[(int64_t)rev_perm[j] * hw + c];
+    T g = vmul(vgrad<ACT>(H[t], act, alpha), dm);
+    if (residual) g = g + G[t];
+    Gout[t] = g;
+  }
+}
+
+// out[i] = (base ? base[i] : 0) + (arg[idx i] == i ? X[idx i] : 0): backward of a max/min scatter
+// of rows i into segments idx i (the final node scatter, the Max / Min readout)
+template <typename T, typename TI>
+__global__ void __launch_bounds__(256) gather_rows_arg_kernel(const T* __restrict__ base,
+                                                              const T* __restrict__ X,
+                                                              const int64_t* __restrict__ idx,
+                                                              const TI* __restrict__ arg, int64_t n,
+                                                              int64_t hw, T* __restrict__ out) {
+  const int64_t total = n * hw;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / hw, c = t - i * hw;
+    const int64_t s = idx[i];
+    const T x = arg_mask(X[s * hw + c], arg[s * hw + c], i);
+    out[t] = base ? base[t] + x : x;
+  }
+}
+
 // ---- bf16 storage (bf16 training): same math in fp32 registers, one rounding per stored element ----
 template <bool VEC, int ACT>
 __global__ void __launch_bounds__(256) message_bf16(const bf16_raw* __restrict__ H,
@@ -377,6 +451,82 @@ extern "C" int nt_gather_rows(const void* base, const void* X, const int64_t* id
     else
       gather_rows_kernel<float, false><<<grid, 256, 0, stream>>>(
           (const float*)base, (const float*)X, idx, seg_ptr, n, h, (float*)out);
+  }
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+extern "C" int nt_segment_arg(const void* X, const int32_t* seg_ptr, const int32_t* perm, int64_t nseg,
+                              int64_t h, int reduce, int act, float act_alpha, int dtype, int32_t* arg,
+                              void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_segment_arg: fp32 only");
+  NT_REQUIRE(reduce == NT_MAX || reduce == NT_MIN, NT_EINVAL, "nt_segment_arg: reduce must be max or min");
+  NT_REQUIRE(valid_act(act), NT_EINVAL, "bad act code");
+  NT_REQUIRE(nseg >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  if (nseg == 0) return NT_OK;
+  NT_REQUIRE(X && seg_ptr && arg, NT_EINVAL, "NULL pointer");
+  hipStream_t stream = as_stream(stream_);
+  const int grid = grid_for(nseg * h, 256, 256 * 32);
+#define NT_SA(MAXR_)                                                                          \
+  NT_BW_DISPATCH_ACT(act, (segment_arg_kernel<A_, MAXR_><<<grid, 256, 0, stream>>>(           \
+                              (const float*)X, seg_ptr, perm, nseg, h, act, act_alpha, arg)))
+  if (reduce == NT_MAX) NT_SA(true); else NT_SA(false);
+#undef NT_SA
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+extern "C" int nt_dmpnn_edge_backward_arg(const void* G, const void* H, const void* dA, const void* dS,
+                                          const int32_t* arg, const int64_t* dst,
+                                          const int32_t* rev_ptr, const int32_t* rev_perm, int64_t V,
+                                          int64_t E, int64_t h, int residual, int act, float act_alpha,
+                                          int dtype, void* G_out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_edge_backward_arg: fp32 only");
+  NT_REQUIRE(valid_act(act), NT_EINVAL, "bad act code");
+  NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  if (E == 0) return NT_OK;
+  NT_REQUIRE(H && dA && dS && arg && dst && rev_ptr && rev_perm && G_out, NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(!residual || G, NT_EINVAL, "residual needs G");
+  hipStream_t stream = as_stream(stream_);
+  if (h % 4 == 0 && aligned16(H) && aligned16(dA) && aligned16(dS) && aligned16(G_out) &&
+      aligned16(arg) && (!residual || aligned16(G))) {
+    const int64_t hw = h / 4;
+    const int grid = grid_for(E * hw, 256, 256 * 32);
+    NT_BW_DISPATCH_ACT(act, (edge_backward_arg_kernel<float4, int4, A_><<<grid, 256, 0, stream>>>(
+                                (const float4*)G, (const float4*)H, (const float4*)dA, (const float4*)dS,
+                                (const int4*)arg, dst, rev_ptr, rev_perm, E, hw, residual, act,
+                                act_alpha, (float4*)G_out)));
+  } else {
+    const int grid = grid_for(E * h, 256, 256 * 32);
+    NT_BW_DISPATCH_ACT(act, (edge_backward_arg_kernel<float, int, A_><<<grid, 256, 0, stream>>>(
+                                (const float*)G, (const float*)H, (const float*)dA, (const float*)dS,
+                                arg, dst, rev_ptr, rev_perm, E, h, residual, act, act_alpha,
+                                (float*)G_out)));
+  }
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+extern "C" int nt_gather_rows_arg(const void* base, const void* X, const int64_t* idx, const int32_t* arg,
+                                  int64_t n, int64_t h, int dtype, void* out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_gather_rows_arg: fp32 only");
+  NT_REQUIRE(n >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  if (n == 0) return NT_OK;
+  NT_REQUIRE(X && idx && arg && out, NT_EINVAL, "NULL pointer");
+  hipStream_t stream = as_stream(stream_);
+  if (h % 4 == 0 && aligned16(X) && aligned16(out) && aligned16(arg) && (!base || aligned16(base))) {
+    const int64_t hw = h / 4;
+    gather_rows_arg_kernel<float4, int4><<<grid_for(n * hw, 256, 256 * 32), 256, 0, stream>>>(
+        (const float4*)base, (const float4*)X, idx, (const int4*)arg, n, hw, (float4*)out);
+  } else {
+    gather_rows_arg_kernel<float, int><<<grid_for(n * h, 256, 256 * 32), 256, 0, stream>>>(
+        (const float*)base, (const float*)X, idx, arg, n, h, (float*)out);
   }
   NT_LAUNCH_CHECK();
   return NT_OK;

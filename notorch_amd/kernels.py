@@ -33,6 +33,9 @@ __all__ = [
     "node_scores",
     "softmax_pool",
     "dense_matmul",
+    "segment_arg",
+    "dmpnn_edge_backward_arg",
+    "gather_rows_arg",
     "watch_device_status",
     "check_device_status",
     "reset_device_status",
@@ -437,6 +440,48 @@ def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None) -> Tensor:
     if out is None:
         out = torch.empty_like(X)
     _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_F32, _ptr(out), _stream(dev))
+    return out
+
+
+def segment_arg(X: Tensor, seg_ptr: Tensor, perm: Tensor | None, nseg: int, reduce: str, *,
+                act: tuple[int, float] = (_lib.NT_ACT_IDENTITY, 0.0)) -> Tensor:
+    """int32 (nseg x h): the first row (ascending CSR order) of each segment holding the max / min
+    of act(X) per column, -1 for empty segments (torch_scatter scatter_max / scatter_min's arg)."""
+    dev = _require_device(X, seg_ptr, perm)
+    _require_f32("X", X)
+    if reduce not in ("max", "min"):
+        raise ValueError("segment_arg: reduce must be 'max' or 'min'")
+    h = X.shape[1]
+    arg = torch.empty(nseg, h, dtype=torch.int32, device=dev)
+    _run(dev, _lib.load().nt_segment_arg, _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce),
+         act[0], act[1], NT_F32, _ptr(arg), _stream(dev))
+    return arg
+
+
+def dmpnn_edge_backward_arg(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor, arg: Tensor, dst: Tensor,
+                            rev_ptr: Tensor, rev_perm: Tensor, *, residual: bool = True,
+                            act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0)) -> Tensor:
+    """dL/dH_l for a max / min aggregation (arg = segment_arg of act(H_l) over the dst CSR)."""
+    dev = _require_device(G, H, dA, dS, arg, dst, rev_ptr, rev_perm)
+    for n_, t in (("H", H), ("dA", dA), ("dS", dS)):
+        _require_f32(n_, t)
+    E, h = H.shape
+    V = dS.shape[0]
+    out = torch.empty_like(H)
+    _run(dev, _lib.load().nt_dmpnn_edge_backward_arg, _ptr(G), _ptr(H), _ptr(dA), _ptr(dS), _ptr(arg),
+         _ptr(dst), _ptr(rev_ptr), _ptr(rev_perm), V, E, h, int(residual), act[0], act[1], NT_F32,
+         _ptr(out), _stream(dev))
+    return out
+
+
+def gather_rows_arg(X: Tensor, idx: Tensor, arg: Tensor, *, base: Tensor | None = None) -> Tensor:
+    """out[i] = base[i] + (arg[idx i] == i ? X[idx i] : 0) (max / min scatter backward)."""
+    dev = _require_device(X, idx, arg, base)
+    _require_f32("X", X)
+    n, h = idx.numel(), X.shape[1]
+    out = torch.empty(n, h, dtype=X.dtype, device=dev)
+    _run(dev, _lib.load().nt_gather_rows_arg, _ptr(base), _ptr(X), _ptr(idx), _ptr(arg), n, h, NT_F32,
+         _ptr(out), _stream(dev))
     return out
 
 

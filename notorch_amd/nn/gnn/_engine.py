@@ -521,9 +521,12 @@ def _weight_grad(G: Tensor, A: Tensor) -> Tensor:
 
 
 def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, residual, V, need_x,
-                   drop=None):
-    """Kernel backward of block_forward for reduce in {sum, mean} (see csrc/backward.hip).
+                   drop=None, H_last=None):
+    """Kernel backward of block_forward (see csrc/backward.hip).  reduce in {sum, mean}; fp32 also
+    max / min, whose aggregations send each gradient element to its arg (torch_scatter's scatter_max
+    / scatter_min): H_last = the forward's H_d, for the final node scatter's arg.
     Returns (dXv, dXe, [dW_l], [db_l])."""
+    maxmin = reduce in ("max", "min")
     E, h = states[0][0].shape if states else dH.shape
     src_ptr, src_perm, rev_ptr, rev_perm = backward_layout(lay, src, rev, V, E)
     mean_ptr = lay.dst_ptr if reduce == "mean" else None
@@ -532,7 +535,11 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
     else:
         G = dH.contiguous()
     if dnode is not None:
-        G = K.gather_rows(dnode.contiguous(), dst, base=G, seg_ptr=mean_ptr)
+        if maxmin:  # chemprop.py:86 with scatter_max / scatter_min
+            arg = K.segment_arg(H_last, lay.dst_ptr, lay.dst_perm, V, reduce)
+            G = K.gather_rows_arg(dnode.contiguous(), dst, arg, base=G)
+        else:
+            G = K.gather_rows(dnode.contiguous(), dst, base=G, seg_ptr=mean_ptr)
     d = len(weights)
     dWs: list = [None] * d
     dbs: list = [None] * d
@@ -551,8 +558,13 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             dA = torch.mm(Gu, W)
         del Gu
         dS = K.segment_reduce(dA, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY)
-        G = K.dmpnn_edge_backward(G, H_l, dA, dS, dst, rev_ptr, rev_perm, lay.dst_ptr,
-                                  residual=residual, act=act, reduce=reduce)
+        if maxmin:  # chemprop.py:39 with scatter_max / scatter_min: the arg of act(H_l) per node
+            arg = K.segment_arg(H_l, lay.dst_ptr, lay.dst_perm, V, reduce, act=act)
+            G = K.dmpnn_edge_backward_arg(G, H_l, dA, dS, arg, dst, rev_ptr, rev_perm,
+                                          residual=residual, act=act)
+        else:
+            G = K.dmpnn_edge_backward(G, H_l, dA, dS, dst, rev_ptr, rev_perm, lay.dst_ptr,
+                                      residual=residual, act=act, reduce=reduce)
     dXv = K.segment_reduce(G, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY) if need_x[0] else None
     return dXv, G if need_x[1] else None, dWs, dbs
 
@@ -566,11 +578,14 @@ class ChempropBlockFunction(torch.autograd.Function):
         weights = list(params[:nlayers])
         biases = list(params[nlayers:])
         src = edge_index[0].contiguous()
-        kernel_bwd = (reduce in ("sum", "mean") and Xv.dtype in (torch.float32, torch.bfloat16)
+        kernel_bwd = ((reduce in ("sum", "mean") and Xv.dtype in (torch.float32, torch.bfloat16)
+                       or reduce in ("max", "min") and Xv.dtype == torch.float32)
                       and os.environ.get("NT_BWD", "kernel") != "torch")
         node, H, states = block_forward(Xv, Xe, src, rev, lay, weights, biases, act, reduce, residual,
                                         keep_states=kernel_bwd, drop=drop)
         flat = [t for hs in states for t in hs]
+        if kernel_bwd and reduce in ("max", "min"):
+            flat.append(H)  # the final node scatter's arg is taken over H_d
         ctx.save_for_backward(Xv, Xe, edge_index, rev,
                               *[p if p is not None else torch.empty(0) for p in params], *flat)
         ctx.cfg = (act_mod, act, reduce, residual, nlayers, [p is None for p in params], lay, kernel_bwd, drop)
@@ -586,11 +601,12 @@ class ChempropBlockFunction(torch.autograd.Function):
         if kernel_bwd:
             flat = rest[nparams:]
             states = [(flat[2 * i], flat[2 * i + 1]) for i in range(nlayers)]
+            H_last = flat[2 * nlayers] if reduce in ("max", "min") else None
             src = edge_index[0].contiguous()
             dst = edge_index[1].contiguous()
             dXv, dXe, dWs, dbs = block_backward(
                 dnode, dH, states, params[:nlayers], src, dst, rev, lay, act, reduce, residual,
-                Xv.shape[0], (need[0], need[1]), drop,
+                Xv.shape[0], (need[0], need[1]), drop, H_last,
             )
             res_params = [dW if need[11 + i] else None for i, dW in enumerate(dWs)]
             res_params += [None if p is None or not need[11 + nlayers + i] else dbs[i]
@@ -649,6 +665,7 @@ class ReadoutFunction(torch.autograd.Function):
     def forward(ctx, X, mol_ptr, mol_perm, B, reduce, batch_node_index, chunks=None):
         ctx.save_for_backward(X, batch_node_index)
         ctx.cfg = (B, reduce, mol_ptr)
+        ctx.mol_perm = mol_perm
         return _aggregate(X, mol_ptr, mol_perm, B, reduce, _IDENTITY, chunks)
 
     @staticmethod
@@ -658,6 +675,12 @@ class ReadoutFunction(torch.autograd.Function):
         if reduce in ("sum", "mean") and dout.dtype in (torch.float32, torch.bfloat16):
             # dX[v] = dout[batch v] (/ count for mean): one gather kernel
             dX = K.gather_rows(dout.contiguous(), bni, seg_ptr=mol_ptr if reduce == "mean" else None)
+            return dX, None, None, None, None, None, None
+        if reduce in ("max", "min") and dout.dtype == torch.float32:
+            # agg.py:45 scatter_max: dX[v] = dout[batch v] where v is the molecule's arg
+            mol_perm = ctx.mol_perm
+            arg = K.segment_arg(X.contiguous(), mol_ptr, mol_perm, B, reduce)
+            dX = K.gather_rows_arg(dout.contiguous(), bni, arg)
             return dX, None, None, None, None, None, None
         with torch.enable_grad():
             X_ = X.detach().requires_grad_(True)

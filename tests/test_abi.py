@@ -24,7 +24,7 @@ def test_header_declares_the_boundary():
         "nt_dmpnn_update_fused", "nt_dmpnn_message", "nt_dmpnn_edge_backward", "nt_gather_rows",
         "nt_embed_bag", "nt_dmpnn_init_embed", "nt_node_scores", "nt_softmax_pool",
         "nt_collate_graphs", "nt_segment_reduce_chunked", "nt_device_status", "nt_device_status_reset",
-        "nt_dmpnn_dense_matmul",
+        "nt_dmpnn_dense_matmul", "nt_segment_arg", "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg",
     }
 
 

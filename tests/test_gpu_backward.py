@@ -53,13 +53,13 @@ def _oracle_grads(G, Xv, Xe, blk, act_fn, residual, reduce, readout, dtype):
 
 
 def _device_grads(G, Xv, Xe, blk, readout):
-    from notorch_amd.nn import Mean, Sum
+    from notorch_amd.nn import Max, Mean, Min, Sum
 
     blk = blk.to(DEV).train()
     Xv_d = Xv.to(DEV).requires_grad_(True)
     Xe_d = Xe.to(DEV).requires_grad_(True)
     out = blk(G.update(node_feats=Xv_d, edge_feats=Xe_d).to(DEV))
-    ro = {"sum": Sum, "mean": Mean}[readout]()(out)
+    ro = {"sum": Sum, "mean": Mean, "max": Max, "min": Min}[readout]()(out)
     e = out.edge_feats
     loss = ro.pow(2).sum() + (e * torch.linspace(-1, 1, e.shape[1], device=DEV)).sum()
     loss.backward()
@@ -225,9 +225,40 @@ def test_block_grads_config2_fp32(act):
         assert_parity(a, b, max(2e-5, 2 * norm_err(c, b)), name)
 
 
-def test_max_reduce_takes_recompute_backward():
-    """max/min have no kernel backward: the torch-device recompute path must still be exact."""
+@pytest.mark.parametrize("reduce,readout,act", [("max", "sum", "SiLU"), ("min", "max", "Tanh"),
+                                                ("max", "min", "Identity"), ("max", "max", "ReLU")])
+def test_max_min_kernel_backward(reduce, readout, act, monkeypatch):
+    """fp32 max / min aggregations and Max / Min readouts train through the arg kernels
+    (nt_segment_arg + nt_dmpnn_edge_backward_arg + nt_gather_rows_arg; torch_scatter's scatter_max
+    / scatter_min gradient at chemprop.py:39,86 and agg.py:45), never through the torch recompute."""
+    from notorch_amd.nn.gnn import _engine
+
+    def boom(*a, **k):
+        raise AssertionError("fp32 max/min backward must use the kernel path")
+
+    monkeypatch.setattr(_engine, "_torch_block", boom)
+    monkeypatch.setattr(_engine, "_torch_scatter", boom)
+    _check(_graph("qm9", 12, seed=12), 24, depth=2, reduce=reduce, readout=readout, act=act)
+
+
+def test_max_reduce_recompute_backward_still_exact(monkeypatch):
+    """NT_BWD=torch (the recompute path, which bf16 max / min still take) agrees with the oracle."""
+    monkeypatch.setenv("NT_BWD", "torch")
     _check(_graph("qm9", 8, seed=12), 24, depth=2, reduce="max")
+
+
+def test_segment_arg_first_occurrence():
+    """Ties go to the first row in ascending CSR order (torch_scatter's CPU reducer: strict > / <);
+    empty segments get -1."""
+    from notorch_amd import kernels as K
+
+    X = torch.tensor([[1.0, 5.0], [3.0, 5.0], [3.0, -1.0], [0.0, 2.0]], device=DEV)
+    seg_ptr = torch.tensor([0, 3, 3, 4], dtype=torch.int32, device=DEV)  # segments {0,1,2}, {}, {3}
+    perm = torch.tensor([2, 0, 1, 3], dtype=torch.int32, device=DEV)     # visiting order 2, 0, 1
+    a_max = K.segment_arg(X, seg_ptr, perm, 3, "max").cpu().tolist()
+    a_min = K.segment_arg(X, seg_ptr, perm, 3, "min").cpu().tolist()
+    assert a_max == [[2, 0], [-1, -1], [3, 3]]
+    assert a_min == [[0, 2], [-1, -1], [3, 3]]
 
 
 def test_backward_does_not_route_through_torch_block_for_sum(monkeypatch):
