@@ -81,6 +81,54 @@ __global__ void __launch_bounds__(256) init_aggregate_vec4(
   }
 }
 
+// One wave per node (the node id is wave-uniform, so the index chain seg_ptr -> perm -> src runs on
+// scalar loads once per wave instead of once per 16-B piece): lanes take the node's row pieces
+// (p = lane + 64 k), the in-edges go 4 at a time with all their row loads in flight.  Same order of
+// operations as init_aggregate_vec4, so the same bits.
+template <int R, int ACT>
+__global__ void __launch_bounds__(256) init_aggregate_wave(
+    const float4* __restrict__ Xv, const float4* __restrict__ Xe, const int64_t* __restrict__ src,
+    const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm, int64_t V, int64_t hv,
+    int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t v = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+       v < V; v += nwaves) {
+    const int32_t b = seg_ptr[v], en = seg_ptr[v + 1];
+    for (int64_t c = lane; c < hv; c += 64) {
+      Reducer4<R> r;
+      r.init();
+      int32_t j = b;
+      for (; j + 4 <= en; j += 4) {
+        int64_t ed[4], sv[4];
+        float4 a[4], x[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ed[u] = perm[j + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) sv[u] = src[ed[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          a[u] = Xv[sv[u] * hv + c];
+          x[u] = Xe[ed[u] * hv + c];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const float4 h0 = a[u] + x[u];
+          H0[ed[u] * hv + c] = h0;
+          r.push(act4_t<ACT>(h0, act, alpha));
+        }
+      }
+      for (; j < en; ++j) {
+        const int64_t ed = perm[j];
+        const float4 h0 = Xv[src[ed] * hv + c] + Xe[ed * hv + c];
+        H0[ed * hv + c] = h0;
+        r.push(act4_t<ACT>(h0, act, alpha));
+      }
+      S[v * hv + c] = r.result();
+    }
+  }
+}
+
 template <int R, int ACT>
 __global__ void __launch_bounds__(256) init_aggregate_scalar(
     const float* __restrict__ Xv, const float* __restrict__ Xe, const int64_t* __restrict__ src,
@@ -199,11 +247,19 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
     NT_REQUIRE(E == 0 || (Xv && Xe && src && H0), NT_EINVAL, "NULL pointer");
     if (vec) {
       const int64_t hv = h / 4;
-      const int grid = grid_for(V * hv, 256, 256 * 32);
-      NT_DISPATCH_RA(reduce, act,
-                     (init_aggregate_vec4<R_, A_><<<grid, 256, 0, stream>>>(
-                         (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
-                         act_alpha, (float4*)H0, (float4*)S)));
+      if (hv >= 32) {  // rows of >= 32 pieces: a wave per node
+        const int grid = grid_for(V * 64, 256, 256 * 32);
+        NT_DISPATCH_RA(reduce, act,
+                       (init_aggregate_wave<R_, A_><<<grid, 256, 0, stream>>>(
+                           (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
+                           act_alpha, (float4*)H0, (float4*)S)));
+      } else {
+        const int grid = grid_for(V * hv, 256, 256 * 32);
+        NT_DISPATCH_RA(reduce, act,
+                       (init_aggregate_vec4<R_, A_><<<grid, 256, 0, stream>>>(
+                           (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
+                           act_alpha, (float4*)H0, (float4*)S)));
+      }
     } else {
       const int grid = grid_for(V * h, 256, 256 * 32);
       NT_DISPATCH_RA(reduce, act,

@@ -705,7 +705,8 @@ class DeviceStatusError(RuntimeError):
     """A bounded wait inside the persistent update kernel gave up: outputs are invalid."""
 
 
-_STATUS: dict = {}  # device index -> (pinned uint32[1], torch.cuda.Event)
+_STATUS: dict = {}  # device index -> [pinned uint32[1], torch.cuda.Event, forwards since the last copy]
+STATUS_EVERY = 8  # copy the (sticky) word every STATUS_EVERY forwards: ~10 us per copy on the stream
 
 
 def _status_error(dev: torch.device) -> DeviceStatusError:
@@ -723,14 +724,17 @@ def watch_device_status(dev: torch.device) -> None:
         return  # no queries / copies inside a hipGraph capture: replays are checked by check_device_status
     ent = _STATUS.get(dev.index)
     if ent is None:
-        ent = (torch.zeros(1, dtype=torch.int32).pin_memory(), torch.cuda.Event())
+        ent = [torch.zeros(1, dtype=torch.int32).pin_memory(), torch.cuda.Event(), 0]
         _STATUS[dev.index] = ent
         fresh = True
     else:
         fresh = False
-    host, ev = ent
+    host, ev, n = ent
     if not fresh and ev.query() and int(host[0]) != 0:
         raise _status_error(dev)
+    ent[2] = n + 1
+    if n % STATUS_EVERY:
+        return  # the word is sticky: a give-up is seen by the next copy, at most STATUS_EVERY forwards on
     _run(dev, _lib.load().nt_device_status, host.data_ptr(), _stream(dev))
     ev.record(torch.cuda.current_stream(dev))
 

@@ -313,10 +313,10 @@ def test_device_status_word_raises_on_next_forward():
         torch.cuda.synchronize()
         K.check_device_status()
         assert fn(ctypes.byref(cnt), 2) == 0  # simulate a give-up
-        blk(Gd)  # copies the (set) word
-        torch.cuda.synchronize()
         with pytest.raises(K.DeviceStatusError):
-            blk(Gd)
+            for _ in range(K.STATUS_EVERY + 2):  # the periodic copy picks the word up
+                blk(Gd)
+                torch.cuda.synchronize()
         with pytest.raises(K.DeviceStatusError):
             K.check_device_status()
         K.reset_device_status()
