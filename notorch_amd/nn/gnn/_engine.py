@@ -14,18 +14,23 @@ d + 1 launches (+ one nt_dmpnn_pack_weight per distinct weight, cached).  Otherw
 
     nt_dmpnn_init; for l: nt_dmpnn_update, nt_segment_reduce; nt_segment_reduce (node)   2 + 2d launches
 
-bf16 features (BASELINE config 3) run the unfused sequence on the bf16 kernels (csrc/bf16.hip).
+bf16 features (BASELINE config 3) run the same d + 1 launch sequence on the bf16 kernels
+(csrc/bf16.hip: the 64-edge-tile update fused with the next aggregation).  Activations without a
+kernel code, or layers that differ in activation / dropout, run layer by layer
+(block_forward_layerwise).
 
-Backward (training), reduce in {sum, mean}, fp32: the forward keeps (H_l, S_l) of
-every layer; per layer, last to first (csrc/backward.hip):
+Backward (training): the forward keeps (H_l, S_l) of every layer; per layer,
+last to first (csrc/backward.hip):
 
     nt_dmpnn_message        A_l = S_l[src] - act(H_l)[rev]                   (recomputed, for dW)
-    GEMM (library)          dW_l = G^T A_l,  db_l = colsum(G),  dA = G W_l
+    GEMM (library)          dW_l = G^T A_l (split-K),  db_l = colsum(G)
+    nt_dmpnn_dense_matmul   dA = G W_l                 (fp32: the bf16x6 MFMA kernel; bf16: library)
     nt_segment_reduce       dS = scatter_sum(dA, src)            (src CSR, cached on the layout)
     nt_dmpnn_edge_backward  G <- G + act'(H_l) * (dS[dst] / c - scatter_sum(dA, rev))  (rev CSR)
+      (max / min, fp32: nt_segment_arg + nt_dmpnn_edge_backward_arg: dS[dst] reaches only the arg)
 
-then dXe = G, dXv = scatter_sum(G, src).  max/min reductions and bf16 recompute the block in
-PyTorch device ops and run autograd (``_torch_block``).
+then dXe = G, dXv = scatter_sum(G, src).  bf16 max / min recompute the block in PyTorch device ops
+and run autograd (``_torch_block``).
 """
 from __future__ import annotations
 
