@@ -118,6 +118,17 @@ class DeviceLayout:
         return self.map_tensors(lambda t: t.to(device, non_blocking=True), edge_index, batch_node_index)
 
 
+def _rebaser(old: Tensor, new: Tensor):
+    """Map a contiguous view into buffer ``old`` to the same bytes of buffer ``new``."""
+    base = old.data_ptr()
+
+    def fn(t: Tensor) -> Tensor:
+        off = t.data_ptr() - base
+        return new[off:off + t.numel() * t.element_size()].view(t.dtype).view(t.shape)
+
+    return fn
+
+
 @dataclass(repr=False, eq=False)
 class Graph(UpdateMixin):
     """A single graph: ``node_feats`` V x *, ``edge_feats`` E x *, ``edge_index`` 2 x E,
@@ -148,15 +159,73 @@ class Graph(UpdateMixin):
 
     def to(self, device, non_blocking: bool = False):
         """Move in place (reference graph.py:41-43).  non_blocking: asynchronous copies from pinned
-        host memory (pin_memory()), ordered on the current stream."""
-        types_ok = self._layout_types_ok()
+        host memory (pin_memory()), ordered on the current stream.  A packed graph (pack()) moves
+        as one buffer: one copy instead of one per tensor."""
         self._device = device
-        self.node_feats = self.node_feats.to(device, non_blocking=non_blocking)
-        self.edge_feats = self.edge_feats.to(device, non_blocking=non_blocking)
-        self.edge_index = self.edge_index.to(device, non_blocking=non_blocking)
-        self.rev_index = self.rev_index.to(device, non_blocking=non_blocking)
-        self._move_layout(device, types_ok)
+        if device is None:
+            return self
+        buf = self._packed_base()
+        if buf is not None:
+            new = buf.to(device, non_blocking=non_blocking)
+            self._apply(_rebaser(buf, new), self)
+            self._nt_packed = new
+        else:
+            self._apply(lambda t: t.to(device, non_blocking=non_blocking), self)
         return self
+
+    def _apply(self, fn, other) -> None:
+        """other's fields and kernel layout := fn(self's); the layout's host statistics stay bound
+        to the features when they described them."""
+        types_ok = self._layout_types_ok()
+        lay = getattr(self, "_nt_layout", None)
+        for name in self._field_names():
+            setattr(other, name, fn(getattr(self, name)))
+        if lay is not None:
+            moved = lay.map_tensors(fn, other.edge_index, getattr(other, "batch_node_index", None))
+            if types_ok:
+                moved.type_src = (weakref.ref(other.node_feats), weakref.ref(other.edge_feats),
+                                  (other.node_feats._version, other.edge_feats._version))
+            else:
+                moved.type_range = None
+            other._nt_layout = moved
+
+    def pack(self):
+        """Copy every host tensor of the graph and its layout into ONE contiguous buffer (views at
+        64-B aligned offsets), so pickling to the main process, pinning and the H2D copy each move
+        one storage instead of ~15 (DataLoader workers: data/loader.py)."""
+        ts, seen = [], set()
+        for t in self.tensors():
+            if id(t) not in seen:
+                seen.add(id(t))
+                ts.append(t)
+        if any(t.device.type != "cpu" or t.numel() == 0 for t in ts):
+            return self
+        offs, total = {}, 0
+        for t in ts:
+            offs[id(t)] = total
+            total += (t.numel() * t.element_size() + 63) // 64 * 64
+        buf = torch.empty(total, dtype=torch.uint8)
+        views = {}
+        for t in ts:
+            o = offs[id(t)]
+            v = buf[o:o + t.numel() * t.element_size()].view(t.dtype).view(t.shape)
+            v.copy_(t)
+            views[id(t)] = v
+        self._apply(lambda t: views[id(t)], self)
+        self._nt_packed = buf
+        return self
+
+    def _packed_base(self) -> Optional[Tensor]:
+        """The packed buffer if every tensor of the graph is still a contiguous view into it."""
+        buf = getattr(self, "_nt_packed", None)
+        if buf is None:
+            return None
+        lo, hi = buf.data_ptr(), buf.data_ptr() + buf.numel()
+        for t in self.tensors():
+            p = t.data_ptr()
+            if t.device != buf.device or not t.is_contiguous() or p < lo or p + t.numel() * t.element_size() > hi:
+                return None
+        return buf
 
     def _feature_tensors(self) -> list:
         return [self.node_feats, self.edge_feats, self.edge_index, self.rev_index]
@@ -170,19 +239,15 @@ class Graph(UpdateMixin):
         """Copy of the graph with every host tensor (features, indices, CSR layout, plans) in pinned
         memory, so .to(device, non_blocking=True) is an asynchronous DMA.  torch's DataLoader calls
         this on collated batches when pin_memory=True."""
-        types_ok = self._layout_types_ok()
         other = copy(self)
-        for name in self._field_names():
-            setattr(other, name, getattr(self, name).pin_memory())
-        lay = getattr(self, "_nt_layout", None)
-        if lay is not None:
-            moved = lay.map_tensors(Tensor.pin_memory, other.edge_index, getattr(other, "batch_node_index", None))
-            if types_ok:
-                moved.type_src = (weakref.ref(other.node_feats), weakref.ref(other.edge_feats),
-                                  (other.node_feats._version, other.edge_feats._version))
-            else:
-                moved.type_range = None
-            other._nt_layout = moved
+        buf = self._packed_base()
+        if buf is not None:
+            new = buf.pin_memory()
+            self._apply(_rebaser(buf, new), other)
+            other._nt_packed = new
+        else:
+            self._apply(Tensor.pin_memory, other)
+            other._nt_packed = None
         return other
 
     def _field_names(self) -> list:
@@ -198,17 +263,6 @@ class Graph(UpdateMixin):
     def _layout_types_ok(self) -> bool:
         lay = getattr(self, "_nt_layout", None)
         return lay is not None and lay.type_range is not None and _same_types(lay, self.node_feats, self.edge_feats)
-
-    def _move_layout(self, device, types_ok: bool = False):
-        lay = getattr(self, "_nt_layout", None)
-        if lay is not None and device is not None:
-            moved = lay.to(device, self.edge_index, getattr(self, "batch_node_index", None))
-            if types_ok:  # the statistics described the tensors just moved: re-bind them
-                moved.type_src = (weakref.ref(self.node_feats), weakref.ref(self.edge_feats),
-                                  (self.node_feats._version, self.edge_feats._version))
-            else:
-                moved.type_range = None
-            self._nt_layout = moved
 
     @property
     def A(self) -> Tensor:
@@ -255,14 +309,6 @@ class BatchedGraph(Graph):
 
     def __len__(self) -> int:
         return self._size
-
-    def to(self, device, non_blocking: bool = False):
-        types_ok = self._layout_types_ok()
-        self._device = device
-        for name in self._field_names():
-            setattr(self, name, getattr(self, name).to(device, non_blocking=non_blocking))
-        self._move_layout(device, types_ok)
-        return self
 
     def _field_names(self) -> list:
         return ["node_feats", "edge_feats", "edge_index", "rev_index", "batch_node_index", "batch_edge_index"]

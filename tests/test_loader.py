@@ -38,3 +38,27 @@ def test_graph_tensors_cover_layout():
     lay = G._nt_layout
     for t in (lay.dst_ptr, lay.dst_perm, lay.mol_ptr, lay.plan[0], lay.plan[2], G.batch_edge_index):
         assert any(t is u for u in ts)
+
+
+def test_pack_one_buffer_same_values_and_pickles_as_one_storage():
+    import io
+
+    graphs = make_batch("qm9", 40, seed=5).to_graphs()
+    ref = BatchedGraph.from_graphs(graphs, "nodes")
+    G = BatchedGraph.from_graphs(graphs, "nodes").pack()
+    _same(G, ref)
+    buf = G._nt_packed
+    assert G._packed_base() is buf
+    assert {t.untyped_storage().data_ptr() for t in G.tensors()} == {buf.untyped_storage().data_ptr()}
+    # through a worker queue (torch's shared-memory reductions): still one buffer in the main process
+    dl = torch.utils.data.DataLoader(graphs, batch_size=40, collate_fn=GraphCollator("nodes"), num_workers=1)
+    (G2,) = list(dl)
+    _same(G2, ref)
+    assert G2._packed_base() is not None
+    # a graph whose features were replaced (update) falls back to per-tensor moves
+    G3 = G.update(node_feats=G.node_feats.clone())
+    assert G3._packed_base() is None
+    G3.to("cpu")
+    for x, y in zip(G3.tensors(), ref.tensors()):
+        assert torch.equal(x, y)
+    assert G3._nt_layout.type_range is None  # the statistics described the replaced tensor
