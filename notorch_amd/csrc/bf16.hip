@@ -573,7 +573,7 @@ int launch_init_bf16(const void* Xv, const void* Xe, const int64_t* src, const i
                    (S == nullptr || aligned16(S));
   if (S != nullptr) {
     if (V == 0) return NT_OK;
-    NT_REQUIRE(seg_ptr && perm, NT_EINVAL, "fused aggregation needs the dst CSR");
+    NT_REQUIRE(seg_ptr && (perm || E == 0), NT_EINVAL, "fused aggregation needs the dst CSR");
     NT_REQUIRE(E == 0 || (Xv && Xe && src && H0), NT_EINVAL, "NULL pointer");
     if (vec) {
       const int grid = grid_for(V * (h / 8), 256, 256 * 32);

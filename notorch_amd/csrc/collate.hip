@@ -40,8 +40,9 @@ extern "C" int nt_collate_graphs(int64_t B, const void* const* node_feats, const
   }
   NT_REQUIRE(V < (int64_t(1) << 31) && E < (int64_t(1) << 31), NT_EINVAL,
              "batch too large for the int32 CSR (V, E < 2^31)");
-  NT_REQUIRE(edge_index_out && rev_out && batch_node_index && batch_edge_index && dst_ptr &&
-                 (E == 0 || dst_perm) && mol_ptr,
+  // edge outputs may be NULL (empty tensors) when the batch has no edge at all
+  NT_REQUIRE((E == 0 || (edge_index_out && rev_out && batch_edge_index && dst_perm)) &&
+                 (V == 0 || batch_node_index) && dst_ptr && mol_ptr,
              NT_EINVAL, "NULL output pointer");
   NT_REQUIRE(node_row_bytes == 0 || V == 0 || (node_feats && node_out), NT_EINVAL, "NULL node_feats");
   NT_REQUIRE(edge_row_bytes == 0 || E == 0 || (edge_feats && edge_out), NT_EINVAL, "NULL edge_feats");

@@ -318,7 +318,7 @@ extern "C" int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_type
   NT_REQUIRE(V >= 0 && E >= 0 && h > 0 && kv >= 0 && ke >= 0 && num_node_types >= 0 &&
                  num_edge_types >= 0,
              NT_EINVAL, "bad sizes");
-  NT_REQUIRE(S == nullptr || (seg_ptr && perm), NT_EINVAL, "fused aggregation needs the dst CSR");
+  NT_REQUIRE(S == nullptr || (seg_ptr && (perm || E == 0)), NT_EINVAL, "fused aggregation needs the dst CSR");
   NT_REQUIRE(E == 0 || (node_table && edge_table && src && H0 && (node_types || kv == 0) &&
                         (edge_types || ke == 0)),
              NT_EINVAL, "NULL pointer");

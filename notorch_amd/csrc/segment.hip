@@ -243,7 +243,7 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
                    (S == nullptr || aligned16(S));
   if (S != nullptr) {
     if (V == 0) return NT_OK;
-    NT_REQUIRE(seg_ptr && perm, NT_EINVAL, "fused aggregation needs the dst CSR");
+    NT_REQUIRE(seg_ptr && (perm || E == 0), NT_EINVAL, "fused aggregation needs the dst CSR");
     NT_REQUIRE(E == 0 || (Xv && Xe && src && H0), NT_EINVAL, "NULL pointer");
     if (vec) {
       const int64_t hv = h / 4;

@@ -375,6 +375,11 @@ class BatchedGraph(Graph):
         return super().__repr__()[:-1] + f", batch_size={len(self)})"
 
 
+def _row_bytes(x: Tensor) -> int:
+    """Bytes of one row (dim 0) of x, also when x has no rows."""
+    return int(np.prod(x.shape[1:], dtype=np.int64)) * x.element_size()
+
+
 def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
     """BatchedGraph.from_graphs through nt_collate_graphs (host C++; see include/notorch_amd.h)."""
     import ctypes
@@ -432,8 +437,8 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
     keep: list = []
     lib = _lib.load()
     _lib.check(lib.nt_collate_graphs(
-        B, ptrs(nf), n_nodes.data_ptr(), nd[0].numel() * nd.element_size() if nd.dim() else nd.element_size(),
-        ptrs(ef), n_edges.data_ptr(), ed[0].numel() * ed.element_size() if ed.dim() else ed.element_size(),
+        B, ptrs(nf), n_nodes.data_ptr(), _row_bytes(nd),
+        ptrs(ef), n_edges.data_ptr(), _row_bytes(ed),
         ptrs(ei), ptrs(rv), 0 if rev_offset == "nodes" else 1, node_out.data_ptr(), edge_out.data_ptr(),
         edge_index.data_ptr(), rev_index.data_ptr(), bni.data_ptr(), bei.data_ptr(),
         dst_ptr.data_ptr(), dst_perm.data_ptr(), mol_ptr.data_ptr(),

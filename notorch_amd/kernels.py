@@ -224,6 +224,8 @@ def segment_reduce(
     h = X.shape[1]
     if out is None:
         out = torch.empty(nseg, h, dtype=X.dtype, device=dev)
+    if X.shape[0] == 0:  # no rows (an edge-free batch): every segment is empty -> 0 (torch_scatter)
+        return out.zero_()
     lib = _lib.load()
     _run(dev, lib.nt_segment_reduce,
          _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce), act[0], act[1], code,
@@ -453,6 +455,8 @@ def segment_arg(X: Tensor, seg_ptr: Tensor, perm: Tensor | None, nseg: int, redu
         raise ValueError("segment_arg: reduce must be 'max' or 'min'")
     h = X.shape[1]
     arg = torch.empty(nseg, h, dtype=torch.int32, device=dev)
+    if X.shape[0] == 0:  # no rows: every segment is empty
+        return arg.fill_(-1)
     _run(dev, _lib.load().nt_segment_arg, _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce),
          act[0], act[1], NT_F32, _ptr(arg), _stream(dev))
     return arg

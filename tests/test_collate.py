@@ -146,3 +146,19 @@ def test_host_plans_ship_with_the_collate():
     chunk_pos, nchunks, chunk_ptr = lay.dst_chunks
     assert chunk_pos.numel() == nchunks + 1 and int(chunk_ptr[-1]) == nchunks
     assert (np.diff(chunk_pos.numpy()) <= 32).all()
+
+
+def test_all_zero_bond_batch_collates():
+    """Every molecule without a bond (E = 0 in the whole batch): the native collate still returns
+    the reference layout (empty edge tensors of the right shapes, one molecule per node)."""
+    import torch
+
+    from notorch_amd.data.models.graph import BatchedGraph, Graph
+
+    one = Graph(torch.tensor([[1, 12, 20, 25, 30, 36, 41]]), torch.zeros(0, 2, dtype=torch.long),
+                torch.zeros(2, 0, dtype=torch.long), torch.zeros(0, dtype=torch.long))
+    G = BatchedGraph.from_graphs([one, one, one])
+    assert G.num_nodes == 3 and G.num_edges == 0 and len(G) == 3
+    assert G.edge_feats.shape == (0, 2) and G.edge_index.shape == (2, 0) and G.rev_index.shape == (0,)
+    assert G.batch_node_index.tolist() == [0, 1, 2]
+    assert G._nt_layout.dst_ptr.tolist() == [0, 0, 0, 0]

@@ -561,3 +561,27 @@ def test_config4_shard_decomposition_bitexact():
     parts = [run(batch.subset(a, c)) for a, c in ranges]
     assert torch.equal(whole.edge_feats, torch.cat([p.edge_feats for p in parts]))
     assert torch.equal(whole.node_feats, torch.cat([p.node_feats for p in parts]))
+
+
+@pytest.mark.parametrize("reduce", ["sum", "max"])
+def test_all_zero_bond_batch_forward_and_backward(reduce):
+    """A batch with no edge at all (E = 0): H is 0 x h, every node row and readout is 0 (empty
+    segments, torch_scatter), and the backward gives zero gradients for Xv / weights."""
+    from notorch_amd.data.models.graph import BatchedGraph, Graph
+    from notorch_amd.nn import ChempropBlock, Sum
+
+    one = Graph(torch.tensor([[1, 12, 20, 25, 30, 36, 41]]), torch.zeros(0, 2, dtype=torch.long),
+                torch.zeros(2, 0, dtype=torch.long), torch.zeros(0, dtype=torch.long))
+    G = BatchedGraph.from_graphs([one, one, one])
+    h = 32
+    Xv = torch.randn(G.num_nodes, h, device=DEV, requires_grad=True)
+    Xe = torch.zeros(0, h, device=DEV, requires_grad=True)
+    blk = ChempropBlock(hidden_dim=h, depth=2, reduce=reduce).to(DEV)
+    out = blk(G.to(DEV).update(node_feats=Xv, edge_feats=Xe))
+    r = Sum()(out)
+    assert out.edge_feats.shape == (0, h) and torch.count_nonzero(out.node_feats) == 0
+    assert r.shape == (3, h) and torch.count_nonzero(r) == 0
+    r.sum().backward()
+    assert torch.count_nonzero(Xv.grad) == 0
+    for m in blk._chemprop_layers():
+        assert m.linear.weight.grad is None or torch.count_nonzero(m.linear.weight.grad) == 0
