@@ -107,7 +107,7 @@ struct Args {
   float aalpha;
   float4* O4;
   float4* SO4;
-  int prio;  // NT_PK_PRIO: 1 = producers at s_setprio 1, 2 = consumers (A/B; 0 = none)
+  int prio;  // 1 = producers at s_setprio 1 (default), 2 = consumers, 0 = none (NT_PK_PRIO, DIAG)
   int nxcd;  // XCDs of the device (xcd_count()): blocks b and b + nxcd share an L2
 };
 
@@ -691,11 +691,14 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
   a.O4 = (float4*)u.H_out;
   a.SO4 = (float4*)S_out;
   a.nxcd = xcd_count();
-  a.prio = 0;  // age arbitration (consumer priority measured +-1%: A/B only)
+  // producers at s_setprio 1: with two consumer waves per SIMD the producers bound the kernel, and
+  // winning issue arbitration takes 4 % off a launch (133.7 -> 128.6 us at config 2; consumer
+  // priority: 134.6)
+  a.prio = 1;
 #ifdef NT_DIAG
   {
     const char* pr = getenv("NT_PK_PRIO");
-    a.prio = pr && pr[0] ? atoi(pr) : 0;
+    if (pr && pr[0]) a.prio = atoi(pr);
   }
 #endif
   if (a.ntiles == 0) return NT_OK;
