@@ -310,6 +310,19 @@ NT_API int nt_gather_rows_arg(const void* base, const void* X, const int64_t* id
 NT_API int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const void* Wp, int dtype,
                                  void* out, void* stream);
 
+/* Weight and bias gradient of one layer (backward of nn.Linear at chemprop.py:26,41, trained through
+ * lightning_models/model.py:224-241; the reference runs it as ATen addmm's autograd), with the
+ * layer message formed on the fly (never written):
+ *   A[e] = S[src[e]] - act(H[rev[e]])   (chemprop.py:40; src = rev = NULL: A[e] = S[e], H unused)
+ *   dW = G^T A  (h x h),   db = sum_e G[e]  (db_out may be NULL)
+ * Split-K bf16x6 MFMA kernel (fp32-accurate), deterministic (partials reduced in fixed order).
+ * workspace: device buffer of at least nt_dmpnn_weight_grad_workspace(E, h) bytes.  fp32 only. */
+NT_API int64_t nt_dmpnn_weight_grad_workspace(int64_t E, int64_t h);
+NT_API int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S, const int64_t* src,
+                                const int64_t* rev, int64_t V, int64_t E, int64_t h, int act,
+                                float act_alpha, int dtype, void* workspace, int64_t workspace_bytes,
+                                void* dW_out, void* db_out, void* stream);
+
 /* Device status word of the calling device (no reference counterpart: the reference's ops cannot
  * hang).  The persistent fp32 update kernel hands work between its waves through bounded LDS waits;
  * a wait that gives up sets this word (sticky) and the launch's outputs are invalid.

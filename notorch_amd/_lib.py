@@ -107,6 +107,11 @@ SIGNATURES: dict[str, tuple] = {
     ),
     "nt_gather_rows_arg": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_int, _vp, _vp]),
     "nt_dmpnn_dense_matmul": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, _vp]),
+    "nt_dmpnn_weight_grad_workspace": (_c_i64, [_c_i64, _c_i64]),
+    "nt_dmpnn_weight_grad": (
+        _c_int,
+        [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _c_int, _vp, _c_i64, _vp, _vp, _vp],
+    ),
     "nt_device_status": (_c_int, [_vp, _vp]),
     "nt_device_status_reset": (_c_int, [_vp]),
 }

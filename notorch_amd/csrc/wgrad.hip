@@ -1,0 +1,289 @@
+// Weight and bias gradient of one D-MPNN layer (backward of nn.Linear at
+// chemprop.py:26,41, trained through lightning_models/model.py:224-241), with the layer message
+// formed while staging so it is never written to HBM:
+//   A[e]  = S[src e] - act(H[rev e])                           (chemprop.py:40; src/rev NULL: A = S)
+//   dW    = G^T A          (h x h, reduced over all E edges)
+//   db    = sum_e G[e]
+//
+// Split-K over edges: a 1-D grid of (64 x 64 output tile, edge chunk) workgroups.  Each workgroup
+// walks its chunk 32 edges at a time: 256 threads load the 32 x 64 slab of G and of A (thread =
+// one column, 8 consecutive edges; each load instruction reads 64 consecutive floats of one row),
+// split every fp32 value into three bf16 parts once, and store them to a double-buffered LDS slab
+// laid out [part][edge group][column] in 16-B units, so both the writes and the MFMA fragment reads
+// are contiguous 1 KiB runs (no bank conflicts).  Wave w owns a 32 x 32 quadrant: 4 MFMA tiles x 6
+// bf16 products (the bf16x6 split of csrc/update_pk.hip: fp32-accurate) per 32 edges.
+// Partials (and the bias partials of the j-tile-0 workgroups) go to a workspace, reduced by a
+// second kernel in fixed order, so the result is deterministic.
+//
+// XCD-aware: all output tiles of one edge chunk run on one XCD (blocks b, b + n share an XCD), so
+// the chunk's G / S / H rows are fetched into that XCD's L2 once and read from there by the 25
+// (at h = 300) tiles.
+//
+// Algorithmic bytes per call: G and A operands E*h*4 each (+ the gathers S[src], H[rev] replace A:
+// 3 rows per edge), partial writes ksplit*h*h*4; flops 2*E*h^2.
+#include "common.hpp"
+
+namespace nt {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+
+constexpr int kT = 64;              // output tile edge
+constexpr int kK = 32;              // edges per step
+constexpr int kPartB = 4 * 64 * 16; // one bf16 part of a 32 x 64 slab: 4 groups x 64 cols x 16 B
+constexpr int kSlabB = 3 * kPartB;  // 12 KiB
+constexpr int kBlocksTarget = 1024;
+
+__device__ __forceinline__ void split3(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const __bf16 h0 = (__bf16)x[j];
+    const float r1 = x[j] - (float)h0;
+    const __bf16 h1 = (__bf16)r1;
+    p0[j] = h0;
+    p1[j] = h1;
+    p2[j] = (__bf16)(r1 - (float)h1);
+  }
+}
+
+struct WgArgs {
+  const float* G;
+  const float* H;
+  const float* S;
+  const int64_t* src;
+  const int64_t* rev;
+  int64_t E, h;
+  int tiles, ksplit, chunk_steps, xcds;
+  float alpha;
+  int act;
+  float* part;     // [ksplit][h][h]
+  float* part_db;  // [ksplit][h] or NULL
+};
+
+template <int ACT>
+__global__ void __launch_bounds__(256) wgrad_kernel(WgArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  // XCD-aware work id: consecutive work ids (the tiles of one chunk) on one XCD
+  const int nb = gridDim.x;
+  int w = blockIdx.x;
+  if (a.xcds > 1 && nb % a.xcds == 0) w = (w % a.xcds) * (nb / a.xcds) + w / a.xcds;
+  const int y = w / a.tiles, tile = w - y * a.tiles;
+  const int tpr = (int)((a.h + kT - 1) / kT);
+  const int ti = tile / tpr, tj = tile - ti * tpr;
+  const int64_t i0 = (int64_t)ti * kT, j0 = (int64_t)tj * kT, h = a.h;
+  const int64_t e_beg = (int64_t)y * a.chunk_steps * kK;
+  const int64_t e_end0 = e_beg + (int64_t)a.chunk_steps * kK;
+  const int64_t e_end = e_end0 < a.E ? e_end0 : a.E;
+  const int nsteps = e_end > e_beg ? (int)((e_end - e_beg + kK - 1) / kK) : 0;
+
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int c = lane;          // staging: my column
+  const int g = wave;          // staging: my edge group (8 edges)
+  const bool ci = i0 + c < h, cj = j0 + c < h;
+  const bool want_db = a.part_db != nullptr && tj == 0;
+  float dbacc = 0.f;
+
+  float gv[8], av[8];
+  auto load = [&](int s) {
+    const int64_t eb = e_beg + (int64_t)s * kK + 8 * g;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int64_t e = eb + r;
+      const bool ok = e < e_end;
+      gv[r] = ok && ci ? a.G[e * h + i0 + c] : 0.f;
+      if (a.src) {
+        const int64_t se = ok ? a.src[e] : 0, re = ok ? a.rev[e] : 0;
+        av[r] = ok && cj ? a.S[se * h + j0 + c] - act_t<ACT>(a.H[re * h + j0 + c], a.act, a.alpha) : 0.f;
+      } else {
+        av[r] = ok && cj ? a.S[e * h + j0 + c] : 0.f;
+      }
+    }
+  };
+  auto store = [&](int buf) {
+    char* base = lds + buf * 2 * kSlabB;
+    const int off = (g * 64 + c) * 16;
+    bf16x8 p0, p1, p2;
+    split3(gv, p0, p1, p2);
+    *reinterpret_cast<bf16x8*>(base + off) = p0;
+    *reinterpret_cast<bf16x8*>(base + kPartB + off) = p1;
+    *reinterpret_cast<bf16x8*>(base + 2 * kPartB + off) = p2;
+    split3(av, p0, p1, p2);
+    base += kSlabB;
+    *reinterpret_cast<bf16x8*>(base + off) = p0;
+    *reinterpret_cast<bf16x8*>(base + kPartB + off) = p1;
+    *reinterpret_cast<bf16x8*>(base + 2 * kPartB + off) = p2;
+    if (want_db) {
+#pragma unroll
+      for (int r = 0; r < 8; ++r) dbacc += gv[r];
+    }
+  };
+
+  // MFMA roles: wave (wi, wj) owns rows 32 wi.. and columns 32 wj.. of the tile
+  const int fr = lane & 15, g16 = lane >> 4;
+  const int wi = wave & 1, wj = wave >> 1;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int z = 0; z < 2; ++z) acc[x][z] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  if (nsteps > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) load(s + 1);
+    const char* gb = lds + buf * 2 * kSlabB;
+    const char* ab = gb + kSlabB;
+    bf16x8 fa[2][3], fb[2][3];
+#pragma unroll
+    for (int x = 0; x < 2; ++x) {
+      const int off_a = (g16 * 64 + 32 * wi + 16 * x + fr) * 16;
+      const int off_b = (g16 * 64 + 32 * wj + 16 * x + fr) * 16;
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        fa[x][p] = *reinterpret_cast<const bf16x8*>(gb + p * kPartB + off_a);
+        fb[x][p] = *reinterpret_cast<const bf16x8*>(ab + p * kPartB + off_b);
+      }
+    }
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int z = 0; z < 2; ++z) {
+        f32x4 cc = acc[x][z];
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x][0], fb[z][2], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x][1], fb[z][1], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x][2], fb[z][0], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x][0], fb[z][1], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x][1], fb[z][0], cc, 0, 0, 0);
+        cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x][0], fb[z][0], cc, 0, 0, 0);
+        acc[x][z] = cc;
+      }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+
+  // D lane (fr, g16), register q = tile row 4 g16 + q (A operand: G column = dW row), column fr
+  float* P = a.part + (int64_t)y * h * h;
+#pragma unroll
+  for (int x = 0; x < 2; ++x)
+#pragma unroll
+    for (int z = 0; z < 2; ++z) {
+      const int64_t col = j0 + 32 * wj + 16 * z + fr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = i0 + 32 * wi + 16 * x + 4 * g16 + q;
+        if (row < h && col < h) P[row * h + col] = acc[x][z][q];
+      }
+    }
+  if (want_db) {
+    float* red = reinterpret_cast<float*>(lds);  // slabs are dead after the last barrier
+    red[g * 64 + c] = dbacc;
+    __syncthreads();
+    if (wave == 0 && ci) a.part_db[(int64_t)y * h + i0 + c] = red[c] + red[64 + c] + red[128 + c] + red[192 + c];
+  }
+}
+
+// out[i] = sum_y part[y][i] in ascending y (fixed order: deterministic)
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int64_t n,
+                                                           int ksplit, float* __restrict__ out) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    float s = 0.f;
+    for (int y = 0; y < ksplit; ++y) s += part[(int64_t)y * n + i];
+    out[i] = s;
+  }
+}
+
+struct Plan {
+  int tiles, ksplit, chunk_steps;
+};
+
+Plan make_plan(int64_t E, int64_t h) {
+  Plan p;
+  const int tpr = (int)((h + kT - 1) / kT);
+  p.tiles = tpr * tpr;
+  const int64_t steps = (E + kK - 1) / kK;
+  int64_t ks = ((kBlocksTarget + p.tiles - 1) / p.tiles + 7) / 8 * 8;
+  if (ks > steps) ks = steps > 0 ? steps : 1;
+  p.chunk_steps = (int)((steps + ks - 1) / ks);
+  if (p.chunk_steps < 1) p.chunk_steps = 1;
+  p.ksplit = (int)((steps + p.chunk_steps - 1) / p.chunk_steps);
+  if (p.ksplit < 1) p.ksplit = 1;
+  return p;
+}
+
+int xcd_count() {
+  int dev = 0, n = 1;
+  if (hipGetDevice(&dev) != hipSuccess) return 1;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess || n < 1) return 1;
+  return n;
+}
+
+}  // namespace
+}  // namespace nt
+
+extern "C" int64_t nt_dmpnn_weight_grad_workspace(int64_t E, int64_t h) {
+  if (E < 0 || h <= 0) return -1;
+  const nt::Plan p = nt::make_plan(E, h);
+  return (int64_t)p.ksplit * (h * h + h) * (int64_t)sizeof(float);
+}
+
+extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S, const int64_t* src,
+                                    const int64_t* rev, int64_t V, int64_t E, int64_t h, int act,
+                                    float act_alpha, int dtype, void* workspace, int64_t workspace_bytes,
+                                    void* dW_out, void* db_out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_weight_grad: fp32 only");
+  NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
+  NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE((src == nullptr) == (rev == nullptr), NT_EINVAL, "src and rev: both or neither");
+  NT_REQUIRE(dW_out, NT_EINVAL, "NULL dW_out");
+  hipStream_t stream = as_stream(stream_);
+  if (E == 0) {
+    NT_HIP(hipMemsetAsync(dW_out, 0, h * h * sizeof(float), stream));
+    if (db_out) NT_HIP(hipMemsetAsync(db_out, 0, h * sizeof(float), stream));
+    return NT_OK;
+  }
+  NT_REQUIRE(G && S && (src == nullptr || H), NT_EINVAL, "NULL pointer");
+  const Plan p = make_plan(E, h);
+  NT_REQUIRE(workspace && workspace_bytes >= (int64_t)p.ksplit * (h * h + h) * (int64_t)sizeof(float),
+             NT_EINVAL, "workspace too small (nt_dmpnn_weight_grad_workspace)");
+  WgArgs a;
+  a.G = (const float*)G;
+  a.H = (const float*)H;
+  a.S = (const float*)S;
+  a.src = src;
+  a.rev = rev;
+  a.E = E;
+  a.h = h;
+  a.tiles = p.tiles;
+  a.ksplit = p.ksplit;
+  a.chunk_steps = p.chunk_steps;
+  a.xcds = xcd_count();
+  a.alpha = act_alpha;
+  a.act = act;
+  a.part = (float*)workspace;
+  a.part_db = db_out ? a.part + (int64_t)p.ksplit * h * h : nullptr;
+  const int grid = p.tiles * p.ksplit;
+  const size_t lds = 4 * kSlabB;
+  if (act == NT_ACT_IDENTITY)
+    wgrad_kernel<NT_ACT_IDENTITY><<<grid, 256, lds, stream>>>(a);
+  else if (act == NT_ACT_RELU)
+    wgrad_kernel<NT_ACT_RELU><<<grid, 256, lds, stream>>>(a);
+  else
+    wgrad_kernel<-1><<<grid, 256, lds, stream>>>(a);
+  NT_LAUNCH_CHECK();
+  wgrad_reduce_kernel<<<grid_for(h * h, 256, 256 * 8), 256, 0, stream>>>(a.part, h * h, p.ksplit, (float*)dW_out);
+  NT_LAUNCH_CHECK();
+  if (db_out) {
+    wgrad_reduce_kernel<<<grid_for(h, 256, 64), 256, 0, stream>>>(a.part_db, h, p.ksplit, (float*)db_out);
+    NT_LAUNCH_CHECK();
+  }
+  return NT_OK;
+}

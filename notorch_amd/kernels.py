@@ -33,6 +33,7 @@ __all__ = [
     "node_scores",
     "softmax_pool",
     "dense_matmul",
+    "weight_grad",
     "segment_arg",
     "dmpnn_edge_backward_arg",
     "gather_rows_arg",
@@ -443,6 +444,38 @@ def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None) -> Tensor:
         out = torch.empty_like(X)
     _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_F32, _ptr(out), _stream(dev))
     return out
+
+
+def weight_grad(G: Tensor, H: Tensor | None, S: Tensor, src: Tensor | None, rev: Tensor | None, *,
+                act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0), bias: bool = True) -> tuple[Tensor, Tensor | None]:
+    """(dW, db) = (G^T A, sum_e G[e]) with A[e] = S[src e] - act(H[rev e]) formed on the fly
+    (src = rev = None: A = S).  fp32, split-K bf16x6 MFMA, deterministic."""
+    dev = _require_device(G, H, S, src, rev)
+    _require_f32("G", G)
+    _require_f32("S", S)
+    E, h = G.shape
+    if (src is None) != (rev is None):
+        raise ValueError("weight_grad: pass both src and rev_index or neither")
+    if src is not None:
+        assert H is not None
+        _require_f32("H", H)
+        _require_i64("src", src)
+        _require_i64("rev_index", rev)
+        if H.shape != (E, h) or S.shape[1] != h or src.numel() != E or rev.numel() != E:
+            raise ValueError("shape mismatch between G, H, S, src and rev_index")
+    elif S.shape != (E, h):
+        raise ValueError("weight_grad: S must be E x h when src is None")
+    for n_, t in (("G", G), ("H", H), ("S", S)):
+        if t is not None and not t.is_contiguous():
+            raise ValueError(f"weight_grad: {n_} must be contiguous")
+    lib = _lib.load()
+    nbytes = lib.nt_dmpnn_weight_grad_workspace(E, h)
+    ws = torch.empty((max(nbytes, 4) + 3) // 4, dtype=torch.float32, device=dev)
+    dW = torch.empty(h, h, dtype=torch.float32, device=dev)
+    db = torch.empty(h, dtype=torch.float32, device=dev) if bias else None
+    _run(dev, lib.nt_dmpnn_weight_grad, _ptr(G), _ptr(H), _ptr(S), _ptr(src), _ptr(rev), S.shape[0], E, h,
+         act[0], act[1], NT_F32, _ptr(ws), ws.numel() * 4, _ptr(dW), _ptr(db), _stream(dev))
+    return dW, db
 
 
 def segment_arg(X: Tensor, seg_ptr: Tensor, perm: Tensor | None, nseg: int, reduce: str, *,

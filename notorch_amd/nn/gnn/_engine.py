@@ -22,8 +22,9 @@ kernel code, or layers that differ in activation / dropout, run layer by layer
 Backward (training): the forward keeps (H_l, S_l) of every layer; per layer,
 last to first (csrc/backward.hip):
 
-    nt_dmpnn_message        A_l = S_l[src] - act(H_l)[rev]                   (recomputed, for dW)
-    GEMM (library)          dW_l = G^T A_l (split-K),  db_l = colsum(G)
+    nt_dmpnn_weight_grad    dW_l = G^T A_l, db_l = colsum(G), A_l = S_l[src] - act(H_l)[rev] formed
+                            while staging (fp32: split-K bf16x6 MFMA; bf16: nt_dmpnn_message + a
+                            split-K library GEMM)
     nt_dmpnn_dense_matmul   dA = G W_l                 (fp32: the bf16x6 MFMA kernel; bf16: library)
     nt_segment_reduce       dS = scatter_sum(dA, src)            (src CSR, cached on the layout)
     nt_dmpnn_edge_backward  G <- G + act'(H_l) * (dS[dst] / c - scatter_sum(dA, rev))  (rev CSR)
@@ -551,12 +552,17 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
     for l in range(d - 1, -1, -1):
         H_l, S_l = states[l]
         W = weights[l].detach()
-        A = K.dmpnn_message(H_l, S_l, src, rev, act=act)
         # dropout: the update's gradient is keep * G / (1 - p); the residual path keeps G
         Gu = G if drop is None else K.dropout_residual(G, drop[0], drop[1], dropout_offset(l, E, h))
-        dWs[l] = _weight_grad(Gu, A)
-        dbs[l] = Gu.sum(0)
-        del A
+        if Gu.dtype == torch.float32 and os.environ.get("NT_WGRAD", "kernel") != "library":
+            # split-K bf16x6 MFMA with A = S[src] - act(H[rev]) formed while staging (never written)
+            dWs[l], dbs[l] = K.weight_grad(Gu.contiguous(), H_l.contiguous(), S_l.contiguous(), src, rev,
+                                           act=act)
+        else:
+            A = K.dmpnn_message(H_l, S_l, src, rev, act=act)
+            dWs[l] = _weight_grad(Gu, A)
+            dbs[l] = Gu.sum(0)
+            del A
         if Gu.dtype == torch.float32 and K.fused_supported(V, E, h, Gu.dtype):
             dA = K.dense_matmul(Gu.contiguous(), K.pack_weights(W.t().contiguous()))  # bf16x6 MFMA
         else:

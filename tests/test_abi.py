@@ -24,7 +24,7 @@ def test_header_declares_the_boundary():
         "nt_dmpnn_update_fused", "nt_dmpnn_message", "nt_dmpnn_edge_backward", "nt_gather_rows",
         "nt_embed_bag", "nt_dmpnn_init_embed", "nt_node_scores", "nt_softmax_pool",
         "nt_collate_graphs", "nt_segment_reduce_chunked", "nt_device_status", "nt_device_status_reset",
-        "nt_dmpnn_dense_matmul", "nt_segment_arg", "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg",
+        "nt_dmpnn_dense_matmul", "nt_dmpnn_weight_grad", "nt_dmpnn_weight_grad_workspace", "nt_segment_arg", "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg",
     }
 
 
@@ -80,3 +80,16 @@ def test_check_raises_with_message():
     lib.nt_dmpnn_pack_weight(None, 1, 0, 0, None, None)
     with pytest.raises(_lib.NativeLibraryError, match="bad sizes"):
         _lib.check(1)
+
+
+def test_weight_grad_host_checks():
+    """nt_dmpnn_weight_grad's workspace query and argument validation (pure host, no launch)."""
+    from notorch_amd import _lib
+
+    lib = _lib.load()
+    assert lib.nt_dmpnn_weight_grad_workspace(77_840, 300) > 0
+    assert lib.nt_dmpnn_weight_grad_workspace(-1, 300) == -1
+    rc = lib.nt_dmpnn_weight_grad(None, None, None, None, None, 4, 8, 16, 1, 0.0, 1, None, 0, None, None, None)
+    assert rc == 3  # bf16: not this kernel
+    rc = lib.nt_dmpnn_weight_grad(None, None, None, None, None, 4, 8, 16, 1, 0.0, 0, None, 0, None, None, None)
+    assert rc == 1 and b"dW_out" in lib.nt_last_error()

@@ -376,3 +376,38 @@ def test_dense_matmul_x6(h, M):
     out = K.dense_matmul(X.to(DEV), K.pack_weights(W.t().contiguous().to(DEV)))
     ref = X.double() @ W.double()
     assert_parity(out, ref, FP32_NORM_TOL, f"dense h={h} M={M}")
+
+
+@pytest.mark.parametrize("h,E,act", [(300, 77_840, "relu"), (300, 1, "relu"), (100, 1000, "identity"),
+                                     (64, 4097, "gelu"), (4, 3, "relu"), (512, 3000, "tanh"),
+                                     (300, 33, "leaky_relu")])
+def test_weight_grad_x6(h, E, act):
+    """nt_dmpnn_weight_grad (the backward's dW = G^T A and db = colsum G of nn.Linear at
+    chemprop.py:26,41, A = S[src] - act(H[rev]) of chemprop.py:40 formed in the kernel) against fp64,
+    fp32 contract; also bit-identical on a repeat (fixed-order split-K reduction)."""
+    K = _K()
+    mods = {"relu": nn.ReLU(), "identity": nn.Identity(), "gelu": nn.GELU(), "tanh": nn.Tanh(),
+            "leaky_relu": nn.LeakyReLU(0.1)}
+    mod = mods[act]
+    g = torch.Generator().manual_seed(E + h)
+    V = max(E // 2, 1)
+    Gr, H, S = torch.randn(E, h, generator=g), torch.randn(E, h, generator=g), torch.randn(V, h, generator=g)
+    src = torch.randint(0, V, (E,), generator=g)
+    rev = torch.randint(0, E, (E,), generator=g)
+    dW, db = K.weight_grad(Gr.to(DEV), H.to(DEV), S.to(DEV), src.to(DEV), rev.to(DEV), act=K.act_code(mod))
+    A = S.double()[src] - mod(H.double())[rev]
+    assert_parity(dW, Gr.double().t() @ A, FP32_NORM_TOL, f"dW h={h} E={E} {act}")
+    assert_parity(db, Gr.double().sum(0), FP32_NORM_TOL, f"db h={h} E={E}")
+    dW2, db2 = K.weight_grad(Gr.to(DEV), H.to(DEV), S.to(DEV), src.to(DEV), rev.to(DEV), act=K.act_code(mod))
+    assert torch.equal(dW, dW2) and torch.equal(db, db2)
+    # dense mode (no gathers): dW = G^T S
+    dWd, _ = K.weight_grad(Gr.to(DEV), None, H.to(DEV), None, None, bias=False)
+    assert_parity(dWd, Gr.double().t() @ H.double(), FP32_NORM_TOL, f"dense dW h={h} E={E}")
+
+
+def test_weight_grad_no_edges():
+    K = _K()
+    Z = torch.empty(0, 16, device=DEV)
+    dW, db = K.weight_grad(Z, Z, torch.randn(3, 16, device=DEV), torch.empty(0, dtype=torch.long, device=DEV),
+                           torch.empty(0, dtype=torch.long, device=DEV))
+    assert torch.count_nonzero(dW) == 0 and torch.count_nonzero(db) == 0
