@@ -85,19 +85,35 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgArgs a) {
   const bool want_db = a.part_db != nullptr && tj == 0;
   float dbacc = 0.f;
 
+  // The 8 edges' (src, rev) of a wave's group are fetched one step ahead as one vector load (lane r:
+  // src of edge r, lane 8 + r: its rev) and broadcast with readlane, so no scalar-load round trip
+  // sits in front of the row gathers.  Every load is unconditional (rows clamped to the chunk,
+  // columns to the row) and masked afterwards.
+  const bool gather = a.src != nullptr;
+  auto load_idx = [&](int s) -> int {
+    int64_t e = e_beg + (int64_t)s * kK + 8 * g + (lane & 7);
+    e = e < e_end ? e : e_end - 1;
+    if (!gather || lane >= 16 || e < 0) return 0;
+    return (int)(lane < 8 ? a.src[e] : a.rev[e]);
+  };
+  const int64_t ic = ci ? i0 + c : 0, jc = cj ? j0 + c : 0;
   float gv[8], av[8];
-  auto load = [&](int s) {
+  auto load = [&](int s, int idxv) {
     const int64_t eb = e_beg + (int64_t)s * kK + 8 * g;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int64_t e = eb + r;
       const bool ok = e < e_end;
-      gv[r] = ok && ci ? a.G[e * h + i0 + c] : 0.f;
-      if (a.src) {
-        const int64_t se = ok ? a.src[e] : 0, re = ok ? a.rev[e] : 0;
-        av[r] = ok && cj ? a.S[se * h + j0 + c] - act_t<ACT>(a.H[re * h + j0 + c], a.act, a.alpha) : 0.f;
+      const int64_t ec = ok ? e : e_end - 1;
+      const float x = a.G[ec * h + ic];
+      gv[r] = ok && ci ? x : 0.f;
+      if (gather) {
+        const int64_t se = __builtin_amdgcn_readlane(idxv, r), re = __builtin_amdgcn_readlane(idxv, 8 + r);
+        const float sv = a.S[se * h + jc], hv = a.H[re * h + jc];
+        av[r] = ok && cj ? sv - act_t<ACT>(hv, a.act, a.alpha) : 0.f;
       } else {
-        av[r] = ok && cj ? a.S[e * h + j0 + c] : 0.f;
+        const float sv = a.S[ec * h + jc];
+        av[r] = ok && cj ? sv : 0.f;
       }
     }
   };
@@ -129,15 +145,20 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgArgs a) {
 #pragma unroll
     for (int z = 0; z < 2; ++z) acc[x][z] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  int idx_next = 0;
   if (nsteps > 0) {
-    load(0);
+    load(0, load_idx(0));
+    if (nsteps > 1) idx_next = load_idx(1);
     store(0);
   }
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
     const bool more = s + 1 < nsteps;
-    if (more) load(s + 1);
+    if (more) {
+      load(s + 1, idx_next);
+      if (s + 2 < nsteps) idx_next = load_idx(s + 2);
+    }
     const char* gb = lds + buf * 2 * kSlabB;
     const char* ab = gb + kSlabB;
     bf16x8 fa[2][3], fb[2][3];
@@ -217,14 +238,9 @@ Plan make_plan(int64_t E, int64_t h) {
   return p;
 }
 
-int xcd_count() {
-  int dev = 0, n = 1;
-  if (hipGetDevice(&dev) != hipSuccess) return 1;
-  if (hipDeviceGetAttribute(&n, hipDeviceAttributeNumberOfXccs, dev) != hipSuccess || n < 1) return 1;
-  return n;
-}
-
 }  // namespace
+
+int xcd_count();  // csrc/update_ps.hip: the current device's XCD count, queried once per device
 }  // namespace nt
 
 extern "C" int64_t nt_dmpnn_weight_grad_workspace(int64_t E, int64_t h) {

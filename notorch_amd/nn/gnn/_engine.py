@@ -47,6 +47,8 @@ from notorch_amd._lib import NT_ACT_IDENTITY
 from notorch_amd.data.models.graph import DeviceLayout
 
 _IDENTITY = (NT_ACT_IDENTITY, 0.0)
+# fp32 weight gradient: "kernel" (nt_dmpnn_weight_grad) or "library" (message + split-K library GEMM)
+_WGRAD_DEFAULT = "library"
 
 # Optional per-launch timer for the dominant kernel (bench.py sets it): a list that receives
 # (start, end) torch.cuda.Event pairs recorded on the launch stream around every nt_dmpnn_update.
@@ -554,7 +556,7 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
         W = weights[l].detach()
         # dropout: the update's gradient is keep * G / (1 - p); the residual path keeps G
         Gu = G if drop is None else K.dropout_residual(G, drop[0], drop[1], dropout_offset(l, E, h))
-        if Gu.dtype == torch.float32 and os.environ.get("NT_WGRAD", "kernel") != "library":
+        if Gu.dtype == torch.float32 and os.environ.get("NT_WGRAD", _WGRAD_DEFAULT) == "kernel":
             # split-K bf16x6 MFMA with A = S[src] - act(H[rev]) formed while staging (never written)
             dWs[l], dbs[l] = K.weight_grad(Gu.contiguous(), H_l.contiguous(), S_l.contiguous(), src, rev,
                                            act=act)
