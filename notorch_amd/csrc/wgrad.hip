@@ -61,7 +61,7 @@ struct WgArgs {
   float* part_db;  // [ksplit][h] or NULL
 };
 
-template <int ACT>
+template <int ACT, bool GATHER>
 __global__ void __launch_bounds__(256) wgrad_kernel(WgArgs a) {
   extern __shared__ __attribute__((aligned(16))) char lds[];
   // XCD-aware work id: consecutive work ids (the tiles of one chunk) on one XCD
@@ -89,35 +89,46 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgArgs a) {
   // src of edge r, lane 8 + r: its rev) and broadcast with readlane, so no scalar-load round trip
   // sits in front of the row gathers.  Every load is unconditional (rows clamped to the chunk,
   // columns to the row) and masked afterwards.
-  const bool gather = a.src != nullptr;
   auto load_idx = [&](int s) -> int {
     int64_t e = e_beg + (int64_t)s * kK + 8 * g + (lane & 7);
     e = e < e_end ? e : e_end - 1;
-    if (!gather || lane >= 16 || e < 0) return 0;
+    if (!GATHER || lane >= 16) return 0;
     return (int)(lane < 8 ? a.src[e] : a.rev[e]);
   };
+  // masks instead of branches: a load whose value is only used under a condition gets sunk into a
+  // branch by the compiler, with a vmcnt(0) wait right behind it (every gather serialised)
   const int64_t ic = ci ? i0 + c : 0, jc = cj ? j0 + c : 0;
-  float gv[8], av[8];
+  const unsigned mi = ci ? ~0u : 0u, mj = cj ? ~0u : 0u;
+  // raw rows of the step in flight (consumed by store(), after the MFMAs of the previous step)
+  float xg[8], xs[8], xh[8];
+  int64_t eb_next = 0;
   auto load = [&](int s, int idxv) {
     const int64_t eb = e_beg + (int64_t)s * kK + 8 * g;
+    eb_next = eb;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int64_t e = eb + r;
-      const bool ok = e < e_end;
-      const int64_t ec = ok ? e : e_end - 1;
-      const float x = a.G[ec * h + ic];
-      gv[r] = ok && ci ? x : 0.f;
-      if (gather) {
+      const int64_t ec = e < e_end ? e : e_end - 1;
+      xg[r] = a.G[ec * h + ic];
+      if constexpr (GATHER) {
         const int64_t se = __builtin_amdgcn_readlane(idxv, r), re = __builtin_amdgcn_readlane(idxv, 8 + r);
-        const float sv = a.S[se * h + jc], hv = a.H[re * h + jc];
-        av[r] = ok && cj ? sv - act_t<ACT>(hv, a.act, a.alpha) : 0.f;
+        xs[r] = a.S[se * h + jc];
+        xh[r] = a.H[re * h + jc];
       } else {
-        const float sv = a.S[ec * h + jc];
-        av[r] = ok && cj ? sv : 0.f;
+        xs[r] = a.S[ec * h + jc];
       }
     }
   };
   auto store = [&](int buf) {
+    float gv[8], av[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const unsigned ok = eb_next + r < e_end ? ~0u : 0u;
+      gv[r] = __uint_as_float(__float_as_uint(xg[r]) & (ok & mi));
+      float v = xs[r];
+      if constexpr (GATHER) v -= act_t<ACT>(xh[r], a.act, a.alpha);
+      av[r] = __uint_as_float(__float_as_uint(v) & (ok & mj));
+    }
     char* base = lds + buf * 2 * kSlabB;
     const int off = (g * 64 + c) * 16;
     bf16x8 p0, p1, p2;
@@ -288,12 +299,14 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
   a.part_db = db_out ? a.part + (int64_t)p.ksplit * h * h : nullptr;
   const int grid = p.tiles * p.ksplit;
   const size_t lds = 4 * kSlabB;
-  if (act == NT_ACT_IDENTITY)
-    wgrad_kernel<NT_ACT_IDENTITY><<<grid, 256, lds, stream>>>(a);
+  if (!src)
+    wgrad_kernel<NT_ACT_IDENTITY, false><<<grid, 256, lds, stream>>>(a);
+  else if (act == NT_ACT_IDENTITY)
+    wgrad_kernel<NT_ACT_IDENTITY, true><<<grid, 256, lds, stream>>>(a);
   else if (act == NT_ACT_RELU)
-    wgrad_kernel<NT_ACT_RELU><<<grid, 256, lds, stream>>>(a);
+    wgrad_kernel<NT_ACT_RELU, true><<<grid, 256, lds, stream>>>(a);
   else
-    wgrad_kernel<-1><<<grid, 256, lds, stream>>>(a);
+    wgrad_kernel<-1, true><<<grid, 256, lds, stream>>>(a);
   NT_LAUNCH_CHECK();
   wgrad_reduce_kernel<<<grid_for(h * h, 256, 256 * 8), 256, 0, stream>>>(a.part, h * h, p.ksplit, (float*)dW_out);
   NT_LAUNCH_CHECK();
