@@ -24,6 +24,7 @@
 #include "common.hpp"
 
 namespace nt {
+int cu_count();   // csrc/update_ps.hip: the current device's CU count, queried once per device
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -33,7 +34,9 @@ constexpr int kT = 64;              // output tile edge
 constexpr int kK = 32;              // edges per step
 constexpr int kPartB = 4 * 64 * 16; // one bf16 part of a 32 x 64 slab: 4 groups x 64 cols x 16 B
 constexpr int kSlabB = 3 * kPartB;  // 12 KiB
-constexpr int kBlocksTarget = 1024;
+constexpr int kBufs = 1;           // LDS slabs: one (24 KiB, two barriers per step) -> 4 workgroups
+                                   // per CU (VGPR-bound) instead of 3 with a double buffer
+constexpr int kWgPerCu = 4;
 
 __device__ __forceinline__ void split3(const float (&x)[8], bf16x8& p0, bf16x8& p1, bf16x8& p2) {
 #pragma unroll
@@ -129,7 +132,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgArgs a) {
       if constexpr (GATHER) v -= act_t<ACT>(xh[r], a.act, a.alpha);
       av[r] = __uint_as_float(__float_as_uint(v) & (ok & mj));
     }
-    char* base = lds + buf * 2 * kSlabB;
+    char* base = lds + (kBufs > 1 ? buf : 0) * 2 * kSlabB;
     const int off = (g * 64 + c) * 16;
     bf16x8 p0, p1, p2;
     split3(gv, p0, p1, p2);
@@ -170,7 +173,7 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgArgs a) {
       load(s + 1, idx_next);
       if (s + 2 < nsteps) idx_next = load_idx(s + 2);
     }
-    const char* gb = lds + buf * 2 * kSlabB;
+    const char* gb = lds + (kBufs > 1 ? buf : 0) * 2 * kSlabB;
     const char* ab = gb + kSlabB;
     bf16x8 fa[2][3], fb[2][3];
 #pragma unroll
@@ -196,7 +199,10 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgArgs a) {
         cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[x][0], fb[z][0], cc, 0, 0, 0);
         acc[x][z] = cc;
       }
-    if (more) store(buf ^ 1);
+    if (more) {
+      if constexpr (kBufs == 1) __syncthreads();  // every wave has read the slab
+      store(buf ^ 1);
+    }
     __syncthreads();
   }
 
@@ -240,7 +246,10 @@ Plan make_plan(int64_t E, int64_t h) {
   const int tpr = (int)((h + kT - 1) / kT);
   p.tiles = tpr * tpr;
   const int64_t steps = (E + kK - 1) / kK;
-  int64_t ks = ((kBlocksTarget + p.tiles - 1) / p.tiles + 7) / 8 * 8;
+  // one round of workgroups: ksplit = the largest multiple of 8 with tiles * ksplit <= resident slots
+  const int slots = kWgPerCu * (cu_count() > 0 ? cu_count() : 256);
+  int64_t ks = slots / p.tiles / 8 * 8;
+  if (ks < 8) ks = 8;
   if (ks > steps) ks = steps > 0 ? steps : 1;
   p.chunk_steps = (int)((steps + ks - 1) / ks);
   if (p.chunk_steps < 1) p.chunk_steps = 1;
@@ -298,7 +307,7 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
   a.part = (float*)workspace;
   a.part_db = db_out ? a.part + (int64_t)p.ksplit * h * h : nullptr;
   const int grid = p.tiles * p.ksplit;
-  const size_t lds = 4 * kSlabB;
+  const size_t lds = kBufs * 2 * kSlabB;
   if (!src)
     wgrad_kernel<NT_ACT_IDENTITY, false><<<grid, 256, lds, stream>>>(a);
   else if (act == NT_ACT_IDENTITY)
