@@ -48,7 +48,7 @@ from notorch_amd.data.models.graph import DeviceLayout
 
 _IDENTITY = (NT_ACT_IDENTITY, 0.0)
 # fp32 weight gradient: "kernel" (nt_dmpnn_weight_grad) or "library" (message + split-K library GEMM)
-_WGRAD_DEFAULT = "library"
+_WGRAD_DEFAULT = "kernel"
 
 # Optional per-launch timer for the dominant kernel (bench.py sets it): a list that receives
 # (start, end) torch.cuda.Event pairs recorded on the launch stream around every nt_dmpnn_update.
