@@ -85,6 +85,9 @@ def parse():
     p.add_argument("--same-device", action="store_true",
                    help="every rank on cuda:0 (rehearsal of the N>1 code path on one GPU; not a "
                    "scaling measurement)")
+    p.add_argument("--launch-check", action="store_true",
+                   help="CPU check of the N-rank launch: ranks join a gloo group, all-reduce the "
+                   "bookkeeping scalars and rank 0 prints n_gpus; no GPU work")
     p.add_argument("--pmc-csv", default=None,
                    help="comma-separated rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE counter CSVs of the "
                    "same command (tools/profile.sh) to fill roofline.traffic")
@@ -285,8 +288,9 @@ def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
         visible = len(os.sched_getaffinity(0))
     except AttributeError:
         visible = os.cpu_count() or 1
-    share = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, visible)
-    thread_counts = sorted({1, share, visible})
+    share = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16, visible)
+    thread_counts = sorted({1, share})  # more threads than the per-GPU share only oversubscribe
+    host = host_cpu_info()
 
     def one():
         with torch.inference_mode():
@@ -297,11 +301,9 @@ def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
     prev = torch.get_num_threads()
     for P in thread_counts:
         torch.set_num_threads(P)
-        over = P > share  # more threads than the box gives this process: one timed run suffices
-        if not over:
-            one()  # warm-up
+        one()  # warm-up
         times, t_start = [], time.perf_counter()
-        while (time.perf_counter() - t_start < budget_s and len(times) < 200) or len(times) < (1 if over else 3):
+        while (time.perf_counter() - t_start < budget_s and len(times) < 200) or len(times) < 3:
             t0 = time.perf_counter()
             one()
             times.append(time.perf_counter() - t0)
@@ -315,12 +317,37 @@ def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
         "cores": best_P,
         "kind": "port",
         "by_threads": {str(p): {"value": E * job.depth / m, "ms": m * 1e3, "runs": n} for p, (m, n) in res.items()},
+        "host": dict(host, cpus_visible=visible),
         "sample": f"oracle/dmpnn_ref.py (ATen CPU restatement of chemprop.py+agg.py) on {sample} "
-        f"(V={G.num_nodes}, E={E}), fp32, torch.set_num_threads(P) for P in {sorted(res)} (P = 1, "
-        f"the box's per-GPU CPU share OMP_NUM_THREADS={share}, and every CPU in sched_getaffinity = "
-        f"{visible}); median of runs within {budget_s:.0f} s each after 1 warm-up; value and cores = "
-        f"the fastest P",
+        f"(V={G.num_nodes}, E={E}), fp32, torch.set_num_threads(P) for P in {sorted(res)} (P = 1 and "
+        f"the box's per-GPU CPU share OMP_NUM_THREADS={share}); host {host.get('model', '?')}, "
+        f"{host.get('physical_cores', '?')} physical cores ({visible} CPUs visible to this process); "
+        f"median of runs within {budget_s:.0f} s each after 1 warm-up; value and cores = the fastest P",
     }
+
+
+def host_cpu_info():
+    """Physical core count and model of the host (lscpu), for the cpu_baseline's `cores` context."""
+    import subprocess
+
+    info = {}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+    except (OSError, subprocess.SubprocessError):
+        return info
+    kv = {}
+    for line in out.splitlines():
+        if ":" in line:
+            k, v = line.split(":", 1)
+            kv[k.strip()] = v.strip()
+    try:
+        info["physical_cores"] = int(kv["Core(s) per socket"]) * int(kv["Socket(s)"])
+        info["threads_per_core"] = int(kv.get("Thread(s) per core", "1"))
+    except (KeyError, ValueError):
+        pass
+    if "Model name" in kv:
+        info["model"] = kv["Model name"]
+    return info
 
 
 WS_BS = None  # (weights, biases) of the headline block on the host, for the CPU baseline
@@ -495,9 +522,32 @@ def summary(res, args, env, pmc_csv=None):
     }
 
 
+def launch_check(args, env):
+    """--launch-check: the rank bookkeeping of an N-rank run without a GPU (gloo): every rank joins
+    the group, the units / max-time all-reduces run, rank 0 prints the line's rank fields."""
+    if env.distributed:
+        dist.init_process_group("gloo")
+    units, secs, rate = aggregate_throughput(1000.0 * (env.rank + 1), 1.0 + env.rank)
+    if env.rank == 0:
+        print(json.dumps({"n_gpus": env.world_size, "value": rate, "units": units, "max_seconds": secs,
+                          "launch_check": True}), flush=True)
+    if env.distributed:
+        dist.destroy_process_group()
+
+
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # `python bench.py --gpus N` without a launcher: start the N rank processes here, before
+        # anything touches the GPU (children, never an exec), and exit with their status.
+        from notorch_amd.shard import launch_local_ranks
+
+        sys.exit(launch_local_ranks([os.path.abspath(__file__), *sys.argv[1:]], args.gpus))
     env = dist_env()
+    if env.world_size != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={env.world_size} ranks were launched")
+    if args.launch_check:
+        return launch_check(args, env)
     dev = torch.device("cuda", 0 if args.same_device else env.local_rank)
     if env.distributed:
         torch.cuda.set_device(dev)
@@ -543,7 +593,7 @@ def main():
             del r2
 
     cpu = None
-    if not args.no_cpu_baseline and env.world_size == 1 and env.rank == 0:
+    if not args.no_cpu_baseline and env.rank == 0:
         cpu = cpu_baseline(job, res["embedding"], args.cpu_seconds)
     if env.rank == 0:
         sharded = res["kind"] == "qm9v"

@@ -22,20 +22,12 @@ struct UpdateArgs {
   hipStream_t stream;
 };
 
-// LDS-DMA streamed fp32 MFMA kernel (update_glds.hip); requires h % 4 == 0, NT <= 32, 16-B aligned
-// H, S, H_out, b.
-int launch_update_glds(const UpdateArgs& a);
-
 // bf16x6 fp32-emulation kernel (update_x6.hip): h % 4 == 0 and 97 <= h <= 512.
 bool x6_supported(int64_t h);
 size_t x6_image_bytes(int64_t h);
 int pack_weight_x6(const float* W, int64_t nlayers, int64_t h, int64_t layer_stride_bytes, void* Wx,
                    hipStream_t stream);
 int launch_update_x6(const UpdateArgs& a);  // a.Wp points at the x6 image
-
-// Warp-specialised producer/consumer bf16x6 kernel (update_pc.hip): h % 4 == 0, 97 <= h <= 320.
-bool pc_supported(int64_t h);
-int launch_update_pc(const UpdateArgs& a);  // a.Wp points at the x6 image
 
 // A-stationary bf16x6 kernel (update_as.hip, 16x16x32 MFMA): h % 4 == 0, h <= 304.
 bool as_supported(int64_t h);

@@ -39,8 +39,7 @@ constexpr int kWaves = 4;
 
 // kernel selection for A/B runs (read per call):
 //   NT_UPDATE_KERNEL = as (default: A-stationary bf16x6) | x6 (LDS-ring bf16x6)
-//                      | pc (producer/consumer bf16x6)
-//                      | glds | ring | stream | tile (exact fp32 MFMA)
+//                      | ring | stream | tile (exact fp32 MFMA)
 static char update_kernel_choice() {
 #ifdef NT_DIAG
   const char* v = getenv("NT_UPDATE_KERNEL");
@@ -595,15 +594,7 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
     return launch_update_as(a);
   }
-#ifdef NT_DIAG
-  if (vec && choice == 'p' && pc_supported(h)) {
-    UpdateArgs a{(const float*)H, (const float*)S, src, rev, (const char*)Wp + f32_image_bytes(h),
-                 (const float*)b, V, E, h, g.KB, g.NT, residual, act, act_alpha, (float*)H_out,
-                 stream};
-    return launch_update_pc(a);
-  }
-#endif
-  if (vec && (choice == 'x' || choice == 'p' || choice == 'a') && x6_supported(h)) {
+  if (vec && (choice == 'x' || choice == 'a') && x6_supported(h)) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, (const char*)Wp + f32_image_bytes(h),
                  (const float*)b, V, E, h, g.KB, g.NT, residual, act, act_alpha, (float*)H_out,
                  stream};
@@ -614,11 +605,6 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                  g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
     return launch_update_ring(a);
-  }
-  if (vec && (choice == 'g' || choice == 'x' || choice == 'p' || choice == 'a')) {
-    UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
-                 g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
-    return launch_update_glds(a);
   }
 #endif
   // 64-edge tiles while two workgroups still fit one CU's LDS (h <= 304), else 32-edge tiles.

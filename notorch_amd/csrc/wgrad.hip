@@ -278,6 +278,9 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
   NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_weight_grad: fp32 only");
   NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
   NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  // row indices are narrowed to int for the lane broadcasts
+  NT_REQUIRE(V < ((int64_t)1 << 31) && E < ((int64_t)1 << 31), NT_EUNSUPPORTED,
+             "nt_dmpnn_weight_grad: V and E must be < 2^31");
   NT_REQUIRE((src == nullptr) == (rev == nullptr), NT_EINVAL, "src and rev: both or neither");
   NT_REQUIRE(dW_out, NT_EINVAL, "NULL dW_out");
   hipStream_t stream = as_stream(stream_);

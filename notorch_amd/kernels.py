@@ -469,7 +469,14 @@ def weight_grad(G: Tensor, H: Tensor | None, S: Tensor, src: Tensor | None, rev:
         if t is not None and not t.is_contiguous():
             raise ValueError(f"weight_grad: {n_} must be contiguous")
     lib = _lib.load()
-    nbytes = lib.nt_dmpnn_weight_grad_workspace(E, h)
+    # the workspace is sized by the plan of the launch device (its CU count): query under its guard
+    if dev.index is not None and dev.index != torch.cuda.current_device():
+        with torch.cuda.device(dev):
+            nbytes = lib.nt_dmpnn_weight_grad_workspace(E, h)
+    else:
+        nbytes = lib.nt_dmpnn_weight_grad_workspace(E, h)
+    if nbytes < 0:
+        raise ValueError(f"weight_grad: bad sizes E={E} h={h}")
     ws = torch.empty((max(nbytes, 4) + 3) // 4, dtype=torch.float32, device=dev)
     dW = torch.empty(h, h, dtype=torch.float32, device=dev)
     db = torch.empty(h, dtype=torch.float32, device=dev) if bias else None

@@ -457,33 +457,45 @@ def _torch_block_layerwise(Xv, Xe, edge_index, rev, weights, biases, act_mods, r
 class LayerwiseBlockFunction(torch.autograd.Function):
     """Kernel forward (block_forward_layerwise); backward by recomputing the same math in PyTorch
     device ops under autograd (any activation module, per-layer dropout masks regenerated by the
-    hash kernel)."""
+    hash kernel).  The activation modules' own parameters (e.g. nn.PReLU's slope) are inputs of
+    the Function and get their gradients from the recompute; the RNG state of the forward is
+    restored for the recompute, so a stochastic activation (nn.RReLU in training) draws the same
+    values in both."""
 
     @staticmethod
-    def forward(ctx, Xv, Xe, edge_index, rev, lay, acts, drops, reduce, residual, nlayers, *params):
-        weights, biases = list(params[:nlayers]), list(params[nlayers:])
+    def forward(ctx, Xv, Xe, edge_index, rev, lay, acts, drops, reduce, residual, nlayers, nact, *params):
+        weights, biases = list(params[:nlayers]), list(params[nlayers:2 * nlayers])
+        dev = Xv.device
+        ctx.rng = (torch.get_rng_state(), torch.cuda.get_rng_state(dev))
         node, H = block_forward_layerwise(Xv, Xe, edge_index[0].contiguous(), rev, lay, acts, weights,
                                           biases, drops, reduce, residual)
         ctx.save_for_backward(Xv, Xe, edge_index, rev, *[p if p is not None else torch.empty(0) for p in params])
-        ctx.cfg = (acts, drops, reduce, residual, nlayers, [p is None for p in params])
+        ctx.cfg = (acts, drops, reduce, residual, nlayers, nact, [p is None for p in params])
         return node, H
 
     @staticmethod
     def backward(ctx, dnode, dH):
-        acts, drops, reduce, residual, nlayers, is_none = ctx.cfg
+        acts, drops, reduce, residual, nlayers, nact, is_none = ctx.cfg
         Xv, Xe, edge_index, rev, *rest = ctx.saved_tensors
         params = [None if n else p for p, n in zip(rest, is_none)]
         need = ctx.needs_input_grad
-        with torch.enable_grad():
+        nfix = 11  # inputs of forward() before *params
+        dev = Xv.device
+        with torch.enable_grad(), torch.random.fork_rng(devices=[dev]):
+            torch.set_rng_state(ctx.rng[0])
+            torch.cuda.set_rng_state(ctx.rng[1], dev)
             Xv_ = Xv.detach().requires_grad_(need[0])
             Xe_ = Xe.detach().requires_grad_(need[1])
-            ps = [None if p is None else p.detach().requires_grad_(True) for p in params]
+            ps = [None if p is None else p.detach().requires_grad_(True) for p in params[:2 * nlayers]]
+            # activation parameters: the module's own tensors (the recompute calls the modules)
+            aps = params[2 * nlayers:]
             E, h = Xe.shape
             masks = [None if d is None else K.dropout_residual(torch.ones_like(Xe), d[0], d[1], dropout_offset(l, E, h))
                      for l, d in enumerate(drops)]
             node, H = _torch_block_layerwise(Xv_, Xe_, edge_index, rev, ps[:nlayers], ps[nlayers:],
                                              [a[0] for a in acts], reduce, residual, masks)
-            leaves = [t for t in [Xv_, Xe_] + ps if t is not None and t.requires_grad]
+            act_leaves = [p for i, p in enumerate(aps) if p is not None and need[nfix + 2 * nlayers + i]]
+            leaves = [t for t in [Xv_, Xe_] + ps if t is not None and t.requires_grad] + act_leaves
             outs, grads = [], []
             for o, g in ((node, dnode), (H, dH)):
                 if g is not None:
@@ -493,7 +505,9 @@ class LayerwiseBlockFunction(torch.autograd.Function):
         it = iter(got)
         res_inputs = [next(it) if need[0] else None, next(it) if need[1] else None]
         res_params = [None if p is None else next(it) for p in ps]
-        return (*res_inputs, None, None, None, None, None, None, None, None, *res_params)
+        res_params += [next(it) if p is not None and need[nfix + 2 * nlayers + i] else None
+                       for i, p in enumerate(aps)]
+        return (*res_inputs, None, None, None, None, None, None, None, None, None, *res_params)
 
 
 def backward_layout(lay: DeviceLayout, src: Tensor, rev: Tensor, V: int, E: int) -> tuple:

@@ -14,7 +14,10 @@ Differences by design:
   (``nt_dropout_residual``) seeded from torch's default generator, not from torch's Philox stream:
   same distribution and scaling as ``nn.Dropout`` (keep with probability 1 - p, scale 1 / (1 - p)),
   different draws;
-* ``act`` must be one of ReLU, Identity, LeakyReLU, ELU, GELU, SiLU, Tanh, Sigmoid.
+* ``act`` may be any activation module (chemprop.py:17,24,37).  ReLU, Identity, LeakyReLU, ELU,
+  GELU, SiLU, Tanh and Sigmoid are fused into the kernels; any other module (e.g. ``nn.PReLU``,
+  whose parameters train) runs as its own elementwise op between the segment-reduce and update
+  kernels (``_engine.block_forward_layerwise``).
 """
 from __future__ import annotations
 
@@ -190,9 +193,12 @@ class ChempropBlock(nn.Module):
             # the layer-by-layer device path (_engine.block_forward_layerwise)
             acts = [(layer.act, c) for layer, c in zip(layers, codes)]
             if needs_grad:
+                # the activation modules' parameters (nn.PReLU's slope ...) train through the
+                # Function's recompute backward; shared modules contribute their tensors once
+                act_params = list({id(p): p for l in layers for p in l.act.parameters()}.values())
                 node, H = _engine.LayerwiseBlockFunction.apply(
                     Xv, Xe, G.edge_index, rev, lay, acts, drops, self.reduce, residual, len(layers),
-                    *weights, *biases,
+                    len(act_params), *weights, *biases, *act_params,
                 )
             else:
                 node, H = _engine.block_forward_layerwise(

@@ -56,6 +56,64 @@ def dist_env() -> DistEnv:
     )
 
 
+def _free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_local_ranks(argv: list[str], nprocs: int, master_port: int | None = None,
+                       poll_s: float = 0.2) -> int:
+    """Start ``nprocs`` rank processes of ``[sys.executable, *argv]`` on this node, the way
+    ``torch.distributed.run --nnodes 1 --nproc-per-node nprocs --master-addr 127.0.0.1`` would
+    (RANK / LOCAL_RANK / WORLD_SIZE / LOCAL_WORLD_SIZE / MASTER_ADDR / MASTER_PORT in each child's
+    environment), and wait for them.  Children inherit stdout / stderr, so rank 0's output is
+    relayed as it is written.  Returns 0 when every rank exits 0; otherwise the first failing
+    rank's exit status (a signal -> 128 + signo), after terminating the ranks still running (by
+    their own PIDs).  The caller must not have touched the GPU: the children are new processes
+    (never an exec of the caller)."""
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    if nprocs < 1:
+        raise ValueError("nprocs must be >= 1")
+    port = master_port or _free_port()
+    procs = []
+    for r in range(nprocs):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
+                   LOCAL_WORLD_SIZE=str(nprocs), GROUP_RANK="0", MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, *argv], env=env))
+    rc = 0
+    try:
+        live = list(procs)
+        while live:
+            for p in list(live):
+                code = p.poll()
+                if code is None:
+                    continue
+                live.remove(p)
+                if code != 0 and rc == 0:
+                    rc = code if code > 0 else 128 - code
+                    for q in live:
+                        q.send_signal(signal.SIGTERM)
+            if live:
+                time.sleep(poll_s)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    p.wait(timeout=30)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+    return rc
+
+
 def aggregate_throughput(local_units: float, local_seconds: float, device=None) -> tuple[float, float, float]:
     """(total_units, max_seconds, aggregate_rate) over all ranks; identity when not distributed.
 

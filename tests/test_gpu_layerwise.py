@@ -108,3 +108,65 @@ def test_standalone_layer_generic_activation():
     with torch.no_grad():
         out = layer.to(DEV)(H.to(DEV), Xv.to(DEV), G.edge_index.to(DEV), G.rev_index.to(DEV))
     assert_parity(out, ref, FP32_NORM_TOL, "layer")
+
+
+def test_prelu_slope_trains():
+    """nn.PReLU's slope is a parameter of the activation module (the reference accepts any
+    nn.Module class, chemprop.py:17,24): its gradient comes back through the layer-by-layer
+    Function and matches fp64 oracle autograd, next to dXv, dXe and every dW / db."""
+    from notorch_amd.nn import ChempropBlock
+
+    G = _graph(24, seed=8)
+    torch.manual_seed(4)
+    h = 48
+    Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
+    blk = ChempropBlock(hidden_dim=h, act=nn.PReLU, depth=2).train()
+    for m in blk._chemprop_layers():
+        nn.init.constant_(m.act.weight, 0.3)
+    Ws, bs = dmpnn_ref.block_params(blk)
+    Xv64, Xe64 = Xv.double().requires_grad_(), Xe.double().requires_grad_()
+    W64 = [w.double().requires_grad_() for w in Ws]
+    b64 = [b.double().requires_grad_() for b in bs]
+    acts64 = [nn.PReLU(init=0.3).double() for _ in range(2)]
+    n64, e64 = _ref_layers(G, Xv64, Xe64, W64, b64, acts64)
+    (n64.sum() + (e64 ** 2).mean()).backward()
+
+    blk = blk.to(DEV)
+    Xv_d, Xe_d = Xv.to(DEV).requires_grad_(), Xe.to(DEV).requires_grad_()
+    out = blk(G.update(node_feats=Xv_d, edge_feats=Xe_d).to(DEV))
+    (out.node_feats.sum() + (out.edge_feats ** 2).mean()).backward()
+    assert_parity(Xv_d.grad, Xv64.grad, FP32_NORM_TOL * 2, "dXv")
+    assert_parity(Xe_d.grad, Xe64.grad, FP32_NORM_TOL * 2, "dXe")
+    for i, m in enumerate(blk._chemprop_layers()):
+        assert m.act.weight.grad is not None, f"PReLU slope of layer {i} got no gradient"
+        assert_parity(m.act.weight.grad, acts64[i].weight.grad, FP32_NORM_TOL * 2, f"dslope{i}")
+        assert_parity(m.linear.weight.grad, W64[i].grad, FP32_NORM_TOL * 2, f"dW{i}")
+
+
+def test_rrelu_training_backward_replays_forward_draws():
+    """A stochastic activation (nn.RReLU in training mode) draws its slopes once in the forward; the
+    recompute backward replays the same draws, so the gradient is that of the function the forward
+    computed: check d(sum H_d)/dXe against torch autograd on the same forward with the same RNG."""
+    from notorch_amd.nn import ChempropBlock
+    from notorch_amd.nn.gnn import _engine
+
+    G = _graph(16, seed=9, rev_offset="edges")
+    torch.manual_seed(5)
+    h = 32
+    Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
+    blk = ChempropBlock(hidden_dim=h, act=nn.RReLU, depth=2).train().to(DEV)
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
+    Xe_d = Gd.edge_feats.clone().requires_grad_()
+    torch.cuda.manual_seed(11)
+    out = blk(Gd.update(edge_feats=Xe_d))
+    out.edge_feats.sum().backward()
+    # the same forward in device torch ops from the same RNG state
+    Xe_t = Gd.edge_feats.clone().requires_grad_()
+    layers = blk._chemprop_layers()
+    torch.cuda.manual_seed(11)
+    _, H = _engine._torch_block_layerwise(Gd.node_feats, Xe_t, Gd.edge_index, Gd.rev_index,
+                                          [l.linear.weight for l in layers], [l.linear.bias for l in layers],
+                                          [l.act for l in layers], "sum", True, [None, None])
+    assert_parity(out.edge_feats.detach(), H.detach(), FP32_NORM_TOL, "H (same draws)")
+    H.sum().backward()
+    assert_parity(Xe_d.grad, Xe_t.grad, FP32_NORM_TOL, "dXe")

@@ -112,3 +112,48 @@ def test_gloo_world2_sharded_forward_pipeline():
     assert sizes[0][0] == 0 and sizes[0][1] == sizes[1][0] and sizes[1][1] == 48
     assert sizes[0][2] + sizes[1][2] == G.num_nodes and sizes[0][3] + sizes[1][3] == G.num_edges
     np.testing.assert_allclose(out["parts"], ref, rtol=1e-5, atol=1e-5)
+
+
+def test_bench_gpus_n_launches_its_own_ranks():
+    """`python bench.py --gpus 2` with no external launcher starts 2 rank processes itself (before
+    any GPU call) and relays rank 0's line: n_gpus = 2, units summed and time maxed over ranks."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # only rank 0 prints
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["units"] == 3000.0 and d["max_seconds"] == 2.0
+
+
+def test_bench_rejects_world_size_mismatch():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--launch-check"],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode != 0 and "WORLD_SIZE=1" in r.stderr
+
+
+def test_launcher_propagates_a_failing_rank(tmp_path):
+    """One rank exiting non-zero makes launch_local_ranks return non-zero and stop the others."""
+    import time
+
+    from notorch_amd.shard import launch_local_ranks
+
+    script = tmp_path / "w.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "assert os.environ['WORLD_SIZE'] == '3' and os.environ['MASTER_ADDR'] == '127.0.0.1'\n"
+                      "sys.exit(7) if r == 1 else time.sleep(120)\n")
+    t0 = time.time()
+    rc = launch_local_ranks([str(script)], 3)
+    assert rc == 7 and time.time() - t0 < 60
