@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define NT_ABI_VERSION 1
+#define NT_ABI_VERSION 2
 
 #if defined(NT_BUILD)
 #define NT_API __attribute__((visibility("default")))
@@ -81,13 +81,15 @@ NT_API int nt_embed_bag(const void* table, int64_t num_types, const int64_t* idx
  *                               Xe[e] = sum_j edge_table[edge_types[e][j]]
  *   S[v]  = reduce_{e: dst e = v} act(H0[e])   if S != NULL (then seg_ptr / perm = dst CSR)
  * Bit-identical to nt_embed_bag twice followed by nt_dmpnn_init.
+ * amax_out (fp32 only, may be NULL): 2 device floats, atomically raised to max|H0| and max|S| (the
+ * caller zero-fills them); the fp32 layer kernel scales its fp16 split by them.
  */
 NT_API int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_types,
                                const int64_t* node_types, int64_t kv, const void* edge_table,
                                int64_t num_edge_types, const int64_t* edge_types, int64_t ke,
                                const int64_t* src, const int32_t* seg_ptr, const int32_t* perm,
                                int64_t V, int64_t E, int64_t h, int act, float act_alpha, int reduce,
-                               int dtype, void* H0, void* S, void* stream);
+                               int dtype, void* H0, void* S, float* amax_out, void* stream);
 
 /*
  * Host-side collate of B per-molecule graphs (BatchedGraph.from_graphs, notorch/data/models/
@@ -130,10 +132,20 @@ NT_API int nt_csr_build(const int64_t* idx, int64_t n, int64_t nseg, int32_t* se
  *   H0[e] = Xv[src[e]] + Xe[e]                                  (chemprop.py:82-83)
  *   S[v]  = reduce_{e: dst[e]=v} act(H0[e])  if S != NULL       (chemprop.py:37-39, layer 0)
  * src = edge_index[0] (int64, E); (seg_ptr, perm) = nt_csr_build(edge_index[1], E, V).
+ * amax_out (fp32 only, may be NULL): 2 device floats, atomically raised to max|H0| and max|S| (S
+ * only when S != NULL); the caller zero-fills them.  They are the amax_in of layer 0's
+ * nt_dmpnn_update_fused.
  */
 NT_API int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src, const int32_t* seg_ptr,
                   const int32_t* perm, int64_t V, int64_t E, int64_t h, int act, float act_alpha,
-                  int reduce, int dtype, void* H0, void* S, void* stream);
+                  int reduce, int dtype, void* H0, void* S, float* amax_out, void* stream);
+
+/*
+ * max |X| over n fp32 elements, atomically max-ed into *out (device float; non-negative floats
+ * order like their bit patterns, so the caller zero-fills it first).  The amax_in of a layer whose
+ * inputs did not come from nt_dmpnn_init / nt_dmpnn_update_fused.
+ */
+NT_API int nt_absmax(const void* X, int64_t n, int dtype, float* out, void* stream);
 
 /*
  * Segmented reduction over CSR segments:
@@ -183,17 +195,29 @@ NT_API int nt_dmpnn_update(const void* H, const void* S, const int64_t* src, con
 
 /*
  * Tile plan for nt_dmpnn_update_fused: cuts the dst-sorted edge order (positions of the
- * nt_csr_build(edge_index[1]) permutation) into tiles of at most 64 positions at node boundaries,
- * so every node's in-edges fall in one tile.  Tile k starts at dst_ptr[first v with
- * dst_ptr[v] >= k L], L = 65 - max(max_in_degree, 1); tile_ptr[ntiles] = E.
- * dst_sorted[p] = the node whose in-edge sits at position p.
- * max_in_degree must be <= 32 (graphs with hubs use the unfused nt_dmpnn_update +
- * nt_segment_reduce path); ntiles must equal nt_dmpnn_tile_count(E, max_in_degree).
+ * nt_csr_build(edge_index[1]) permutation) at node boundaries, so every node's in-edges fall in one
+ * tile.  Tile k starts at dst_ptr[first v with dst_ptr[v] >= k stride]; tile_ptr[ntiles] = E; a
+ * tile then holds at most stride + max_in_degree - 1 positions.  dst_sorted[p] = the node whose
+ * in-edge sits at position p.
+ * nt_dmpnn_tile_stride(E, max_in_degree, rows, ncu): the stride for tiles of at most `rows`
+ * positions (rows = nt_dmpnn_fused_tile_rows), balanced so that the tile count is a whole number of
+ * rounds of ncu tiles (ncu <= 0: the largest stride); 0 when max_in_degree > rows.
+ * ntiles must equal nt_dmpnn_tile_count(E, stride).  Graphs whose max in-degree exceeds 32 take the
+ * unfused path (nt_dmpnn_update_fused without a plan + nt_segment_reduce).
  * Replaces the per-layer segmentation implied by scatter(..., dest) (chemprop.py:39, :86).
  */
-NT_API int64_t nt_dmpnn_tile_count(int64_t E, int max_in_degree);
-NT_API int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, int max_in_degree,
+NT_API int64_t nt_dmpnn_tile_stride(int64_t E, int max_in_degree, int rows, int ncu);
+NT_API int64_t nt_dmpnn_tile_count(int64_t E, int64_t stride);
+NT_API int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, int64_t stride,
                               int32_t* tile_ptr, int64_t ntiles, int32_t* dst_sorted, void* stream);
+
+/*
+ * Row capacity of one nt_dmpnn_update_fused tile for a layer of hidden size h, activation act and
+ * aggregation (reduce, agg_act): the plan passed with that layer must have tiles of at most this
+ * many rows.  fp32: 128 for h <= 384 with act = relu, reduce = sum and agg_act in {relu,
+ * identity}, else 64; bf16: 64.
+ */
+NT_API int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, int agg_act);
 
 /*
  * One D-MPNN layer fused with the aggregation that consumes it (chemprop.py:36-43 of layer l,
@@ -201,16 +225,23 @@ NT_API int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, int 
  * final node scatter of chemprop.py:86):
  *   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b
  *   S_out[v] = reduce_{e: dst[e]=v} agg_act(H_out[e])      (ascending e; empty segment -> 0)
- * (tile_ptr, ntiles, dst_sorted) = nt_dmpnn_tile_plan; perm = the dst CSR permutation.
- * With tile_ptr = NULL (and perm, dst_sorted, S_out = NULL) only H_out is computed (same result as
- * nt_dmpnn_update, persistent producer/consumer kernel).  Requires h % 4 == 0, h <= 304,
- * 16-byte aligned feature pointers.  S_out must not alias S.
+ * (tile_ptr, ntiles, dst_sorted) = nt_dmpnn_tile_plan with tiles of at most tile_rows <=
+ * nt_dmpnn_fused_tile_rows(h, dtype, act, reduce, agg_act) rows; max_in_degree >= the graph's largest
+ * in-degree (<= 32); perm = the dst CSR permutation.  Nodes without in-edges are not written (the
+ * caller zero-fills S_out).  With tile_ptr = NULL (and perm, dst_sorted, S_out = NULL) only H_out
+ * is computed.
+ * fp32 (h % 4 == 0, any h): two-part fp16 split on fp16 MFMA (fp32 accuracy); amax_in = 2 device
+ * floats >= max|H|, max|S| (from nt_dmpnn_init / the previous layer's amax_out / nt_absmax);
+ * amax_out (may be NULL) = 2 zero-filled device floats raised to max|H_out|, max|S_out|.
+ * bf16 (h % 8 == 0, h <= 512): bf16 MFMA, tile_rows <= 64, amax ignored.
+ * 16-byte aligned feature pointers; S_out must not alias S.
  */
 NT_API int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* src, const int64_t* rev,
                                  const void* Wp, const void* b, int64_t V, int64_t E, int64_t h,
                                  int residual, int act, float act_alpha, const int32_t* tile_ptr,
-                                 int64_t ntiles, const int32_t* perm, const int32_t* dst_sorted,
-                                 int reduce, int agg_act, float agg_alpha, int dtype, void* H_out,
+                                 int64_t ntiles, int tile_rows, int max_in_degree, const int32_t* perm,
+                                 const int32_t* dst_sorted, int reduce, int agg_act, float agg_alpha,
+                                 int dtype, const float* amax_in, float* amax_out, void* H_out,
                                  void* S_out, void* stream);
 
 /*
@@ -308,7 +339,7 @@ NT_API int nt_gather_rows_arg(const void* base, const void* X, const int64_t* id
  * for dA = G W).  The persistent bf16x6 MFMA layer kernel without gathers (fp32-accurate).
  * fp32 only; h % 4 == 0, h <= 304; 16-byte aligned; out != X. */
 NT_API int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const void* Wp, int dtype,
-                                 void* out, void* stream);
+                                 const float* amax_in, void* out, void* stream);
 
 /* Weight and bias gradient of one layer (backward of nn.Linear at chemprop.py:26,41, trained through
  * lightning_models/model.py:224-241; the reference runs it as ATen addmm's autograd), with the

@@ -17,7 +17,7 @@ _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # environment variables, ablation / stamp builds); the default is the shipping library.
 DIAG = os.environ.get("NT_LIB", "") == "diag"
 LIB_PATH = os.path.join(_LIB_DIR, "libnotorch_amd_diag.so" if DIAG else "libnotorch_amd.so")
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 NT_F32, NT_BF16 = 0, 1
 NT_SUM, NT_MEAN, NT_MAX, NT_MIN = 0, 1, 2, 3
@@ -49,7 +49,7 @@ SIGNATURES: dict[str, tuple] = {
     "nt_dmpnn_init_embed": (
         _c_int,
         [_vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64,
-         _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp],
+         _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp, _vp],
     ),
     "nt_collate_graphs": (
         _c_int,
@@ -60,8 +60,9 @@ SIGNATURES: dict[str, tuple] = {
     "nt_csr_build": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_size, _vp, _vp]),
     "nt_dmpnn_init": (
         _c_int,
-        [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp],
+        [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp, _vp],
     ),
+    "nt_absmax": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp]),
     "nt_segment_reduce": (
         _c_int,
         [_vp, _vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp],
@@ -76,12 +77,14 @@ SIGNATURES: dict[str, tuple] = {
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp],
     ),
-    "nt_dmpnn_tile_count": (_c_i64, [_c_i64, _c_int]),
-    "nt_dmpnn_tile_plan": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
+    "nt_dmpnn_tile_stride": (_c_i64, [_c_i64, _c_int, _c_int, _c_int]),
+    "nt_dmpnn_tile_count": (_c_i64, [_c_i64, _c_i64]),
+    "nt_dmpnn_tile_plan": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp, _vp]),
+    "nt_dmpnn_fused_tile_rows": (_c_int, [_c_i64, _c_int, _c_int, _c_int, _c_int]),
     "nt_dmpnn_update_fused": (
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _vp, _c_i64,
-         _vp, _vp, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp],
+         _c_int, _c_int, _vp, _vp, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp, _vp, _vp],
     ),
     "nt_node_scores": (
         _c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _vp, _c_f32, _c_int, _vp, _vp],
@@ -106,7 +109,7 @@ SIGNATURES: dict[str, tuple] = {
          _vp],
     ),
     "nt_gather_rows_arg": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_int, _vp, _vp]),
-    "nt_dmpnn_dense_matmul": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, _vp]),
+    "nt_dmpnn_dense_matmul": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, _vp, _vp]),
     "nt_dmpnn_weight_grad_workspace": (_c_i64, [_c_i64, _c_i64]),
     "nt_dmpnn_weight_grad": (
         _c_int,

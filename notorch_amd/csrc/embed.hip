@@ -18,6 +18,10 @@
 #include "rows.hpp"
 
 namespace nt {
+int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);  // update_pk.hip
+}
+
+namespace nt {
 int cu_count();  // update_ps.hip
 
 namespace {
@@ -124,9 +128,10 @@ template <typename T, bool VEC, int R, int ACT, int KV, int KE, bool LDS = false
 __global__ void __launch_bounds__(LDS ? kLdsThreads : 256, LDS ? 2 : 1) init_embed_aggregate_k(
     EmbedArgs a, const int64_t* __restrict__ src, const int32_t* __restrict__ seg_ptr,
     const int32_t* __restrict__ perm, int64_t V, int64_t h, int act, float alpha,
-    T* __restrict__ H0, T* __restrict__ S) {
+    T* __restrict__ H0, T* __restrict__ S, float* __restrict__ amax) {
   constexpr int N = Piece<T, VEC>::N;
   constexpr int U = LDS ? 2 : 4;  // LDS rows are cheap: fewer edges in flight, more waves
+  float mh = 0.f, ms = 0.f;       // max |H0|, max |S| of this lane (amax != NULL)
   const T* Tv = (const T*)a.Tv;
   const T* Te = (const T*)a.Te;
   if constexpr (LDS) {
@@ -197,13 +202,30 @@ __global__ void __launch_bounds__(LDS ? kLdsThreads : 256, LDS ? 2 : 1) init_emb
         for (int i = 0; i < N; ++i) x[i] = as_stored<T>(as_stored<T>(xv[i]) + as_stored<T>(xe[i]));
         Piece<T, VEC>::store(H0 + e[u] * h + c, x);
 #pragma unroll
-        for (int i = 0; i < N; ++i) r[i].push(act_t<ACT>(x[i], act, alpha));
+        for (int i = 0; i < N; ++i) {
+          mh = fmaxf(mh, fabsf(x[i]));
+          r[i].push(act_t<ACT>(x[i], act, alpha));
+        }
       }
     }
     float y[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) y[i] = r[i].result();
+    for (int i = 0; i < N; ++i) {
+      y[i] = r[i].result();
+      ms = fmaxf(ms, fabsf(y[i]));
+    }
     Piece<T, VEC>::store(S + v * h + c, y);
+  }
+  if (amax) {  // one atomic max per wave (non-negative floats order like their bits)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      mh = fmaxf(mh, __shfl_xor(mh, o));
+      ms = fmaxf(ms, __shfl_xor(ms, o));
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(mh));
+      atomicMax(reinterpret_cast<unsigned int*>(amax + 1), __float_as_uint(ms));
+    }
   }
 }
 
@@ -225,13 +247,14 @@ __global__ void __launch_bounds__(256) init_embed_only(EmbedArgs a, const int64_
 template <typename T, bool VEC>
 int launch_init_embed(const EmbedArgs& a, const int64_t* src, const int32_t* seg_ptr,
                       const int32_t* perm, int64_t V, int64_t E, int64_t h, int act, float alpha,
-                      int reduce, void* H0, void* S, hipStream_t stream) {
+                      int reduce, void* H0, void* S, float* amax, hipStream_t stream) {
   constexpr int N = Piece<T, VEC>::N;
   if (S == nullptr) {
     if (E == 0) return NT_OK;
     init_embed_only<T, VEC><<<grid_for(E * (h / N), 256, 256 * 32), 256, 0, stream>>>(
         a, src, E, h, (T*)H0);
     NT_LAUNCH_CHECK();
+    if (amax) return fk_absmax((const float*)H0, E * h, amax, stream);
     return NT_OK;
   }
   if (V == 0) return NT_OK;
@@ -246,10 +269,10 @@ int launch_init_embed(const EmbedArgs& a, const int64_t* src, const int32_t* seg
   do {                                                                                           \
     if (lds)                                                                                     \
       init_embed_aggregate_k<T, VEC, R_, A_, 7, 2, true><<<grid_lds, kLdsThreads, 0, stream>>>(  \
-          a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S);                               \
+          a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S, amax);                         \
     else if (k72)                                                                                \
       init_embed_aggregate_k<T, VEC, R_, A_, 7, 2><<<grid, 256, 0, stream>>>(                    \
-          a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S);                               \
+          a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S, amax);                         \
     else                                                                                         \
       init_embed_aggregate<T, VEC, R_, A_><<<grid, 256, 0, stream>>>(a, src, seg_ptr, perm, V, h, \
                                                                      act, alpha, (T*)H0, (T*)S);  \
@@ -269,6 +292,11 @@ int launch_init_embed(const EmbedArgs& a, const int64_t* src, const int32_t* seg
 #undef NT_IE_A
 #undef NT_IE
   NT_LAUNCH_CHECK();
+  if (amax && !k72) {  // the generic variant: two max passes over the outputs
+    int rc = fk_absmax((const float*)H0, E * h, amax, stream);
+    if (rc == NT_OK) rc = fk_absmax((const float*)S, V * h, amax + 1, stream);
+    return rc;
+  }
   return NT_OK;
 }
 
@@ -309,7 +337,8 @@ extern "C" int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_type
                                    int64_t num_edge_types, const int64_t* edge_types, int64_t ke,
                                    const int64_t* src, const int32_t* seg_ptr, const int32_t* perm,
                                    int64_t V, int64_t E, int64_t h, int act, float act_alpha,
-                                   int reduce, int dtype, void* H0, void* S, void* stream_) {
+                                   int reduce, int dtype, void* H0, void* S, float* amax_out,
+                                   void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
@@ -329,10 +358,15 @@ extern "C" int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_type
                   (S == nullptr || aligned16(S));
   if (dtype == NT_F32) {
     if (h % 4 == 0 && al)
-      return launch_init_embed<float, true>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S, stream);
-    return launch_init_embed<float, false>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S, stream);
+      return launch_init_embed<float, true>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S,
+                                            amax_out, stream);
+    return launch_init_embed<float, false>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S,
+                                           amax_out, stream);
   }
+  NT_REQUIRE(amax_out == nullptr, NT_EINVAL, "amax_out is fp32 only");
   if (h % 8 == 0 && al)
-    return launch_init_embed<bf16_raw, true>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S, stream);
-  return launch_init_embed<bf16_raw, false>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S, stream);
+    return launch_init_embed<bf16_raw, true>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S,
+                                             nullptr, stream);
+  return launch_init_embed<bf16_raw, false>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S,
+                                            nullptr, stream);
 }

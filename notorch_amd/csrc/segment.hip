@@ -89,8 +89,9 @@ template <int R, int ACT>
 __global__ void __launch_bounds__(256) init_aggregate_wave(
     const float4* __restrict__ Xv, const float4* __restrict__ Xe, const int64_t* __restrict__ src,
     const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm, int64_t V, int64_t hv,
-    int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S) {
+    int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S, float* __restrict__ amax) {
   const int lane = threadIdx.x & 63;
+  float mh = 0.f, ms = 0.f;  // max |H0|, max |S| of this lane (amax != NULL)
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
   for (int64_t v = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
        v < V; v += nwaves) {
@@ -115,6 +116,7 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
         for (int u = 0; u < 4; ++u) {
           const float4 h0 = a[u] + x[u];
           H0[ed[u] * hv + c] = h0;
+          mh = fmaxf(mh, fmaxf(fmaxf(fabsf(h0.x), fabsf(h0.y)), fmaxf(fabsf(h0.z), fabsf(h0.w))));
           r.push(act4_t<ACT>(h0, act, alpha));
         }
       }
@@ -122,9 +124,23 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
         const int64_t ed = perm[j];
         const float4 h0 = Xv[src[ed] * hv + c] + Xe[ed * hv + c];
         H0[ed * hv + c] = h0;
+        mh = fmaxf(mh, fmaxf(fmaxf(fabsf(h0.x), fabsf(h0.y)), fmaxf(fabsf(h0.z), fabsf(h0.w))));
         r.push(act4_t<ACT>(h0, act, alpha));
       }
-      S[v * hv + c] = r.result();
+      const float4 sv = r.result();
+      S[v * hv + c] = sv;
+      ms = fmaxf(ms, fmaxf(fmaxf(fabsf(sv.x), fabsf(sv.y)), fmaxf(fabsf(sv.z), fabsf(sv.w))));
+    }
+  }
+  if (amax) {  // one atomic max per wave (non-negative floats order like their bits)
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      mh = fmaxf(mh, __shfl_xor(mh, o));
+      ms = fmaxf(ms, __shfl_xor(ms, o));
+    }
+    if (lane == 0) {
+      atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(mh));
+      atomicMax(reinterpret_cast<unsigned int*>(amax + 1), __float_as_uint(ms));
     }
   }
 }
@@ -227,18 +243,24 @@ extern "C" int nt_segment_reduce(const void* X, const int32_t* seg_ptr, const in
   return NT_OK;
 }
 
+namespace nt {
+int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);  // update_pk.hip
+}
+
 extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
                              const int32_t* seg_ptr, const int32_t* perm, int64_t V, int64_t E,
                              int64_t h, int act, float act_alpha, int reduce, int dtype, void* H0,
-                             void* S, void* stream_) {
+                             void* S, float* amax_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
   NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
   hipStream_t stream = as_stream(stream_);
-  if (dtype == NT_BF16)
+  if (dtype == NT_BF16) {
+    NT_REQUIRE(amax_out == nullptr, NT_EINVAL, "amax_out is fp32 only");
     return launch_init_bf16(Xv, Xe, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S, stream);
+  }
   const bool vec = (h % 4 == 0) && aligned16(Xv) && aligned16(Xe) && aligned16(H0) &&
                    (S == nullptr || aligned16(S));
   if (S != nullptr) {
@@ -252,7 +274,9 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
         NT_DISPATCH_RA(reduce, act,
                        (init_aggregate_wave<R_, A_><<<grid, 256, 0, stream>>>(
                            (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
-                           act_alpha, (float4*)H0, (float4*)S)));
+                           act_alpha, (float4*)H0, (float4*)S, amax_out)));
+        NT_LAUNCH_CHECK();
+        return NT_OK;
       } else {
         const int grid = grid_for(V * hv, 256, 256 * 32);
         NT_DISPATCH_RA(reduce, act,
@@ -267,6 +291,13 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
                          (const float*)Xv, (const float*)Xe, src, seg_ptr, perm, V, h, act,
                          act_alpha, (float*)H0, (float*)S)));
     }
+    NT_LAUNCH_CHECK();
+    if (amax_out) {  // the other init variants: two max passes over the outputs
+      int rc = fk_absmax((const float*)H0, E * h, amax_out, stream);
+      if (rc == NT_OK) rc = fk_absmax((const float*)S, V * h, amax_out + 1, stream);
+      return rc;
+    }
+    return NT_OK;
   } else {
     if (E == 0) return NT_OK;
     NT_REQUIRE(Xv && Xe && src && H0, NT_EINVAL, "NULL pointer");
@@ -280,6 +311,7 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
     }
   }
   NT_LAUNCH_CHECK();
+  if (amax_out) return fk_absmax((const float*)H0, E * h, amax_out, stream);
   return NT_OK;
 }
 

@@ -47,6 +47,18 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
                      const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
                      float* S_out);
 
+// fp16x3 persistent layer kernel (update_fk.hpp, built in update_pk.hip): any h % 4 == 0; tiles of
+// at most fk_tile_rows(h, act, reduce, aact, fused) rows; Wimg = the fk image of the layer (header + fragment blocks).
+int fk_tile_rows(int64_t h, int act, int reduce, int aact, bool fused);
+int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in, float* amax_out,
+                     const int32_t* tile_ptr, int64_t ntiles, int tile_rows, int max_in_degree,
+                     const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
+                     float* S_out);
+int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_t img_stride, void* img,
+            hipStream_t stream);
+int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);
+inline int64_t fk_image_bytes(int64_t h) { return 256 + ((h + 31) / 32) * ((h + 15) / 16) * 2 * 1024; }
+
 // Deeper-ring variant (S/H 2 chunks ahead); requires additionally NT <= 24.
 int launch_update_ring(const UpdateArgs& a);
 

@@ -510,10 +510,12 @@ static int dispatch_cpw(const float* H, const float* S, const int64_t* src, cons
 
 }  // namespace nt
 
-// Packed image per layer: [fp32 fragment image (16x16x4 MFMA)][bf16x6 image (32x32x16 MFMA)]
-// [bf16x6 image (16x16x32 MFMA)], each part 256-B aligned; the update kernel variant picks the
-// part it consumes.
+// Packed image per layer (fp32 weights): [fp32 fragment image (16x16x4 MFMA)][bf16x6 image (32x32x16
+// MFMA)][bf16x6 image (16x16x32 MFMA)][fk image (two-part fp16, 16x16x32 MFMA, scale header)], each
+// part 256-B aligned; the update kernel variant picks the part it consumes.  Hidden sizes above 512
+// carry only the fk image.
 static size_t f32_image_bytes(int64_t h) {
+  if (h > 512) return 0;
   const nt::UpdateGeom g = nt::geom_for(h);
   return ((size_t)g.KB * g.NT * 64 * sizeof(float4) + 255) & ~size_t(255);
 }
@@ -525,10 +527,12 @@ static size_t as_part_bytes(int64_t h) {
   return nt::as_supported(h) ? ((nt::as_image_bytes(h) + 255) & ~size_t(255)) : 0;
 }
 
+static size_t fk_offset(int64_t h) { return f32_image_bytes(h) + x6_part_bytes(h) + as_part_bytes(h); }
+
 extern "C" size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype) {
   if (h <= 0) return 0;
   if (dtype == NT_BF16) return (nt::bf16_image_bytes(h) + 255) & ~size_t(255);
-  return f32_image_bytes(h) + x6_part_bytes(h) + as_part_bytes(h);
+  return fk_offset(h) + (((size_t)nt::fk_image_bytes(h) + 255) & ~size_t(255));
 }
 
 extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, int dtype, void* Wp,
@@ -536,23 +540,26 @@ extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, i
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
-  NT_REQUIRE(nlayers >= 0 && h > 0 && h <= 512, NT_EINVAL, "bad sizes (1 <= h <= 512)");
+  NT_REQUIRE(nlayers >= 0 && h > 0 && (dtype == NT_F32 || h <= 512) && h <= 8192, NT_EINVAL,
+             "bad sizes (1 <= h <= 512 for bf16, <= 8192 for fp32)");
   if (nlayers == 0) return NT_OK;
   NT_REQUIRE(W && Wp && aligned16(Wp), NT_EINVAL, "NULL or misaligned pointer");
   if (dtype == NT_BF16)
     return pack_weight_bf16(W, nlayers, h, (int64_t)nt_dmpnn_packed_weight_bytes(h, dtype), Wp,
                             as_stream(stream_));
-  const UpdateGeom g = geom_for(h);
   const size_t per_layer = nt_dmpnn_packed_weight_bytes(h, dtype);
   NT_REQUIRE(per_layer % 16 == 0, NT_EINVAL, "internal: packed layer size");
   hipStream_t stream = as_stream(stream_);
-  // fp32 image of every layer (layer stride = per_layer bytes)
-  for (int64_t l = 0; l < nlayers; ++l) {
-    const int64_t total = (int64_t)g.KB * g.NT * 64;
-    pack_weight_f32<<<grid_for(total, 256), 256, 0, stream>>>(
-        (const float*)W + l * h * h, 1, h, g.KB, g.NT,
-        (float4*)((char*)Wp + l * per_layer));
-    NT_LAUNCH_CHECK();
+  if (h <= 512) {
+    const UpdateGeom g = geom_for(h);
+    // fp32 image of every layer (layer stride = per_layer bytes)
+    for (int64_t l = 0; l < nlayers; ++l) {
+      const int64_t total = (int64_t)g.KB * g.NT * 64;
+      pack_weight_f32<<<grid_for(total, 256), 256, 0, stream>>>(
+          (const float*)W + l * h * h, 1, h, g.KB, g.NT,
+          (float4*)((char*)Wp + l * per_layer));
+      NT_LAUNCH_CHECK();
+    }
   }
   if (x6_supported(h)) {
     int rc = pack_weight_x6((const float*)W, nlayers, h, (int64_t)per_layer,
@@ -564,7 +571,22 @@ extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, i
                             (char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), stream);
     if (rc != NT_OK) return rc;
   }
-  return NT_OK;
+  return fk_pack((const float*)W, nlayers, h, h * h, (int64_t)per_layer, (char*)Wp + fk_offset(h), stream);
+}
+
+extern "C" int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, int agg_act) {
+  if (h <= 0) return 0;
+  if (dtype == NT_BF16) return 64;
+  return nt::fk_tile_rows(h, act, reduce, agg_act, true);
+}
+
+extern "C" int nt_absmax(const void* X, int64_t n, int dtype, float* out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_absmax: fp32 only");
+  NT_REQUIRE(n >= 0, NT_EINVAL, "bad size");
+  NT_REQUIRE(out != nullptr && (n == 0 || X != nullptr), NT_EINVAL, "NULL pointer");
+  return fk_absmax((const float*)X, n, out, as_stream(stream_));
 }
 
 extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
@@ -620,51 +642,62 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
 extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* src,
                                      const int64_t* rev, const void* Wp, const void* b, int64_t V,
                                      int64_t E, int64_t h, int residual, int act, float act_alpha,
-                                     const int32_t* tile_ptr, int64_t ntiles, const int32_t* perm,
+                                     const int32_t* tile_ptr, int64_t ntiles, int tile_rows,
+                                     int max_in_degree, const int32_t* perm,
                                      const int32_t* dst_sorted, int reduce, int agg_act,
-                                     float agg_alpha, int dtype, void* H_out, void* S_out,
-                                     void* stream_) {
+                                     float agg_alpha, int dtype, const float* amax_in,
+                                     float* amax_out, void* H_out, void* S_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
   NT_REQUIRE(agg_act >= NT_ACT_IDENTITY && agg_act <= NT_ACT_SIGMOID, NT_EINVAL, "bad agg_act code");
   NT_REQUIRE(reduce >= NT_SUM && reduce <= NT_MIN, NT_EINVAL, "bad reduce code");
-  NT_REQUIRE(V >= 0 && E >= 0 && E < (int64_t(1) << 31) && h > 0, NT_EINVAL, "bad sizes");
-  NT_REQUIRE(dtype == NT_BF16 ? bf16_fused_supported(h) : ps_supported(h), NT_EUNSUPPORTED,
-             "update_fused needs h % 4 == 0 and h <= 304 (fp32), h % 8 == 0 and h <= 512 (bf16)");
+  NT_REQUIRE(V >= 0 && E >= 0 && E < (int64_t(1) << 31) && V < (int64_t(1) << 31) && h > 0, NT_EINVAL,
+             "bad sizes");
+  NT_REQUIRE(dtype == NT_BF16 ? bf16_fused_supported(h) : (h % 4 == 0 && h <= 8192), NT_EUNSUPPORTED,
+             "update_fused needs h % 4 == 0 (fp32), h % 8 == 0 and h <= 512 (bf16)");
   if (E == 0) return NT_OK;
   NT_REQUIRE(H && S && src && rev && Wp && H_out, NT_EINVAL, "NULL pointer");
   NT_REQUIRE(H != H_out && (S_out == nullptr || S_out != S), NT_EINVAL, "outputs alias inputs");
   NT_REQUIRE(aligned16(H) && aligned16(S) && aligned16(H_out) && aligned16(Wp) &&
                  (b == nullptr || aligned16(b)) && (S_out == nullptr || aligned16(S_out)),
              NT_EINVAL, "feature pointers must be 16-byte aligned");
-  if (dtype == NT_BF16)
+  if (dtype == NT_BF16) {
+    NT_REQUIRE(tile_ptr == nullptr || tile_rows <= 64, NT_EUNSUPPORTED, "bf16 tiles hold at most 64 rows");
     return launch_update_bf16_fused(H, S, src, rev, Wp, b, V, E, h, residual, act, act_alpha,
                                     tile_ptr, ntiles, perm, dst_sorted, reduce, agg_act, agg_alpha,
                                     H_out, S_out, as_stream(stream_));
-  const UpdateGeom g = geom_for(h);
-  UpdateArgs a{(const float*)H, (const float*)S, src, rev,
-               (const char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), (const float*)b, V, E, h,
-               g.KB, g.NT, residual, act, act_alpha, (float*)H_out, as_stream(stream_)};
-  return launch_update_ps(a, tile_ptr, ntiles, perm, dst_sorted, reduce, agg_act, agg_alpha,
+  }
+  UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
+               0, 0, residual, act, act_alpha, (float*)H_out, as_stream(stream_)};
+  return launch_update_fk(a, (const char*)Wp + fk_offset(h), amax_in, amax_out, tile_ptr, ntiles,
+                          tile_rows, max_in_degree, perm, dst_sorted, reduce, agg_act, agg_alpha,
                           (float*)S_out);
 }
 
-// out = X W^T (the layer GEMM alone: no gathers, no residual, no bias) on the persistent bf16x6
-// MFMA kernel in its dense mode (row e of A is X[e]); the backward's dA = G W passes the packed
-// image of W^T.
+// out = X W^T (the layer GEMM alone: no gathers, no residual, no bias); the backward's dA = G W passes
+// the packed image of W^T.  amax_in = (unused, max|X|) on the device: the fp16x3 fk kernel in its
+// dense mode (row e of A is X[e]), any h % 4 == 0; amax_in = NULL: the persistent bf16x6 pk kernel
+// (h <= 304).
 extern "C" int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const void* Wp, int dtype,
-                                     void* out, void* stream_) {
+                                     const float* amax_in, void* out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul: fp32 only");
   NT_REQUIRE(M >= 0 && M < (int64_t(1) << 31) && h > 0, NT_EINVAL, "bad sizes");
-  NT_REQUIRE(ps_supported(h), NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul needs h % 4 == 0 and h <= 304");
+  NT_REQUIRE(amax_in ? (h % 4 == 0 && h <= 8192) : ps_supported(h), NT_EUNSUPPORTED,
+             "nt_dmpnn_dense_matmul needs h % 4 == 0 (and h <= 304 without amax_in)");
   if (M == 0) return NT_OK;
   NT_REQUIRE(X && Wp && out, NT_EINVAL, "NULL pointer");
   NT_REQUIRE(X != out, NT_EINVAL, "out aliases X");
   NT_REQUIRE(aligned16(X) && aligned16(out) && aligned16(Wp), NT_EINVAL, "pointers must be 16-byte aligned");
+  if (amax_in) {
+    UpdateArgs a{nullptr, (const float*)X, nullptr, nullptr, Wp, nullptr, M, M, h,
+                 0, 0, 0, NT_ACT_IDENTITY, 0.f, (float*)out, as_stream(stream_)};
+    return launch_update_fk(a, (const char*)Wp + fk_offset(h), amax_in, nullptr, nullptr, 0, 0, 0, nullptr,
+                            nullptr, NT_SUM, NT_ACT_IDENTITY, 0.f, nullptr);
+  }
   const UpdateGeom g = geom_for(h);
   UpdateArgs a{(const float*)X, (const float*)X, nullptr, nullptr,
                (const char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), nullptr, M, M, h,

@@ -1,0 +1,701 @@
+// fp32 D-MPNN layer kernel on fp16 MFMA with a two-part split ("fk"), optionally fused with the
+// aggregation its output feeds.  Included by update_pk.hip (it shares that unit's device status
+// word g_pk_timeout).
+//
+//   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b        (chemprop.py:36-43,
+//                                                                                 residual.py:27-28)
+//   S_out[v] = reduce_{e: dst[e] = v} aact(H_out[e])                               (chemprop.py:37-39,
+//                                                                                 :86 with identity)
+//
+// Numerics (fp32 contract).  Every operand is split into two fp16 parts, x = x0 + x1 with
+// x0 = fp16(x), x1 = fp16(x - x0), after a power-of-two scale that puts the operand's magnitude
+// bound at 2^14: the A rows by s_A (from amax_in = max|H|, max|S| of the inputs, written by the
+// kernels that produced them), W by s_W (stored in the image header by the pack kernel).  Three
+// v_mfma_f32_16x16x32_f16 products per k-step, W1 A0 + W0 A1 + W0 A0, accumulate in fp32; the
+// dropped W1 A1 term and the two split roundings are ~2^-22 relative, i.e. the result is as close to
+// fp64 as an fp32 GEMM's (3.5e-7 normalised at config 2).  Half the MFMA work of a bf16x6 split and
+// two thirds of its operand bytes.  The residual row enters the accumulator scaled by s_A s_W while
+// the K loop runs; the epilogue multiplies by the exact inverse and adds the bias.
+//
+// Structure: persistent, one 512-thread workgroup (8 waves, two per SIMD) per CU over a tile plan
+// of up to 16 RT rows per tile, cut at node boundaries (nt_dmpnn_tile_plan) and balanced to a
+// whole number of tiles per CU.  Each XCD walks one contiguous 1/nxcd of the plan (rows of
+// neighbouring tiles stay in that XCD's L2).  Per 32-deep k-step every thread gathers its
+// (row, 8-k) piece of S[src] and H[rev] two steps ahead into registers, forms A, splits it and
+// writes both fp16 parts straight into MFMA fragment order in an LDS double buffer; all 8 waves
+// then read the whole A slice (16 ds_read_b128 per wave) and run the MFMAs for their own output
+// column tiles (wave w: tiles w, w + 8, w + 16 of the chunk) with W fragments prefetched one step
+// ahead from the L2-resident image.  One barrier per k-step.  The tile's W image is read once per
+// 16 RT rows (128 at h <= 384), so W bytes per edge are a quarter of the 64-row bf16x6 kernel's.
+// Epilogue per wave and output column tile: scale + bias, H_out as 16-B row pieces from the
+// accumulators, and the fused aggregation as a left-to-right segmented scan over the tile's rows
+// (DPP row shifts within 16 lanes, carries between row tiles): the node sums come out in ascending
+// edge order, bit-identical to CPU scatter_add_ of the same H_out.  Hidden sizes beyond one chunk
+// of 128 columns x CT (h > 384 / 512) loop over column chunks, re-gathering A per chunk.
+#pragma once
+
+#include <type_traits>
+
+#include "common.hpp"
+
+namespace nt {
+namespace fk {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kThreads = 512;
+constexpr int kWaves = 8;
+constexpr int kImgHdr = 256;  // image header bytes (float s_W at 0); fragment blocks follow
+constexpr int kEmaps = 4;     // row-info buffers (tile index mod 4)
+constexpr int kFlagStart = 1, kFlagEnd = 2;
+
+__host__ __device__ constexpr int ks_for(int64_t h) { return (int)((h + 31) / 32); }
+__host__ __device__ constexpr int nt_for(int64_t h) { return (int)((h + 15) / 16); }
+// image bytes of one layer: header + KS x NT x 2 parts x 1 KiB fragment blocks
+__host__ __device__ constexpr int64_t image_bytes(int64_t h) {
+  return kImgHdr + (int64_t)ks_for(h) * nt_for(h) * 2 * 1024;
+}
+
+struct Args {
+  const float* H;     // E x h (NULL in dense mode)
+  const float* S;     // V x h (dense mode: the M x h operand X)
+  const int64_t* src;  // NULL: dense mode (A[e] = S[e])
+  const int64_t* rev;  // NULL: nothing subtracted
+  const char* Wimg;   // fk image of one layer
+  const float* bias;  // may be NULL
+  const float* amax_in;  // [0] max|H| (unused in dense mode), [1] max|S|
+  float* amax_out;       // may be NULL: [0] max over H_out, [1] max over S_out (atomic max)
+  int64_t V, E;
+  int h, hv, KS, NT, nchunks;
+  int residual, act;
+  float alpha;
+  const int* tile_ptr;  // NULL: fixed tiles of 16 RT rows in edge order (no aggregation)
+  int ntiles;
+  const int* perm;  // dst-sorted position -> edge (fused mode)
+  const int* dsts;  // dst-sorted position -> node (fused mode)
+  int reduce, aact;
+  float aalpha;
+  float* O;
+  float* SO;  // NULL: no aggregation
+  int nxcd;
+};
+
+// power-of-two scale that maps a magnitude bound to < 2^14 (exponent clamped to [-100, 24]);
+// a zero or non-finite bound leaves the operand unscaled
+__host__ __device__ inline int scale_exp(float bound) {
+  if (!(bound > 0.f) || !(bound <= 3.0e38f)) return 0;
+  int e;
+  frexpf(bound, &e);  // bound < 2^e
+  int s = 14 - e;
+  return s < -100 ? -100 : (s > 24 ? 24 : s);
+}
+
+// upper bound of |act(x)| for |x| <= m (every act code: relu / identity / gelu / silu <= m + 1,
+// leaky <= max(1, |alpha|) m, elu <= max(m, |alpha|), tanh / sigmoid <= 1)
+__device__ __forceinline__ float act_bound(float m, int act, float alpha) {
+  if (act == NT_ACT_RELU || act == NT_ACT_IDENTITY) return m;
+  const float a = fabsf(alpha) > 1.f ? fabsf(alpha) : 1.f;
+  return a * m + a;
+}
+
+__device__ __forceinline__ void atomic_max_abs(float* p, float v) {
+  // non-negative floats order like their bit patterns
+  atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+
+__device__ __forceinline__ f16x8 as_f16x8(uint4 v) { return __builtin_bit_cast(f16x8, v); }
+
+// compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>), so register
+// arrays are only ever indexed by constants (a dynamic index would put them in scratch)
+template <typename F, int... Is>
+__device__ __forceinline__ void sfor_impl(F&& f, std::integer_sequence<int, Is...>) {
+  (f(std::integral_constant<int, Is>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void sfor(F&& f) {
+  sfor_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// DPP: y[lane] = x[lane - 1] within each row of 16 lanes; lane 0 of a row keeps `old`
+__device__ __forceinline__ float dpp_shr1(float old, float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(__builtin_bit_cast(int, old),
+                                                               __builtin_bit_cast(int, x), 0x111, 0xf,
+                                                               0xf, false));
+}
+// DPP: y[lane] = x[lane + 15 mod 16] within each row (lane 0 gets lane 15)
+__device__ __forceinline__ float dpp_ror1(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x121,
+                                                               0xf, 0xf, false));
+}
+
+// --------------------------------------------------------------------------- per-row tile info
+struct RowSrc {
+  int soff, qoff;  // float4 offsets of S[src[e]] and H[rev[e]] rows (-1: none / row past the tile)
+};
+
+struct TileHead {  // level 1: tile bounds
+  int T, n;
+};
+
+template <int RT>
+__device__ __forceinline__ TileHead tile_head(const Args& a, int t) {
+  if (a.tile_ptr) {
+    const int T = a.tile_ptr[t], n = a.tile_ptr[t + 1] - T;
+    return {T, n};
+  }
+  const int64_t T = (int64_t)t * (16 * RT);
+  const int64_t n = a.E - T < 16 * RT ? a.E - T : 16 * RT;
+  return {(int)T, (int)n};
+}
+
+struct RowIdx {  // level 2: edge and node of the thread's row
+  int e, v, flags;
+};
+
+template <int RT>
+__device__ __forceinline__ RowIdx row_idx(const Args& a, TileHead th, int row) {
+  RowIdx r{-1, -1, kFlagStart | kFlagEnd};
+  const int n = th.n < 16 * RT ? th.n : 16 * RT;
+  if (row < n) {
+    const int pos = th.T + row;
+    r.e = a.perm ? a.perm[pos] : pos;
+    if (a.SO) {
+      r.v = a.dsts[pos];
+      const int vp = row > 0 ? a.dsts[pos - 1] : -1;
+      const int vn = row + 1 < n ? a.dsts[pos + 1] : -1;
+      r.flags = (vp != r.v ? kFlagStart : 0) | (vn != r.v ? kFlagEnd : 0);
+    }
+  }
+  return r;
+}
+
+__device__ __forceinline__ RowSrc row_src(const Args& a, int e) {  // level 3
+  RowSrc rs{-1, -1};
+  if (e >= 0) {
+    const int64_t s = a.src ? a.src[e] : e, q = a.rev ? a.rev[e] : -1;
+    rs.soff = (s >= 0 && s < a.V) ? (int)s * a.hv : -1;
+    rs.qoff = (q >= 0 && q < a.E) ? (int)q * a.hv : -1;
+  }
+  return rs;
+}
+
+// --------------------------------------------------------------------------- kernel
+// Per-thread state of the kernel.  Plain members + force-inlined free functions taking it by
+// reference (no lambdas: closures holding pointers to these arrays kept them in scratch).
+template <int RT, int CT, int GD = 2>
+struct State {
+  static constexpr int ROWS = 16 * RT;
+  static constexpr int PPT = RT / 4;        // 16-B pieces per thread per tensor per k-step (2 or 1)
+  static constexpr int kPartB = RT * 1024;  // one fp16 part of a k-slice
+  static constexpr int kBufB = 2 * kPartB;  // both parts
+  f32x4 acc[RT][CT];
+  uint4 wb[2][CT][2];  // W fragments (parity, column tile, part)
+  f32x4 gs[GD][PPT], gq[GD][PPT];  // staged pieces, GD k-steps ahead
+  int gso[GD], gqo[GD];  // their row sources
+  float mxH, mxS;
+  // constants of the thread / launch
+  int lane, wave, fr, g16, grt, grow, kp0, hv, NT, CTC;
+  float sA, sAW, inv;
+  char* abuf;
+  int4* emap;
+  __amdgpu_buffer_rsrc_t wrsrc;
+};
+
+template <int RT, int CT, int ACT, int P, int GD>
+__device__ __forceinline__ void fk_gather(State<RT, CT, GD>& st, const Args& a, int soff, int qoff, int s) {
+  st.gso[P] = soff;
+  st.gqo[P] = qoff;
+  const int sb = soff >= 0 ? soff : 0, qb = qoff >= 0 ? qoff : 0;
+  const f32x4* S4 = reinterpret_cast<const f32x4*>(a.S);
+  const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H);
+#pragma unroll
+  for (int u = 0; u < State<RT, CT, GD>::PPT; ++u) {
+    int p = 8 * s + st.kp0 + u;
+    p = p < st.hv ? p : 0;
+    st.gs[P][u] = S4[sb + p];
+    st.gq[P][u] = H4 ? H4[qb + p] : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+// A = S[src] - act(H[rev]) of the staged piece, scaled by s_A, split into two fp16 parts written in
+// MFMA B-fragment order (row tile grt, lane (k-group, row): 16 B per part) into LDS buffer P
+template <int RT, int CT, int ACT, int P, int BUF, int GD>
+__device__ __forceinline__ void fk_split(State<RT, CT, GD>& st, const Args& a, int s) {
+  using St = State<RT, CT, GD>;
+  const bool sok = st.gso[P] >= 0, qok = st.gqo[P] >= 0;
+  float x[4 * St::PPT];
+#pragma unroll
+  for (int u = 0; u < St::PPT; ++u) {
+    const bool in = 8 * s + st.kp0 + u < st.hv;
+    const f32x4 sv = st.gs[P][u];
+    const f32x4 qv = st.gq[P][u];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float q = act_t<ACT>(qv[c], a.act, a.alpha);
+      const float av = (sok && in ? sv[c] : 0.f) - (qok && in ? q : 0.f);
+      x[4 * u + c] = av * st.sA;
+    }
+  }
+  char* base = st.abuf + BUF * St::kBufB + st.grt * 1024 + st.lane * 16 +
+               (RT == 8 ? 0 : 8 * (st.wave >> 2));
+  if constexpr (St::PPT == 2) {
+    f16x8 h0, h1;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const _Float16 t0 = (_Float16)x[c];
+      h0[c] = t0;
+      h1[c] = (_Float16)(x[c] - (float)t0);
+    }
+    *reinterpret_cast<f16x8*>(base) = h0;
+    *reinterpret_cast<f16x8*>(base + St::kPartB) = h1;
+  } else {
+    f16x4 h0, h1;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const _Float16 t0 = (_Float16)x[c];
+      h0[c] = t0;
+      h1[c] = (_Float16)(x[c] - (float)t0);
+    }
+    *reinterpret_cast<f16x4*>(base) = h0;
+    *reinterpret_cast<f16x4*>(base + St::kPartB) = h1;
+  }
+}
+
+template <int RT, int CT, int P, int GD>
+__device__ __forceinline__ void fk_load_w(State<RT, CT, GD>& st, int c, int s) {
+#pragma unroll
+  for (int j = 0; j < CT; ++j) {
+    const int ct = c * st.CTC + st.wave + 8 * j;
+    if (ct < st.NT) {
+      const int soff = __builtin_amdgcn_readfirstlane(kImgHdr + ((s * st.NT + ct) * 2) * 1024);
+      st.wb[P][j][0] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff, 0));
+      st.wb[P][j][1] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff + 1024, 0));
+    }
+  }
+}
+
+template <int RT, int CT, int P, int GD>
+__device__ __forceinline__ void fk_mfma(State<RT, CT, GD>& st, int c, int nrt) {
+  using St = State<RT, CT, GD>;
+  const char* bb = st.abuf + P * St::kBufB + st.lane * 16;
+  // A fragments one row tile ahead; the schedule barriers keep the compiler from hoisting every row
+  // tile's fragments (64 VGPRs) above the MFMAs
+  f16x8 a0 = *reinterpret_cast<const f16x8*>(bb);
+  f16x8 a1 = *reinterpret_cast<const f16x8*>(bb + St::kPartB);
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    if (rt < nrt) {
+      f16x8 n0 = a0, n1 = a1;
+      if (rt + 1 < RT) {
+        n0 = *reinterpret_cast<const f16x8*>(bb + (rt + 1) * 1024);
+        n1 = *reinterpret_cast<const f16x8*>(bb + St::kPartB + (rt + 1) * 1024);
+      }
+#pragma unroll
+      for (int j = 0; j < CT; ++j) {
+        if (c * st.CTC + st.wave + 8 * j < st.NT) {
+          const f16x8 w0 = as_f16x8(st.wb[P][j][0]), w1 = as_f16x8(st.wb[P][j][1]);
+          f32x4 t = st.acc[rt][j];
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, a0, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a1, t, 0, 0, 0);
+          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a0, t, 0, 0, 0);
+          st.acc[rt][j] = t;
+        }
+      }
+      a0 = n0;
+      a1 = n1;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+}
+
+// Residual rows H[e] of (tile i, chunk c), column tile j, loaded straight into the accumulators:
+// issued by the epilogue of the previous (tile, chunk) as soon as it has stored column tile j, so
+// they land during the rest of that epilogue; fk_resid_scale multiplies them by s_A s_W before the
+// first MFMA of the K loop (48 packed multiplies per tile, no staging registers).
+template <int RT, int CT, int GD>
+__device__ __forceinline__ void fk_resid_load(State<RT, CT, GD>& st, const Args& a, int i, int c, int j) {
+  using St = State<RT, CT, GD>;
+  const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H);
+  int pc = 4 * (c * st.CTC + st.wave + 8 * j) + st.g16;
+  pc = pc < st.hv ? pc : 0;
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    const int e = st.emap[(i % kEmaps) * St::ROWS + 16 * rt + st.fr].x;
+    st.acc[rt][j] = H4[(int64_t)(e >= 0 ? e : 0) * st.hv + pc];
+  }
+}
+
+template <int RT, int CT, int GD>
+__device__ __forceinline__ void fk_resid_scale(State<RT, CT, GD>& st) {
+  const f32x4 s4 = f32x4{st.sAW, st.sAW, st.sAW, st.sAW};
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+    for (int j = 0; j < CT; ++j) st.acc[rt][j] = st.acc[rt][j] * s4;
+}
+
+// epilogue of (tile i, chunk c): scale + bias, H_out from the accumulators, fused aggregation as a
+// left-to-right segmented scan over each row tile's 16 rows (rows on lanes fr, carries between row
+// tiles): after L rounds the last row of every node holds ((m_first + m_2) + ...) + m_last.
+// Column tiles and row tiles are compile-time (template recursion: the loops hold convergent DPP /
+// ballot operations that the unroller leaves alone, and a runtime index puts the accumulators in
+// scratch).
+struct EpiCtx {
+  const f32x4* b4;
+  f32x4* O4;
+  f32x4* SO4;
+  const int4* em;
+  int n;
+};
+
+template <int RTI, int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD>
+__device__ __forceinline__ void fk_epi_row(State<RT, CT, GD>& st, const Args& a, const EpiCtx& x0, int pc,
+                                           bool pok, const f32x4& bj, f32x4& carry, float& ccnt) {
+  if (16 * RTI < x0.n) {
+    const int hv = st.hv;
+    const int4 ri = x0.em[16 * RTI + st.fr];
+    f32x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[RTI][J][q], st.inv, bj[q]);
+    const bool rok = ri.x >= 0 && pok;
+    if (rok) {
+      x0.O4[(int64_t)ri.x * hv + pc] = o;
+      st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+    }
+    if (x0.SO4 != nullptr) {
+      // MAXL rounds of x[r] = start[r] ? m[r] : x[r - 1] + m[r] (the carry enters at row 0): a
+      // row's value is final once the rounds cover its distance from its node's first row, at
+      // most max in-degree - 1 (<= 16 within a row tile); extra rounds leave converged rows as they
+      // are.  Straight-line code: a branch around the rounds costs the kernel its registers.
+      const bool start = (ri.z & kFlagStart) != 0;
+      f32x4 m;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) m[q] = act_t<AACT>(o[q], a.aact, a.aalpha);
+      f32x4 x = m, cin;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) cin[q] = dpp_ror1(carry[q]);
+      float cnt = 1.f;
+      const float cinc = SUMONLY ? 0.f : dpp_ror1(ccnt);
+#pragma unroll
+      for (int it = 0; it < MAXL; ++it) {
+        f32x4 y;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) y[q] = dpp_shr1(cin[q], x[q]);
+        if constexpr (SUMONLY) {
+          x = start ? m : y + m;
+        } else {
+          const float yc = dpp_shr1(cinc, cnt);
+          f32x4 z;
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float mx = fmaxf(y[q], m[q]), mn = fminf(y[q], m[q]), sm = y[q] + m[q];
+            z[q] = a.reduce == NT_MAX ? mx : (a.reduce == NT_MIN ? mn : sm);
+          }
+          x = start ? m : z;
+          cnt = start ? 1.f : yc + 1.f;
+        }
+      }
+      if ((ri.z & kFlagEnd) && rok) {
+        f32x4 r = x;
+        if (!SUMONLY && a.reduce == NT_MEAN) r = x / cnt;
+        x0.SO4[(int64_t)ri.y * hv + pc] = r;
+        st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(r[0]), fabsf(r[1])), fmaxf(fabsf(r[2]), fabsf(r[3]))));
+      }
+      carry = x;
+      ccnt = cnt;
+    }
+  }
+  if constexpr (RTI + 1 < RT)
+    fk_epi_row<RTI + 1, J, RT, CT, AACT, SUMONLY, MAXL, GD>(st, a, x0, pc, pok, bj, carry, ccnt);
+}
+
+template <int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD>
+__device__ __forceinline__ void fk_epi_col(State<RT, CT, GD>& st, const Args& a, const EpiCtx& x0, int i, int c,
+                                           bool load_next, int i_next, int c_next) {
+  const int ct = c * st.CTC + st.wave + 8 * J;
+  if (ct < st.NT) {
+    const int pc = 4 * ct + st.g16;
+    const bool pok = pc < st.hv;
+    const f32x4 bj = (x0.b4 && pok) ? x0.b4[pc] : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 carry = f32x4{0.f, 0.f, 0.f, 0.f};
+    float ccnt = 0.f;
+    fk_epi_row<0, J, RT, CT, AACT, SUMONLY, MAXL, GD>(st, a, x0, pc, pok, bj, carry, ccnt);
+  }
+  // column tile J is stored: its accumulators start the next (tile, chunk)
+  if (load_next) {
+    fk_resid_load(st, a, i_next, c_next, J);
+  } else {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if constexpr (J + 1 < CT)
+    fk_epi_col<J + 1, RT, CT, AACT, SUMONLY, MAXL, GD>(st, a, x0, i, c, load_next, i_next, c_next);
+}
+
+template <int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD>
+__device__ __forceinline__ void fk_epilogue(State<RT, CT, GD>& st, const Args& a, int i, int c, int n,
+                                            bool load_next, int i_next, int c_next) {
+  EpiCtx x0;
+  x0.b4 = reinterpret_cast<const f32x4*>(a.bias);
+  x0.O4 = reinterpret_cast<f32x4*>(a.O);
+  x0.SO4 = reinterpret_cast<f32x4*>(a.SO);
+  x0.em = st.emap + (i % kEmaps) * State<RT, CT, GD>::ROWS;
+  x0.n = n;
+  fk_epi_col<0, RT, CT, AACT, SUMONLY, MAXL, GD>(st, a, x0, i, c, load_next, i_next, c_next);
+}
+
+__device__ __forceinline__ void fk_barrier() {
+  // LDS writes of this step retired, then the workgroup barrier (vector-memory loads stay in flight)
+  __syncthreads();
+}
+
+template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL, int GD = 2>
+__global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
+  using St = State<RT, CT, GD>;
+  constexpr int ROWS = St::ROWS;
+  constexpr int kEmapB = kEmaps * ROWS * 16;
+  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * St::kBufB + kEmapB) / 16];
+
+  // XCD-aware persistent walk (blocks b and b + nxcd share an L2): each XCD one contiguous chunk
+  int t0 = (int)blockIdx.x, tstride = (int)gridDim.x, ntl;
+  const int nx = a.nxcd;
+  if (nx > 1 && (int)gridDim.x % nx == 0) {
+    const int x = (int)blockIdx.x % nx, chunk = (a.ntiles + nx - 1) / nx;
+    const int lo = x * chunk, hi = min(a.ntiles, lo + chunk);
+    t0 = lo + (int)blockIdx.x / nx;
+    tstride = (int)gridDim.x / nx;
+    ntl = hi > t0 ? (hi - t0 + tstride - 1) / tstride : 0;
+  } else {
+    ntl = (a.ntiles - t0 + tstride - 1) / tstride;
+  }
+  if (ntl <= 0) return;
+
+  St st;
+  const int tid = threadIdx.x;
+  st.lane = tid & 63;
+  st.wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  st.fr = st.lane & 15;
+  st.g16 = st.lane >> 4;
+  st.grt = RT == 8 ? st.wave : (st.wave & 3);
+  st.grow = 16 * st.grt + st.fr;
+  st.kp0 = RT == 8 ? 2 * st.g16 : 2 * st.g16 + (st.wave >> 2);
+  st.hv = a.hv;
+  st.NT = a.NT;
+  st.CTC = 8 * CT;
+  st.abuf = reinterpret_cast<char*>(smem);
+  st.emap = reinterpret_cast<int4*>(st.abuf + 2 * St::kBufB);
+  st.wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.Wimg, (short)0, (int)image_bytes(a.h), 0x00020000);
+  st.mxH = 0.f;
+  st.mxS = 0.f;
+  // scales: s_A from the bound of |A| = |S[src] - act(H[rev])|, s_W from the image header
+  const float bound = a.src ? a.amax_in[1] + (a.rev ? act_bound(a.amax_in[0], a.act, a.alpha) : 0.f)
+                            : a.amax_in[1];
+  st.sA = ldexpf(1.f, scale_exp(bound));
+  const float sW = *reinterpret_cast<const float*>(a.Wimg);
+  st.sAW = st.sA * sW;
+  st.inv = 1.f / st.sAW;  // exact: a power of two
+  const bool resid = a.residual && a.H != nullptr;
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int j = 0; j < CT; ++j) st.acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const bool info_writer = st.g16 == 0 && (RT == 8 || st.wave < 4);
+  const int SPT = a.nchunks * a.KS;  // steps per tile
+  const int G = ntl * SPT;
+
+  // ---- tile info pipeline: cur (tile i), nxt (i + 1), prog (tile i + 2, built over three steps)
+  int cur_s, cur_q, nxt_s = -1, nxt_q = -1;
+  TileHead pth{0, 0};
+  RowIdx pri{-1, -1, 3};
+  int prs_s = -1, prs_q = -1;
+  int n_cur, n_nxt = 0;
+  {
+    const TileHead h0 = tile_head<RT>(a, t0);
+    const RowIdx r0 = row_idx<RT>(a, h0, st.grow);
+    const RowSrc s0 = row_src(a, r0.e);
+    cur_s = s0.soff;
+    cur_q = s0.qoff;
+    if (info_writer) st.emap[0 * ROWS + st.grow] = int4{r0.e, r0.v, r0.flags, 0};
+    if (h0.n > ROWS && tid == 0) atomicOr(&g_pk_timeout, 2u);
+    n_cur = h0.n < ROWS ? h0.n : ROWS;
+    if (ntl > 1) {
+      const TileHead h1 = tile_head<RT>(a, t0 + tstride);
+      const RowIdx r1 = row_idx<RT>(a, h1, st.grow);
+      const RowSrc s1 = row_src(a, r1.e);
+      nxt_s = s1.soff;
+      nxt_q = s1.qoff;
+      if (info_writer) st.emap[1 * ROWS + st.grow] = int4{r1.e, r1.v, r1.flags, 0};
+      if (h1.n > ROWS && tid == 0) atomicOr(&g_pk_timeout, 2u);
+      n_nxt = h1.n < ROWS ? h1.n : ROWS;
+    }
+    if (ntl > 2) pth = tile_head<RT>(a, t0 + 2 * tstride);
+  }
+
+  // ---- prologue: steps 0 and 1 staged, W of step 0, slice 0 split into buffer 0
+  __syncthreads();  // emap of tiles 0 and 1
+  if (resid) {
+#pragma unroll
+    for (int j = 0; j < CT; ++j) fk_resid_load(st, a, 0, 0, j);
+  }
+  fk_gather<RT, CT, ACT, 0>(st, a, cur_s, cur_q, 0);
+  if constexpr (GD == 2) {
+    if (G > 1) {
+      if (SPT > 1) fk_gather<RT, CT, ACT, 1>(st, a, cur_s, cur_q, 1 % a.KS);
+      else fk_gather<RT, CT, ACT, 1>(st, a, nxt_s, nxt_q, 0);
+    }
+  }
+  fk_load_w<RT, CT, 0>(st, 0, 0);
+  fk_split<RT, CT, ACT, 0, 0>(st, a, 0);
+  fk_barrier();
+
+  const int l2 = SPT > 1 ? 1 : 0, l3 = SPT > 2 ? 2 : l2;
+  int g = 0, i = 0, k = 0;  // global step, tile-local index, step within the tile
+  while (g < G) {
+#pragma unroll
+    for (int P = 0; P < 2; ++P) {
+      if (g < G) {
+        const int c = k / a.KS, s = k - c * a.KS;
+        // (1) tile-info pipeline: rows of tile i + 2 (level 2 at step l2, level 3 at step l3)
+        if (i + 2 < ntl) {
+          if (k == l2) pri = row_idx<RT>(a, pth, st.grow);
+          if (k == l3) {
+            const RowSrc rs = row_src(a, pri.e);
+            prs_s = rs.soff;
+            prs_q = rs.qoff;
+          }
+        }
+        // (2) stage step g + GD (its register slot was split at step g - 1)
+        if (g + GD < G) {
+          const int k2 = k + GD;
+          const int adv = k2 >= SPT ? (k2 >= 2 * SPT ? 2 : 1) : 0;
+          const int s2 = (k2 - adv * SPT) % a.KS;
+          const int so = adv == 0 ? cur_s : (adv == 1 ? nxt_s : prs_s);
+          const int qo = adv == 0 ? cur_q : (adv == 1 ? nxt_q : prs_q);
+          if (GD == 1 || P == 0) fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s2);
+          else fk_gather<RT, CT, ACT, GD - 1>(st, a, so, qo, s2);
+        }
+        // (3) W fragments of step g + 1
+        const int k1 = k + 1 < SPT ? k + 1 : 0;
+        const int c1 = k1 / a.KS, s1 = k1 - c1 * a.KS;
+        if (g + 1 < G) {
+          if (P == 0) fk_load_w<RT, CT, 1>(st, c1, s1);
+          else fk_load_w<RT, CT, 0>(st, c1, s1);
+        }
+        // (4) residual rows (loaded by the previous epilogue) into the accumulators' scale
+        if (resid && s == 0) fk_resid_scale(st);
+        // (5) MFMAs of step g
+        if (P == 0) fk_mfma<RT, CT, 0>(st, c, (n_cur + 15) >> 4);
+        else fk_mfma<RT, CT, 1>(st, c, (n_cur + 15) >> 4);
+        // (6) split step g + 1's staged piece into the other buffer
+        if (g + 1 < G) {
+          if (P == 0) fk_split<RT, CT, ACT, GD - 1, 1>(st, a, s1);
+          else fk_split<RT, CT, ACT, 0, 0>(st, a, s1);
+        }
+        fk_barrier();
+        // (7) epilogue at the chunk's last k-step; it starts the next (tile, chunk)'s residual loads
+        if (s == a.KS - 1) {
+          const bool last_c = c + 1 == a.nchunks;
+          const int i_next = last_c ? i + 1 : i, c_next = last_c ? 0 : c + 1;
+          fk_epilogue<RT, CT, AACT, SUMONLY, MAXL>(st, a, i, c, n_cur, resid && i_next < ntl, i_next, c_next);
+        }
+        // (8) advance
+        ++g;
+        if (++k == SPT) {
+          k = 0;
+          ++i;
+          if (i < ntl) {
+            cur_s = nxt_s;
+            cur_q = nxt_q;
+            n_cur = n_nxt;
+            if (i + 1 < ntl) {  // tile i + 1 was built during tile i - 1: publish its rows
+              nxt_s = prs_s;
+              nxt_q = prs_q;
+              if (info_writer) st.emap[((i + 1) % kEmaps) * ROWS + st.grow] = int4{pri.e, pri.v, pri.flags, 0};
+              if (pth.n > ROWS && tid == 0) atomicOr(&g_pk_timeout, 2u);
+              n_nxt = pth.n < ROWS ? pth.n : ROWS;
+              if (i + 2 < ntl) pth = tile_head<RT>(a, t0 + (i + 2) * tstride);
+            }
+          }
+        }
+      }
+    }
+  }
+  if (a.amax_out) {
+    const float mh = wave_max(st.mxH), ms = wave_max(st.mxS);
+    if (st.lane == 0) {
+      atomic_max_abs(a.amax_out, mh);
+      if (a.SO) atomic_max_abs(a.amax_out + 1, ms);
+    }
+  }
+}
+
+// --------------------------------------------------------------------------- packing
+// One thread per 16-B fragment slot: image block ((s NT + ct) 2 + p), lane l holds
+// W[16 ct + (l & 15)][32 s + 8 (l >> 4) + j], j < 8, part p of the scaled two-part fp16 split.
+// Every block first reduces max|W| of its layer (the scale is the same in every block).
+__global__ void __launch_bounds__(256) pack_fk_kernel(const float* __restrict__ W, int64_t h, int KS,
+                                                      int NT, int64_t w_stride, int64_t img_stride,
+                                                      char* __restrict__ img) {
+  const int layer = blockIdx.y;
+  const float* Wl = W + layer * w_stride;
+  char* out = img + layer * img_stride;
+  __shared__ float red[256];
+  float m = 0.f;
+  for (int64_t q = threadIdx.x; q < h * h; q += 256) m = fmaxf(m, fabsf(Wl[q]));
+  red[threadIdx.x] = m;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
+    __syncthreads();
+  }
+  const float sW = ldexpf(1.f, scale_exp(red[0]));
+  const int64_t slots = (int64_t)KS * NT * 2 * 64;
+  const int64_t q = blockIdx.x * 256LL + threadIdx.x;
+  if (q == 0) *reinterpret_cast<float*>(out) = sW;
+  if (q >= slots) return;
+  const int l = (int)(q & 63);
+  const int64_t blk = q >> 6;
+  const int p = (int)(blk & 1);
+  const int64_t sc = blk >> 1;
+  const int ct = (int)(sc % NT), s = (int)(sc / NT);
+  const int col = 16 * ct + (l & 15);
+  f16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 32 * s + 8 * (l >> 4) + j;
+    const float w = (col < h && k < h) ? Wl[(int64_t)col * h + k] * sW : 0.f;
+    const _Float16 w0 = (_Float16)w;
+    v[j] = p == 0 ? w0 : (_Float16)(w - (float)w0);
+  }
+  *reinterpret_cast<f16x8*>(out + kImgHdr + q * 16) = v;
+}
+
+// atomically max |X| over n elements into *out (non-negative float bit order)
+__global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ X, int64_t n,
+                                                     float* __restrict__ out) {
+  float m = 0.f;
+  const int64_t n4 = (reinterpret_cast<uintptr_t>(X) & 15) == 0 ? n / 4 : 0;
+  const float4* X4 = reinterpret_cast<const float4*>(X);
+  for (int64_t q = blockIdx.x * 256LL + threadIdx.x; q < n4; q += (int64_t)gridDim.x * 256) {
+    const float4 v = X4[q];
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  }
+  for (int64_t q = 4 * n4 + blockIdx.x * 256LL + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256)
+    m = fmaxf(m, fabsf(X[q]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) atomic_max_abs(out, m);
+}
+
+}  // namespace fk
+}  // namespace nt

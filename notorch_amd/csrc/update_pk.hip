@@ -37,6 +37,14 @@ __device__ unsigned int g_pk_timeout;
 // loop; [7] consumer waves, [8] producer waves.
 __device__ unsigned long long g_pk_stamps[10];
 
+}  // namespace nt
+
+// the fp16x3 layer kernel (shares g_pk_timeout: bit 1 = bounded wait gave up, bit 2 = a tile larger
+// than the fk kernel's row capacity)
+#include "update_fk.hpp"
+
+namespace nt {
+
 namespace {
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -714,6 +722,141 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
   if (u.act == NT_ACT_IDENTITY && !fused)  // dense mode (the backward's dA) and identity layers
     return dispatch_pk<NT_ACT_IDENTITY, NT_ACT_IDENTITY, true>(a, KS, grid, u.stream, Seq{});
   return dispatch_pk<-1, -1, false>(a, KS, grid, u.stream, Seq{});
+}
+
+// ------------------------------------------------------------------------------ fk launcher
+namespace {
+template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL>
+int launch_fk_t(const fk::Args& a, int grid, hipStream_t stream) {
+  fk::update_fk_kernel<RT, CT, ACT, AACT, SUMONLY, MAXL><<<grid, fk::kThreads, 0, stream>>>(a);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+// 128-row tiles: relu layers with a sum aggregation whose act is relu / identity, or no aggregation
+template <int CT>
+int launch_fk_wide(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
+  const bool fused = a.SO != nullptr;
+  const bool relu = a.act == NT_ACT_RELU;
+  if (!fused) {  // plain update / dense mode: no aggregation
+    if (relu) return launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 1>(a, grid, stream);
+    if (a.act == NT_ACT_IDENTITY)
+      return launch_fk_t<8, CT, NT_ACT_IDENTITY, NT_ACT_IDENTITY, true, 1>(a, grid, stream);
+    return launch_fk_t<8, CT, -1, NT_ACT_IDENTITY, true, 1>(a, grid, stream);
+  }
+  // fused (fk_tile_rows: act = relu): scan rounds 3 cover in-degree <= 4 (molecules), 16 every plan
+  if (a.aact == NT_ACT_RELU)
+    return maxl <= 3 ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 3>(a, grid, stream)
+                     : launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 16>(a, grid, stream);
+  return maxl <= 3 ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 3>(a, grid, stream)
+                   : launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 16>(a, grid, stream);
+}
+
+// 64-row tiles: every other combination (any reduce, any aggregation act) and h > 384
+template <int CT>
+int launch_fk_narrow(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
+  const bool fused = a.SO != nullptr;
+  const bool relu = a.act == NT_ACT_RELU;
+  const bool fast = !fused || (a.reduce == NT_SUM && (a.aact == NT_ACT_RELU || a.aact == NT_ACT_IDENTITY));
+  if (fast) {
+    if (!fused)
+      return relu ? launch_fk_t<4, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 1>(a, grid, stream)
+                  : launch_fk_t<4, CT, -1, NT_ACT_IDENTITY, true, 1>(a, grid, stream);
+    if (a.aact == NT_ACT_RELU)
+      return relu ? launch_fk_t<4, CT, NT_ACT_RELU, NT_ACT_RELU, true, 16>(a, grid, stream)
+                  : launch_fk_t<4, CT, -1, NT_ACT_RELU, true, 16>(a, grid, stream);
+    return relu ? launch_fk_t<4, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 16>(a, grid, stream)
+                : launch_fk_t<4, CT, -1, NT_ACT_IDENTITY, true, 16>(a, grid, stream);
+  }
+  (void)maxl;
+  return launch_fk_t<4, CT, -1, -1, false, 16>(a, grid, stream);
+}
+}  // namespace
+
+// Row capacity of the fk tiles for a layer: 128 for h <= 384 with act = relu and a sum aggregation
+// whose act is relu / identity, or with no aggregation (fused < 0); else 64.  (The other variants
+// need more registers than two waves per SIMD hold at 128 rows.)
+int fk_tile_rows(int64_t h, int act, int reduce, int aact, bool fused) {
+  const bool wide_ok =
+      !fused || (act == NT_ACT_RELU && reduce == NT_SUM && (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY));
+  return (fk::nt_for(h) <= 24 && wide_ok) ? 128 : 64;
+}
+
+int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in, float* amax_out,
+                     const int32_t* tile_ptr, int64_t ntiles, int tile_rows, int max_in_degree,
+                     const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
+                     float* S_out) {
+  const bool fused = tile_ptr != nullptr;
+  NT_REQUIRE(fused == (S_out != nullptr), NT_EINVAL, "S_out must be given exactly with a tile plan");
+  NT_REQUIRE(!fused || (perm && dsts), NT_EINVAL, "fused mode needs perm and dst_sorted");
+  NT_REQUIRE(amax_in != nullptr, NT_EINVAL, "fp32 update needs amax_in (max|H|, max|S| on the device)");
+  NT_REQUIRE(u.h % 4 == 0, NT_EUNSUPPORTED, "fp32 update needs h % 4 == 0");
+  NT_REQUIRE((u.E * u.h) / 4 < (int64_t(1) << 31) && (u.V * u.h) / 4 < (int64_t(1) << 31),
+             NT_EUNSUPPORTED, "fp32 update: E*h and V*h must stay below 2^33");
+  const int cap = fk_tile_rows(u.h, u.act, reduce, aact, fused);
+  NT_REQUIRE(!fused || (tile_rows >= 1 && tile_rows <= cap), NT_EUNSUPPORTED,
+             "tile plan rows exceed nt_dmpnn_fused_tile_rows for this layer");
+  NT_REQUIRE(!fused || (max_in_degree >= 0 && max_in_degree <= 32), NT_EUNSUPPORTED,
+             "fused aggregation needs max_in_degree <= 32");
+  fk::Args a;
+  a.H = u.H;
+  a.S = u.S;
+  a.src = u.src;
+  a.rev = u.rev;
+  a.Wimg = (const char*)Wimg;
+  a.bias = u.b;
+  a.amax_in = amax_in;
+  a.amax_out = amax_out;
+  a.V = u.V;
+  a.E = u.E;
+  a.h = (int)u.h;
+  a.hv = (int)(u.h / 4);
+  a.KS = fk::ks_for(u.h);
+  a.NT = fk::nt_for(u.h);
+  a.residual = u.residual;
+  a.act = u.act;
+  a.alpha = u.alpha;
+  a.tile_ptr = tile_ptr;
+  a.perm = perm;
+  a.dsts = dsts;
+  a.reduce = reduce;
+  a.aact = aact;
+  a.aalpha = aalpha;
+  a.O = u.H_out;
+  a.SO = S_out;
+  a.nxcd = xcd_count();
+  a.ntiles = fused ? (int)ntiles : (int)((u.E + cap - 1) / cap);
+  if (a.ntiles == 0) return NT_OK;
+  const int grid = a.ntiles < cu_count() ? a.ntiles : cu_count();
+  const int maxl = max_in_degree - 1;  // scan rounds needed within a 16-row tile
+  // up to 3 column tiles per wave (NT <= 24, one chunk); waves past NT skip theirs at run time
+  if (cap == 128) {
+    a.nchunks = 1;
+    return launch_fk_wide<3>(a, maxl, grid, u.stream);
+  }
+  if (a.NT <= 24) {
+    a.nchunks = 1;
+    return launch_fk_narrow<3>(a, maxl, grid, u.stream);
+  }
+  a.nchunks = (a.NT + 31) / 32;
+  return launch_fk_narrow<4>(a, maxl, grid, u.stream);
+}
+
+int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_t img_stride, void* img,
+            hipStream_t stream) {
+  const int KS = fk::ks_for(h), NT = fk::nt_for(h);
+  const int64_t slots = (int64_t)KS * NT * 2 * 64;
+  dim3 grid((unsigned)((slots + 255) / 256), (unsigned)nlayers);
+  fk::pack_fk_kernel<<<grid, 256, 0, stream>>>(W, h, KS, NT, w_stride, img_stride, (char*)img);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream) {
+  if (n <= 0) return NT_OK;
+  fk::absmax_kernel<<<grid_for(n / 4 + 1, 256, 256 * 8), 256, 0, stream>>>(X, n, out);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
 }
 
 }  // namespace nt

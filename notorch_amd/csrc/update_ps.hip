@@ -624,20 +624,33 @@ bool ps_supported(int64_t h) { return h % 4 == 0 && h >= 4 && h <= 304; }
 
 }  // namespace nt
 
-extern "C" int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, int max_in_degree,
+extern "C" int64_t nt_dmpnn_tile_stride(int64_t E, int max_in_degree, int rows, int ncu) {
+  if (E <= 0 || rows < 1 || max_in_degree > rows) return 0;
+  const int64_t lmax = rows + 1 - (max_in_degree > 1 ? max_in_degree : 1);  // every tile <= rows
+  if (ncu <= 0) return lmax;
+  // balance: the fewest rounds of ncu tiles at stride <= lmax, then the stride that fills them evenly
+  const int64_t rounds = (E + ncu * lmax - 1) / (ncu * lmax);
+  int64_t L = (E + rounds * ncu - 1) / (rounds * ncu);
+  return L < 1 ? 1 : (L > lmax ? lmax : L);
+}
+
+extern "C" int64_t nt_dmpnn_tile_count(int64_t E, int64_t stride) {
+  if (E <= 0 || stride <= 0) return 0;
+  return (E + stride - 1) / stride;
+}
+
+extern "C" int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, int64_t stride,
                                   int32_t* tile_ptr, int64_t ntiles, int32_t* dst_sorted,
                                   void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(V >= 0 && E >= 0 && E < (int64_t(1) << 31), NT_EINVAL, "bad sizes");
-  NT_REQUIRE(max_in_degree >= 0 && max_in_degree <= 32, NT_EUNSUPPORTED,
-             "max in-degree > 32: no fused tile plan (use the unfused path)");
-  NT_REQUIRE(ntiles == nt_dmpnn_tile_count(E, max_in_degree), NT_EINVAL,
-             "ntiles != nt_dmpnn_tile_count(E, max_in_degree)");
+  NT_REQUIRE(E == 0 || (stride >= 1 && stride < (int64_t(1) << 30)), NT_EINVAL, "bad stride");
+  NT_REQUIRE(ntiles == nt_dmpnn_tile_count(E, stride), NT_EINVAL,
+             "ntiles != nt_dmpnn_tile_count(E, stride)");
   NT_REQUIRE(dst_ptr && tile_ptr && (E == 0 || dst_sorted), NT_EINVAL, "NULL pointer");
   hipStream_t stream = as_stream(stream_);
-  const int L = 65 - (max_in_degree > 1 ? max_in_degree : 1);
-  tile_plan_kernel<<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, stream>>>(dst_ptr, V, E, L,
+  tile_plan_kernel<<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, stream>>>(dst_ptr, V, E, (int)stride,
                                                                             (int)ntiles, tile_ptr);
   NT_LAUNCH_CHECK();
   if (E > 0 && V > 0) {
@@ -645,12 +658,6 @@ extern "C" int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, 
     NT_LAUNCH_CHECK();
   }
   return NT_OK;
-}
-
-extern "C" int64_t nt_dmpnn_tile_count(int64_t E, int max_in_degree) {
-  if (E <= 0) return 0;
-  const int L = 65 - (max_in_degree > 1 ? max_in_degree : 1);
-  return (E + L - 1) / L;
 }
 
 namespace nt {

@@ -60,6 +60,9 @@ class DeviceLayout:
     # fused-update tile plan (tile_ptr, ntiles, dst_sorted, zero_fill), derived lazily on the device
     # by notorch_amd.nn.gnn._engine.fused_plan; False = not available (in-degree > 32)
     plan: object = None
+    # the fp32 layer kernel's wider plan: (tile_ptr, ntiles) of node-aligned tiles of <= 128 rows,
+    # balanced over PLAN_NCU CUs (dst_sorted / zero_fill as in `plan`); False = not available
+    plan_wide: object = None
     # backward CSRs (src -> nodes, rev_index -> edges), built lazily by _engine.backward_layout
     bwd: object = None
     # host-computed statistics the collate ships with the CSR, so a fresh batch needs no
@@ -84,7 +87,7 @@ class DeviceLayout:
     def tensors(self) -> list:
         """Every tensor the layout owns (CSR arrays, plans, chunk plans)."""
         out = [t for t in (self.dst_ptr, self.dst_perm, self.mol_ptr, self.mol_perm) if t is not None]
-        for p in (self.plan, self.dst_chunks, self.mol_chunks[1] if self.mol_chunks else None):
+        for p in (self.plan, self.plan_wide, self.dst_chunks, self.mol_chunks[1] if self.mol_chunks else None):
             if p:
                 out += [x for x in p if isinstance(x, Tensor)]
         return out
@@ -108,6 +111,7 @@ class DeviceLayout:
             self.validated,
         )
         new.plan = mv_plan(self.plan)
+        new.plan_wide = mv_plan(self.plan_wide)
         new.deg_range, new.mol_max, new.type_range = self.deg_range, self.mol_max, self.type_range
         new.dst_chunks = mv_plan(self.dst_chunks)
         if self.mol_chunks is not None and new.mol_ptr is not None:
@@ -514,19 +518,42 @@ LONG_SEGMENT = 64  # segments longer than this aggregate through the chunked red
 CHUNK_ROWS = 32  # rows per chunk of nt_segment_reduce_chunked
 
 
-def host_tile_plan(dst_ptr: np.ndarray, E: int, max_in_degree: int):
-    """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) exactly as nt_dmpnn_tile_plan builds them:
-    tile k starts at dst_ptr[first v with dst_ptr[v] >= k L], L = 65 - max(max_in_degree, 1)."""
-    L = 65 - max(int(max_in_degree), 1)
-    ntiles = (E + L - 1) // L if E > 0 else 0
+PLAN_NCU = 256  # kernels.PLAN_NCU: the CU count the balanced plans are cut for
+WIDE_TILE_ROWS = 128  # rows of the fp32 layer kernel's tiles (nt_dmpnn_fused_tile_rows, h <= 384)
+
+
+def host_tile_stride(E: int, max_in_degree: int, rows: int, ncu: int) -> int:
+    """nt_dmpnn_tile_stride restated: tiles of at most `rows` rows, balanced to whole rounds of ncu."""
+    if E <= 0 or rows < 1 or max_in_degree > rows:
+        return 0
+    lmax = rows + 1 - max(int(max_in_degree), 1)
+    if ncu <= 0:
+        return lmax
+    rounds = (E + ncu * lmax - 1) // (ncu * lmax)
+    L = (E + rounds * ncu - 1) // (rounds * ncu)
+    return max(1, min(L, lmax))
+
+
+def host_tile_ptr(dst_ptr: np.ndarray, E: int, stride: int) -> tuple:
+    """(tile_ptr[ntiles+1], ntiles) as nt_dmpnn_tile_plan builds them: tile k starts at
+    dst_ptr[first v with dst_ptr[v] >= k stride]."""
+    ntiles = (E + stride - 1) // stride if E > 0 else 0
     tile_ptr = np.empty(ntiles + 1, dtype=np.int32)
     if ntiles:
-        v = np.searchsorted(dst_ptr, np.arange(ntiles, dtype=np.int64) * L, side="left")
+        v = np.searchsorted(dst_ptr, np.arange(ntiles, dtype=np.int64) * stride, side="left")
         tile_ptr[:ntiles] = dst_ptr[v]
     tile_ptr[ntiles] = E
+    return torch.from_numpy(tile_ptr), ntiles
+
+
+def host_tile_plan(dst_ptr: np.ndarray, E: int, max_in_degree: int, rows: int = 64, ncu: int = 0):
+    """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) exactly as nt_dmpnn_tile_plan builds them with the
+    stride of nt_dmpnn_tile_stride(E, max_in_degree, rows, ncu)."""
+    stride = host_tile_stride(E, max_in_degree, rows, ncu) if E > 0 else 1
+    tile_ptr, ntiles = host_tile_ptr(dst_ptr, E, stride)
     counts = np.diff(dst_ptr.astype(np.int64))
     dsts = np.repeat(np.arange(len(counts), dtype=np.int32), counts)
-    return torch.from_numpy(tile_ptr), ntiles, torch.from_numpy(dsts)
+    return tile_ptr, ntiles, torch.from_numpy(dsts)
 
 
 def host_chunk_plan(seg_ptr: np.ndarray, chunk: int = CHUNK_ROWS):
@@ -555,8 +582,10 @@ def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional
     if E > 0 and V > 0 and maxdeg <= MAX_FUSED_IN_DEGREE:
         tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg)
         lay.plan = (tile_ptr, ntiles, dsts, mindeg == 0)
+        lay.plan_wide = host_tile_ptr(dst_ptr, E, host_tile_stride(E, maxdeg, WIDE_TILE_ROWS, PLAN_NCU))
     elif E > 0 and V > 0:
         lay.plan = False
+        lay.plan_wide = False
     lay.dst_chunks = host_chunk_plan(dst_ptr) if maxdeg > LONG_SEGMENT else False
     if mol_ptr is not None:
         n = np.diff(mol_ptr.astype(np.int64))

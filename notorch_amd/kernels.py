@@ -21,6 +21,9 @@ __all__ = [
     "pack_weights",
     "dmpnn_update",
     "tile_plan",
+    "tile_stride",
+    "fused_tile_rows",
+    "absmax",
     "fused_supported",
     "dmpnn_update_fused",
     "act_code",
@@ -178,9 +181,12 @@ def dmpnn_init(
     *,
     act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
     reduce: str = "sum",
+    amax: Tensor | None = None,
 ) -> tuple[Tensor, Tensor | None]:
-    """H0 = Xv[src] + Xe, optionally fused with S = scatter(act(H0), dst) (needs the dst CSR)."""
-    dev = _require_device(Xv, Xe, src, seg_ptr, perm)
+    """H0 = Xv[src] + Xe, optionally fused with S = scatter(act(H0), dst) (needs the dst CSR).
+    amax (fp32, 2 zero-filled device floats): raised to max|H0|, max|S| (layer 0's amax_in)."""
+    dev = _require_device(Xv, Xe, src, seg_ptr, perm, amax)
+    _require_amax(amax, Xv.dtype)
     code = _require_feat("node_feats", Xv)
     _require_feat("edge_feats", Xe, Xv.dtype)
     _require_i64("src", src)
@@ -199,8 +205,29 @@ def dmpnn_init(
     lib = _lib.load()
     _run(dev, lib.nt_dmpnn_init,
          _ptr(Xv), _ptr(Xe), _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h, act[0], act[1],
-         reduce_code(reduce), code, _ptr(H0), _ptr(S), _stream(dev))
+         reduce_code(reduce), code, _ptr(H0), _ptr(S), _ptr(amax), _stream(dev))
     return H0, S
+
+
+def _require_amax(amax: Tensor | None, dtype: torch.dtype) -> None:
+    if amax is None:
+        return
+    if dtype != torch.float32:
+        raise ValueError("amax is fp32 only")
+    if amax.dtype != torch.float32 or amax.numel() < 2 or not amax.is_contiguous():
+        raise ValueError("amax must be a contiguous float32 device tensor of 2 elements")
+
+
+def absmax(X: Tensor, out: Tensor | None = None) -> Tensor:
+    """max |X| (fp32) into out[0] (a 1-element float32 device tensor, zero-filled if not given)."""
+    dev = _require_device(X, out)
+    _require_f32("X", X)
+    if not X.is_contiguous():
+        raise ValueError("absmax: X must be contiguous")
+    if out is None:
+        out = torch.zeros(1, dtype=torch.float32, device=dev)
+    _run(dev, _lib.load().nt_absmax, _ptr(X), X.numel(), NT_F32, _ptr(out), _stream(dev))
+    return out
 
 
 def segment_reduce(
@@ -349,26 +376,46 @@ def dmpnn_update(
 
 
 def fused_supported(V: int, E: int, h: int, dtype: torch.dtype = torch.float32) -> bool:
-    """Shapes nt_dmpnn_update_fused accepts: the fp32 persistent kernel (h % 4 == 0, h <= 304) or
-    the bf16 tile kernel (h % 8 == 0, h <= 512)."""
+    """Shapes nt_dmpnn_update_fused accepts: the fp32 fk kernel (h % 4 == 0, h <= 8192) or the bf16
+    tile kernel (h % 8 == 0, h <= 512)."""
     if dtype == torch.bfloat16:
         return h % 8 == 0 and 8 <= h <= 512 and E < 2**31
-    return (dtype == torch.float32 and h % 4 == 0 and 4 <= h <= 304 and E * h // 4 < 2**31
-            and V * h // 4 < 2**31 and E < 2**31)
+    return (dtype == torch.float32 and h % 4 == 0 and 4 <= h <= 8192 and E * h // 4 < 2**31
+            and V * h // 4 < 2**31 and E < 2**31 and V < 2**31)
 
 
-def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int) -> tuple[Tensor, int, Tensor]:
-    """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) for nt_dmpnn_update_fused (max_in_degree <= 32)."""
+PLAN_NCU = 256  # CUs the balanced tile plans are cut for (MI355X; host and device plans agree)
+
+
+def fused_tile_rows(h: int, dtype: torch.dtype, act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
+                    reduce: str = "sum", agg_act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0)) -> int:
+    """Row capacity of a nt_dmpnn_update_fused tile for this layer (128 or 64)."""
+    code = NT_BF16 if dtype == torch.bfloat16 else NT_F32
+    return int(_lib.load().nt_dmpnn_fused_tile_rows(h, code, act[0], reduce_code(reduce), agg_act[0]))
+
+
+def tile_stride(E: int, max_in_degree: int, rows: int, ncu: int = PLAN_NCU) -> int:
+    """Stride of the tile plan with tiles of at most `rows` rows, balanced over ncu CUs."""
+    return int(_lib.load().nt_dmpnn_tile_stride(E, max_in_degree, rows, ncu))
+
+
+def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int, rows: int = 64,
+              ncu: int = PLAN_NCU) -> tuple[Tensor, int, Tensor]:
+    """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) for nt_dmpnn_update_fused: node-aligned tiles of
+    at most `rows` rows (max_in_degree <= 32), balanced to whole rounds of ncu tiles."""
     dev = _require_device(dst_ptr)
     if dst_ptr.dtype != torch.int32:
         raise TypeError("dst_ptr must be int32")
     V = dst_ptr.numel() - 1
     lib = _lib.load()
-    ntiles = int(lib.nt_dmpnn_tile_count(E, max_in_degree))
+    stride = tile_stride(E, max_in_degree, rows, ncu) if E > 0 else 1
+    if E > 0 and stride <= 0:
+        raise ValueError(f"max in-degree {max_in_degree} exceeds the tile rows {rows}")
+    ntiles = int(lib.nt_dmpnn_tile_count(E, stride))
     tile_ptr = torch.empty(ntiles + 1, dtype=torch.int32, device=dev)
     dsts = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
     _run(dev, lib.nt_dmpnn_tile_plan,
-         _ptr(dst_ptr), V, E, max_in_degree, _ptr(tile_ptr), ntiles, _ptr(dsts), _stream(dev))
+         _ptr(dst_ptr), V, E, stride, _ptr(tile_ptr), ntiles, _ptr(dsts), _stream(dev))
     return tile_ptr, ntiles, dsts
 
 
@@ -383,22 +430,30 @@ def dmpnn_update_fused(
     residual: bool = True,
     act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
     plan: tuple[Tensor, int, Tensor] | None = None,
+    tile_rows: int = 64,
+    max_in_degree: int = 32,
     perm: Tensor | None = None,
     reduce: str = "sum",
     agg_act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
     zero_fill: bool = False,
+    amax_in: Tensor | None = None,
+    amax_out: Tensor | None = None,
     out: Tensor | None = None,
     S_out: Tensor | None = None,
 ) -> tuple[Tensor, Tensor | None]:
-    """H_out = (residual ? H : 0) + (S[src] - act(H[rev])) @ W^T + b and, with a tile plan,
-    S_out = scatter(agg_act(H_out), dst, reduce) in the same persistent launch.
+    """H_out = (residual ? H : 0) + (S[src] - act(H[rev])) @ W^T + b and, with a tile plan (tiles of at
+    most ``tile_rows`` rows), S_out = scatter(agg_act(H_out), dst, reduce) in the same persistent launch.
 
+    fp32: ``amax_in`` = (max|H|, max|S|) on the device (computed here with nt_absmax when not given);
+    ``amax_out`` (2 zero-filled floats) receives max|H_out|, max|S_out| for the next layer.
     ``zero_fill`` must be True when some node has no in-edge (its S_out row is then 0)."""
-    dev = _require_device(H, S, src, rev, Wp, bias, out, S_out, perm)
+    dev = _require_device(H, S, src, rev, Wp, bias, out, S_out, perm, amax_in, amax_out)
     code = _require_feat("H", H)
     _require_feat("S", S, H.dtype)
     _require_i64("src", src)
     _require_i64("rev_index", rev)
+    _require_amax(amax_in, H.dtype)
+    _require_amax(amax_out, H.dtype)
     E, h = H.shape
     V = S.shape[0]
     if S.shape[1] != h or src.numel() != E or rev.numel() != E:
@@ -424,25 +479,40 @@ def dmpnn_update_fused(
     else:
         perm = None
         S_out = None
+    if H.dtype == torch.float32 and amax_in is None and E > 0:
+        amax_in = torch.zeros(2, dtype=torch.float32, device=dev)
+        absmax(H.contiguous(), amax_in[0:1])
+        absmax(S.contiguous(), amax_in[1:2])
     lib = _lib.load()
     _run(dev, lib.nt_dmpnn_update_fused,
          _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
-         act[0], act[1], _ptr(tile_ptr), ntiles, _ptr(perm), _ptr(dsts), reduce_code(reduce),
-         agg_act[0], agg_act[1], code, _ptr(out), _ptr(S_out), _stream(dev))
+         act[0], act[1], _ptr(tile_ptr), ntiles, int(tile_rows), int(max_in_degree), _ptr(perm), _ptr(dsts),
+         reduce_code(reduce), agg_act[0], agg_act[1], code, _ptr(amax_in), _ptr(amax_out), _ptr(out),
+         _ptr(S_out), _stream(dev))
     return out, S_out
 
 
-def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None) -> Tensor:
-    """X @ W^T for the packed image Wp of W (fp32, h % 4 == 0, h <= 304): the layer GEMM alone on
-    the bf16x6 MFMA kernel.  With Wp = pack_weights(W.t()) it is the backward's dA = G @ W."""
+def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None, *, kernel: str = "fk") -> Tensor:
+    """X @ W^T for the packed image Wp of W (fp32, h % 4 == 0): the layer GEMM alone.  With
+    Wp = pack_weights(W.t()) it is the backward's dA = G @ W.  kernel = "fk": the fp16x3 layer kernel
+    in dense mode (max|X| by nt_absmax first, any h); "pk": the bf16x6 persistent kernel (h <= 304)."""
     dev = _require_device(X, Wp, out)
     _require_f32("X", X)
     M, h = X.shape
     if Wp.numel() != packed_weight_numel(h, X.dtype):
         raise ValueError("Wp is not a packed fp32 weight image for this hidden size")
+    if not X.is_contiguous():
+        raise ValueError("dense_matmul: X must be contiguous")
     if out is None:
         out = torch.empty_like(X)
-    _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_F32, _ptr(out), _stream(dev))
+    amax = None
+    if kernel == "fk":
+        amax = torch.zeros(2, dtype=torch.float32, device=dev)
+        absmax(X, amax[1:2])
+    elif kernel != "pk":
+        raise ValueError("kernel must be 'fk' or 'pk'")
+    _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_F32, _ptr(amax), _ptr(out),
+         _stream(dev))
     return out
 
 
@@ -646,10 +716,13 @@ def dmpnn_init_embed(
     act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
     reduce: str = "sum",
     validate: bool = True,
+    amax: Tensor | None = None,
 ) -> tuple[Tensor, Tensor | None]:
     """H0 = Xv[src] + Xe with Xv = EmbeddingBag(node_table)(node_types), Xe likewise, never
-    materialised; optionally fused with S = scatter(act(H0), dst) (needs the dst CSR)."""
-    dev = _require_device(node_table, node_types, edge_table, edge_types, src, seg_ptr, perm)
+    materialised; optionally fused with S = scatter(act(H0), dst) (needs the dst CSR).
+    amax (fp32, 2 zero-filled device floats): raised to max|H0|, max|S|."""
+    dev = _require_device(node_table, node_types, edge_table, edge_types, src, seg_ptr, perm, amax)
+    _require_amax(amax, node_table.dtype)
     code = _require_feat("node_table", node_table)
     _require_feat("edge_table", edge_table, node_table.dtype)
     if node_table.shape[1] != edge_table.shape[1]:
@@ -668,7 +741,7 @@ def dmpnn_init_embed(
     _run(dev, _lib.load().nt_dmpnn_init_embed,
          _ptr(node_table), node_table.shape[0], _ptr(node_types), kv, _ptr(edge_table),
          edge_table.shape[0], _ptr(edge_types), ke, _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h,
-         act[0], act[1], reduce_code(reduce), code, _ptr(H0), _ptr(S), _stream(dev))
+         act[0], act[1], reduce_code(reduce), code, _ptr(H0), _ptr(S), _ptr(amax), _stream(dev))
     return H0, S
 
 

@@ -64,13 +64,15 @@ def _note_update(kind: str, dtype: torch.dtype, h: int) -> None:
                     kernel_short="update_bf16", numerics="bf16 storage, bf16 MFMA, fp32 accumulate",
                     products=1)
     elif kind == "fused":
-        info = dict(kernel="update_pk_kernel (persistent producer/consumer, bf16x6 16x16x32 MFMA, "
-                           "aggregation of the next layer fused)", kernel_short="update_pk",
-                    numerics="fp32 via bf16x6 split (6 bf16 MFMA products, fp32 accumulate)", products=6)
+        info = dict(kernel="update_fk_kernel (persistent, 128-row node-aligned tiles, two-part fp16 split on "
+                           "16x16x32 fp16 MFMA, aggregation of the next layer fused)", kernel_short="update_fk",
+                    numerics="fp32 via scaled two-part fp16 split (3 fp16 MFMA products, fp32 accumulate)",
+                    products=3)
     elif kind == "persistent":
-        info = dict(kernel="update_pk_kernel without tile plan (hub graph: aggregation by the chunked "
-                           "segment reduce)", kernel_short="update_pk",
-                    numerics="fp32 via bf16x6 split (6 bf16 MFMA products, fp32 accumulate)", products=6)
+        info = dict(kernel="update_fk_kernel without tile plan (hub graph: aggregation by the chunked "
+                           "segment reduce)", kernel_short="update_fk",
+                    numerics="fp32 via scaled two-part fp16 split (3 fp16 MFMA products, fp32 accumulate)",
+                    products=3)
     else:
         info = dict(kernel="nt_dmpnn_update (unfused fp32 update kernel)", kernel_short="update",
                     numerics="fp32 via bf16x6 split", products=6)
@@ -162,18 +164,26 @@ def _degree_range(lay: DeviceLayout) -> tuple[int, int]:
     return mm
 
 
-def fused_plan(lay: DeviceLayout, V: int, E: int):
-    """Tile plan of the fused update for this layout (cached on it), or None when some node has more
-    than 32 in-edges (polymer hubs): those graphs take the unfused path.  One sync per layout."""
+def fused_plan(lay: DeviceLayout, V: int, E: int, rows: int = 64):
+    """Tile plan of the fused update for this layout with tiles of at most ``rows`` (64 or 128) rows,
+    as (tile_ptr, ntiles, dst_sorted, zero_fill), cached on it; None when some node has more than 32
+    in-edges (polymer hubs): those graphs take the unfused path.  One sync per layout."""
     if lay.plan is None:
         plan = False
         if E > 0 and V > 0:
             maxdeg, mindeg = _degree_range(lay)
             if maxdeg <= 32:
-                tile_ptr, ntiles, dsts = K.tile_plan(lay.dst_ptr, E, maxdeg)
+                tile_ptr, ntiles, dsts = K.tile_plan(lay.dst_ptr, E, maxdeg, rows=64, ncu=0)
                 plan = (tile_ptr, ntiles, dsts, mindeg == 0)
         lay.plan = plan
-    return lay.plan or None
+    if not lay.plan:
+        return None
+    if rows <= 64:
+        return lay.plan
+    if lay.plan_wide is None:  # node-aligned tiles of <= 128 rows, balanced over the CUs
+        tile_ptr, ntiles, _ = K.tile_plan(lay.dst_ptr, E, _degree_range(lay)[0], rows=128)
+        lay.plan_wide = (tile_ptr, ntiles)
+    return lay.plan_wide[0], lay.plan_wide[1], lay.plan[2], lay.plan[3]
 
 
 def dst_chunks(lay: DeviceLayout):
@@ -241,17 +251,30 @@ def block_forward(
     drop = (p, seed): training-mode dropout of every layer update (layer l draws from
     dropout_offset(l, E, h))."""
     V = Xv.shape[0]
+    amax = _amax_buffer(len(weights), Xv)
+    a0 = None if amax is None else amax[0]
     if len(weights) == 0:
         H, _ = K.dmpnn_init(Xv, Xe, src)
         return _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states,
                                drop)
     chunks = dst_chunks(lay)
     if chunks is not None:  # hubs: the fused init would walk a hub's in-edges on one lane
-        H, _ = K.dmpnn_init(Xv, Xe, src)
+        H, _ = K.dmpnn_init(Xv, Xe, src, amax=a0)
         S = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks)
+        if a0 is not None:
+            K.absmax(S, a0[1:2])
     else:
-        H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce)
-    return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop)
+        H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce, amax=a0)
+    return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop,
+                           amax)
+
+
+def _amax_buffer(d: int, X: Tensor) -> Optional[Tensor]:
+    """(d + 1) x 2 zeros: row l = (max|H_l|, max|S_l|), the fp32 layer kernel's split scales (the
+    init writes row 0, layer l reads row l and writes row l + 1).  None for bf16."""
+    if X.dtype != torch.float32 or d == 0:
+        return None
+    return torch.zeros(d + 1, 2, dtype=torch.float32, device=X.device)
 
 
 def dropout_offset(l: int, E: int, h: int) -> int:
@@ -286,16 +309,21 @@ def block_forward_embedded(
         H, _ = K.dmpnn_init_embed(node_table, node_types, edge_table, edge_types, src, validate=validate)
         node, H, _ = _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, False)
         return node, H
+    amax = _amax_buffer(len(weights), node_table)
     H, S = K.dmpnn_init_embed(node_table, node_types, edge_table, edge_types, src, lay.dst_ptr,
-                              lay.dst_perm, act=act, reduce=reduce, validate=validate)
-    node, H, _ = _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, False)
+                              lay.dst_perm, act=act, reduce=reduce, validate=validate,
+                              amax=None if amax is None else amax[0])
+    node, H, _ = _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, False,
+                                 amax=amax)
     return node, H
 
 
-def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop=None):
+def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop=None,
+                    amax=None):
     """The d layers + final node scatter, from H0 and layer 0's aggregation S.  With dropout the
     update runs without its residual and nt_dropout_residual adds it back (the fused and persistent
-    kernels write H_out directly, so dropout takes the unfused update)."""
+    kernels write H_out directly, so dropout takes the unfused update).  amax (fp32): the split
+    scales, row 0 filled by the init (see _amax_buffer)."""
     d = len(weights)
     chunks = dst_chunks(lay)
     if d == 0:
@@ -303,16 +331,25 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
         return node, H, []
     Wps = pack_layer_weights(weights)
     E, h = H.shape
-    plan = (fused_plan(lay, V, E) if drop is None and _fused_enabled() and K.fused_supported(V, E, h, H.dtype)
-            else None)
+    fp32 = H.dtype == torch.float32
+    if fp32 and amax is None:
+        amax = _amax_buffer(d, H)
+        K.absmax(H, amax[0, 0:1])
+        K.absmax(S, amax[0, 1:2])
+    fusable = drop is None and _fused_enabled() and K.fused_supported(V, E, h, H.dtype)
+    rows = 64
+    if fusable and fp32:  # the fp32 kernel's tile capacity for every layer of this block
+        rows = min(K.fused_tile_rows(h, H.dtype, act, reduce, act),
+                   K.fused_tile_rows(h, H.dtype, act, reduce, _IDENTITY))
+    plan = fused_plan(lay, V, E, rows) if fusable else None
     if plan is not None:
-        return _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual, keep_states)
+        return _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, residual, keep_states,
+                              amax)
     states = []
     spare: Optional[Tensor] = None  # ping-pong buffer when states are not kept
-    # graphs the fused plan cannot take (in-degree > 32): fp32 still runs the persistent kernel,
-    # unfused, with the aggregation as a separate segment reduce
-    persistent = (drop is None and _fused_enabled() and H.dtype == torch.float32
-                  and K.fused_supported(V, E, h, H.dtype))
+    # graphs the fused plan cannot take (in-degree > 32): fp32 still runs the persistent layer kernel,
+    # without its aggregation (a separate segment reduce)
+    persistent = fusable and fp32
     timer = UPDATE_EVENTS
     _note_update("persistent" if persistent else "unfused", H.dtype, h)
     for l in range(d):
@@ -326,9 +363,9 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
             U = K.dmpnn_update(H, S, src, rev, Wps[l], b_l, residual=False, act=act, out=spare)
             Hn = K.dropout_residual(U, drop[0], drop[1], dropout_offset(l, E, h),
                                     base=H if residual else None, out=U)
-        elif persistent:  # the persistent pk kernel without its fused aggregation (hub graphs)
+        elif persistent:  # the persistent kernel without its fused aggregation (hub graphs)
             Hn, _ = K.dmpnn_update_fused(H, S, src, rev, Wps[l], b_l, residual=residual, act=act,
-                                         out=spare)
+                                         amax_in=amax[l], amax_out=amax[l + 1], out=spare)
         else:
             Hn = K.dmpnn_update(H, S, src, rev, Wps[l], b_l, residual=residual, act=act, out=spare)
         if timer is not None:
@@ -337,6 +374,8 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
         if l < d - 1:
             S = _aggregate(Hn, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks,
                            out=None if keep_states else S)
+            if persistent:
+                K.absmax(S, amax[l + 1, 1:2])
         if not keep_states:
             spare = H  # H_l is dead once H_{l+1} exists: reuse its buffer for H_{l+2}
         H = Hn
@@ -346,13 +385,14 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
     return node, H, states
 
 
-def _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual, keep_states):
+def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, residual, keep_states, amax):
     tile_ptr, ntiles, dsts, zero_fill = plan
     d = len(Wps)
     states = []
     spare_H: Optional[Tensor] = None
     spare_S: Optional[Tensor] = None
     timer = UPDATE_EVENTS
+    maxdeg = _degree_range(lay)[0]
     _note_update("fused", H.dtype, H.shape[1])
     for l in range(d):
         last = l == d - 1
@@ -363,8 +403,9 @@ def _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual
             ev[0].record()
         Hn, Sn = K.dmpnn_update_fused(
             H, S, src, rev, Wps[l], None if biases[l] is None else biases[l].detach(),
-            residual=residual, act=act, plan=(tile_ptr, ntiles, dsts), perm=lay.dst_perm,
-            reduce=reduce, agg_act=_IDENTITY if last else act, zero_fill=zero_fill,
+            residual=residual, act=act, plan=(tile_ptr, ntiles, dsts), tile_rows=rows, max_in_degree=maxdeg,
+            perm=lay.dst_perm, reduce=reduce, agg_act=_IDENTITY if last else act, zero_fill=zero_fill,
+            amax_in=None if amax is None else amax[l], amax_out=None if amax is None else amax[l + 1],
             out=spare_H, S_out=None if last else spare_S,
         )
         if timer is not None:
@@ -374,7 +415,7 @@ def _fused_forward(H, S, src, rev, lay, plan, Wps, biases, act, reduce, residual
             spare_H = H
             spare_S = S
         H, S = Hn, Sn
-    if H.dtype == torch.float32:  # the persistent kernel's bounded waits (bf16 has none)
+    if H.dtype == torch.float32:  # the persistent kernel's device status word
         K.watch_device_status(H.device)
     return S, H, states
 
@@ -580,7 +621,7 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             dbs[l] = Gu.sum(0)
             del A
         if Gu.dtype == torch.float32 and K.fused_supported(V, E, h, Gu.dtype):
-            dA = K.dense_matmul(Gu.contiguous(), K.pack_weights(W.t().contiguous()))  # bf16x6 MFMA
+            dA = K.dense_matmul(Gu.contiguous(), K.pack_weights(W.t().contiguous()))  # fp16x3 MFMA
         else:
             dA = torch.mm(Gu, W)
         del Gu

@@ -98,9 +98,10 @@ class ChempropLayer(nn.Module):
             Xv = torch.zeros(V, edge_feats.shape[1], device=edge_feats.device, dtype=edge_feats.dtype)
             # H0 = Xv[src] + Xe = edge_feats exactly (adding +0.0)
             if act is None:
+                act_params = list(self.act.parameters())
                 _, H = _engine.LayerwiseBlockFunction.apply(
                     Xv, edge_feats, edge_index, rev_index.contiguous(), lay, [(self.act, None)], [drop],
-                    self.reduce, False, 1, self.linear.weight, self.linear.bias,
+                    self.reduce, False, 1, len(act_params), self.linear.weight, self.linear.bias, *act_params,
                 )
                 return H
             _, H = _engine.ChempropBlockFunction.apply(

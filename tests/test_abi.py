@@ -24,7 +24,9 @@ def test_header_declares_the_boundary():
         "nt_dmpnn_update_fused", "nt_dmpnn_message", "nt_dmpnn_edge_backward", "nt_gather_rows",
         "nt_embed_bag", "nt_dmpnn_init_embed", "nt_node_scores", "nt_softmax_pool",
         "nt_collate_graphs", "nt_segment_reduce_chunked", "nt_device_status", "nt_device_status_reset",
-        "nt_dmpnn_dense_matmul", "nt_dmpnn_weight_grad", "nt_dmpnn_weight_grad_workspace", "nt_segment_arg", "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg",
+        "nt_dmpnn_dense_matmul", "nt_dmpnn_weight_grad", "nt_dmpnn_weight_grad_workspace", "nt_segment_arg",
+        "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg", "nt_absmax", "nt_dmpnn_fused_tile_rows",
+        "nt_dmpnn_tile_stride",
     }
 
 
@@ -44,7 +46,7 @@ def test_abi_version_and_errors_without_gpu():
     from notorch_amd import _lib
 
     lib = _lib.load()
-    assert lib.nt_abi_version() == _lib.ABI_VERSION == 1
+    assert lib.nt_abi_version() == _lib.ABI_VERSION == 2
     assert lib.nt_dmpnn_packed_weight_bytes(300, 0) > 0
     assert lib.nt_dmpnn_packed_weight_bytes(0, 0) == 0
     # argument validation happens before any device call: EINVAL + message

@@ -162,3 +162,34 @@ def test_all_zero_bond_batch_collates():
     assert G.edge_feats.shape == (0, 2) and G.edge_index.shape == (2, 0) and G.rev_index.shape == (0,)
     assert G.batch_node_index.tolist() == [0, 1, 2]
     assert G._nt_layout.dst_ptr.tolist() == [0, 0, 0, 0]
+
+
+def test_host_tile_stride_matches_library():
+    """The host restatement of nt_dmpnn_tile_stride (collate-shipped plans) equals the library's."""
+    from notorch_amd import _lib
+    from notorch_amd.data.models.graph import host_tile_stride
+
+    lib = _lib.load()
+    for E in (1, 7, 614, 77_628, 620_000, 2_370_000):
+        for maxdeg in (1, 4, 13, 32):
+            for rows, ncu in ((64, 0), (128, 256), (128, 0), (64, 256), (128, 80)):
+                assert host_tile_stride(E, maxdeg, rows, ncu) == lib.nt_dmpnn_tile_stride(E, maxdeg, rows, ncu)
+
+
+def test_collate_ships_balanced_wide_plan():
+    """The collate's 128-row plan: node-aligned tiles of <= 128 rows, cut to whole rounds of 256 tiles
+    (config 2: about 3 tiles per CU), next to the 64-row plan of the bf16 kernel."""
+    import numpy as np
+
+    from notorch_amd.data.synth import make_batch
+
+    G = make_batch("qm9", 4096, seed=1000).collate("nodes")
+    lay = G._nt_layout
+    tile_ptr, ntiles = lay.plan_wide
+    tp = tile_ptr.numpy().astype(np.int64)
+    sizes = np.diff(tp)
+    assert tp[0] == 0 and tp[-1] == G.num_edges and sizes.max() <= 128 and sizes.min() > 0
+    starts = set(lay.dst_ptr.numpy().tolist())
+    assert all(int(t) in starts for t in tp)  # every cut is a node boundary
+    assert 2 * 256 < ntiles <= 3 * 256
+    assert lay.plan[1] > ntiles  # the 64-row plan has more, smaller tiles

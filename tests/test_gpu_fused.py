@@ -366,16 +366,28 @@ def test_xcd_walk_branches(dtype, case):
     assert_parity(Sn.float(), rS, tol, f"{case} S ntiles={ntiles}")
 
 
+@pytest.mark.parametrize("kernel", ["fk", "pk"])
 @pytest.mark.parametrize("h,M", [(300, 77_000), (300, 1), (100, 1000), (64, 4097), (4, 3)])
-def test_dense_matmul_x6(h, M):
-    """nt_dmpnn_dense_matmul (the backward's dA = G W, chemprop.py:41 under autograd): the
-    persistent kernel's dense mode against fp64, fp32 contract."""
+def test_dense_matmul(h, M, kernel):
+    """nt_dmpnn_dense_matmul (the backward's dA = G W, chemprop.py:41 under autograd): the fp16x3 fk
+    kernel's and the bf16x6 pk kernel's dense modes against fp64, fp32 contract."""
+    K = _K()
+    g = torch.Generator().manual_seed(M + h)
+    X, W = torch.randn(M, h, generator=g), torch.randn(h, h, generator=g) / h ** 0.5
+    out = K.dense_matmul(X.to(DEV), K.pack_weights(W.t().contiguous().to(DEV)), kernel=kernel)
+    ref = X.double() @ W.double()
+    assert_parity(out, ref, FP32_NORM_TOL, f"dense {kernel} h={h} M={M}")
+
+
+@pytest.mark.parametrize("h,M", [(640, 3000), (1024, 700)])
+def test_dense_matmul_wide_hidden(h, M):
+    """Hidden sizes beyond 512 (the reference takes any hidden_dim, chemprop.py:54): the fk kernel's
+    column chunks in dense mode."""
     K = _K()
     g = torch.Generator().manual_seed(M + h)
     X, W = torch.randn(M, h, generator=g), torch.randn(h, h, generator=g) / h ** 0.5
     out = K.dense_matmul(X.to(DEV), K.pack_weights(W.t().contiguous().to(DEV)))
-    ref = X.double() @ W.double()
-    assert_parity(out, ref, FP32_NORM_TOL, f"dense h={h} M={M}")
+    assert_parity(out, X.double() @ W.double(), FP32_NORM_TOL, f"dense h={h} M={M}")
 
 
 @pytest.mark.parametrize("h,E,act", [(300, 77_840, "relu"), (300, 1, "relu"), (100, 1000, "identity"),
