@@ -227,8 +227,8 @@ NT_API int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, i
  *   S_out[v] = reduce_{e: dst[e]=v} agg_act(H_out[e])      (ascending e; empty segment -> 0)
  * (tile_ptr, ntiles, dst_sorted) = nt_dmpnn_tile_plan with tiles of at most tile_rows <=
  * nt_dmpnn_fused_tile_rows(h, dtype, act, reduce, agg_act) rows; max_in_degree >= the graph's largest
- * in-degree (<= 32); perm = the dst CSR permutation.  Nodes without in-edges are not written (the
- * caller zero-fills S_out).  With tile_ptr = NULL (and perm, dst_sorted, S_out = NULL) only H_out
+ * in-degree (<= 32); perm = the dst CSR permutation (bf16); row_table = nt_dmpnn_row_table (fp32).
+ * Nodes without in-edges are not written (the caller zero-fills S_out).  With tile_ptr = NULL (and perm, dst_sorted, S_out = NULL) only H_out
  * is computed.
  * fp32 (h % 4 == 0, any h): two-part fp16 split on fp16 MFMA (fp32 accuracy); amax_in = 2 device
  * floats >= max|H|, max|S| (from nt_dmpnn_init / the previous layer's amax_out / nt_absmax);
@@ -240,9 +240,19 @@ NT_API int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* sr
                                  const void* Wp, const void* b, int64_t V, int64_t E, int64_t h,
                                  int residual, int act, float act_alpha, const int32_t* tile_ptr,
                                  int64_t ntiles, int tile_rows, int max_in_degree, const int32_t* perm,
-                                 const int32_t* dst_sorted, int reduce, int agg_act, float agg_alpha,
-                                 int dtype, const float* amax_in, float* amax_out, void* H_out,
-                                 void* S_out, void* stream);
+                                 const int32_t* dst_sorted, const void* row_table, int reduce,
+                                 int agg_act, float agg_alpha, int dtype, const float* amax_in,
+                                 float* amax_out, void* H_out, void* S_out, void* stream);
+
+/*
+ * Row table of a fused plan for the fp32 layer kernel: one int32 x 4 entry per dst-sorted position p
+ *   { e = perm[p], src[e] (-1 if outside [0, V)), rev[e] (-1 if outside [0, E)),
+ *     (dst_sorted[p] << 2) | (first in-edge of its node) | (last in-edge of its node) << 1 }
+ * so the kernel reaches a tile's rows in one dependent load.  Depends only on the graph (cache it
+ * with the plan).  V < 2^29, E < 2^31; out: E x 16 bytes, 16-byte aligned.
+ */
+NT_API int nt_dmpnn_row_table(const int32_t* perm, const int32_t* dst_sorted, const int64_t* src,
+                              const int64_t* rev, int64_t V, int64_t E, void* out, void* stream);
 
 /*
  * Attention readout scores (notorch/nn/gnn/agg.py:50-86), one per node row X[v] (n x h):

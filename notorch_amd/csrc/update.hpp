@@ -52,8 +52,9 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
 int fk_tile_rows(int64_t h, int act, int reduce, int aact, bool fused);
 int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in, float* amax_out,
                      const int32_t* tile_ptr, int64_t ntiles, int tile_rows, int max_in_degree,
-                     const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
-                     float* S_out);
+                     const void* row_table, int reduce, int aact, float aalpha, float* S_out);
+int fk_row_table(const int32_t* perm, const int32_t* dsts, const int64_t* src, const int64_t* rev, int64_t V,
+                 int64_t E, void* out, hipStream_t stream);
 int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_t img_stride, void* img,
             hipStream_t stream);
 int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);

@@ -580,6 +580,18 @@ extern "C" int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduc
   return nt::fk_tile_rows(h, act, reduce, agg_act, true);
 }
 
+extern "C" int nt_dmpnn_row_table(const int32_t* perm, const int32_t* dst_sorted, const int64_t* src,
+                                  const int64_t* rev, int64_t V, int64_t E, void* out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(V >= 0 && E >= 0 && E < (int64_t(1) << 31) && V < (int64_t(1) << 29), NT_EINVAL,
+             "bad sizes (E < 2^31, V < 2^29)");
+  if (E == 0) return NT_OK;
+  NT_REQUIRE(perm && dst_sorted && src && rev && out, NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(aligned16(out), NT_EINVAL, "out must be 16-byte aligned");
+  return fk_row_table(perm, dst_sorted, src, rev, V, E, out, as_stream(stream_));
+}
+
 extern "C" int nt_absmax(const void* X, int64_t n, int dtype, float* out, void* stream_) {
   using namespace nt;
   clear_error();
@@ -644,8 +656,8 @@ extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t
                                      int64_t E, int64_t h, int residual, int act, float act_alpha,
                                      const int32_t* tile_ptr, int64_t ntiles, int tile_rows,
                                      int max_in_degree, const int32_t* perm,
-                                     const int32_t* dst_sorted, int reduce, int agg_act,
-                                     float agg_alpha, int dtype, const float* amax_in,
+                                     const int32_t* dst_sorted, const void* row_table, int reduce,
+                                     int agg_act, float agg_alpha, int dtype, const float* amax_in,
                                      float* amax_out, void* H_out, void* S_out, void* stream_) {
   using namespace nt;
   clear_error();
@@ -671,9 +683,9 @@ extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t
   }
   UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                0, 0, residual, act, act_alpha, (float*)H_out, as_stream(stream_)};
+  NT_REQUIRE(row_table == nullptr || aligned16(row_table), NT_EINVAL, "row_table must be 16-byte aligned");
   return launch_update_fk(a, (const char*)Wp + fk_offset(h), amax_in, amax_out, tile_ptr, ntiles,
-                          tile_rows, max_in_degree, perm, dst_sorted, reduce, agg_act, agg_alpha,
-                          (float*)S_out);
+                          tile_rows, max_in_degree, row_table, reduce, agg_act, agg_alpha, (float*)S_out);
 }
 
 // out = X W^T (the layer GEMM alone: no gathers, no residual, no bias); the backward's dA = G W passes
@@ -696,7 +708,7 @@ extern "C" int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const 
     UpdateArgs a{nullptr, (const float*)X, nullptr, nullptr, Wp, nullptr, M, M, h,
                  0, 0, 0, NT_ACT_IDENTITY, 0.f, (float*)out, as_stream(stream_)};
     return launch_update_fk(a, (const char*)Wp + fk_offset(h), amax_in, nullptr, nullptr, 0, 0, 0, nullptr,
-                            nullptr, NT_SUM, NT_ACT_IDENTITY, 0.f, nullptr);
+                            NT_SUM, NT_ACT_IDENTITY, 0.f, nullptr);
   }
   const UpdateGeom g = geom_for(h);
   UpdateArgs a{(const float*)X, (const float*)X, nullptr, nullptr,

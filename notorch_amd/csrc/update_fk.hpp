@@ -73,8 +73,8 @@ struct Args {
   float alpha;
   const int* tile_ptr;  // NULL: fixed tiles of 16 RT rows in edge order (no aggregation)
   int ntiles;
-  const int* perm;  // dst-sorted position -> edge (fused mode)
-  const int* dsts;  // dst-sorted position -> node (fused mode)
+  const int4* rows;  // fused mode: row table {edge, src, rev, (node << 2) | start | end << 1} per
+                     // dst-sorted position (nt_dmpnn_row_table)
   int reduce, aact;
   float aalpha;
   float* O;
@@ -137,17 +137,13 @@ __device__ __forceinline__ float dpp_ror1(float x) {
 }
 
 // --------------------------------------------------------------------------- per-row tile info
-struct RowSrc {
-  int soff, qoff;  // float4 offsets of S[src[e]] and H[rev[e]] rows (-1: none / row past the tile)
-};
-
-struct TileHead {  // level 1: tile bounds
+struct TileHead {  // tile bounds (uniform: scalar loads)
   int T, n;
 };
 
-template <int RT>
+template <int RT, bool PLAN>
 __device__ __forceinline__ TileHead tile_head(const Args& a, int t) {
-  if (a.tile_ptr) {
+  if constexpr (PLAN) {
     const int T = a.tile_ptr[t], n = a.tile_ptr[t + 1] - T;
     return {T, n};
   }
@@ -156,35 +152,27 @@ __device__ __forceinline__ TileHead tile_head(const Args& a, int t) {
   return {(int)T, (int)n};
 }
 
-struct RowIdx {  // level 2: edge and node of the thread's row
-  int e, v, flags;
-};
-
-template <int RT>
-__device__ __forceinline__ RowIdx row_idx(const Args& a, TileHead th, int row) {
-  RowIdx r{-1, -1, kFlagStart | kFlagEnd};
-  const int n = th.n < 16 * RT ? th.n : 16 * RT;
-  if (row < n) {
-    const int pos = th.T + row;
-    r.e = a.perm ? a.perm[pos] : pos;
-    if (a.SO) {
-      r.v = a.dsts[pos];
-      const int vp = row > 0 ? a.dsts[pos - 1] : -1;
-      const int vn = row + 1 < n ? a.dsts[pos + 1] : -1;
-      r.flags = (vp != r.v ? kFlagStart : 0) | (vn != r.v ? kFlagEnd : 0);
-    }
-  }
-  return r;
+// The thread's row of a tile in one dependent step: the row-table entry (fused mode) or
+// {edge, src, rev} of the edge-ordered position (plain / dense mode).  Rows past the tile read the
+// tile's first row (valid memory, no branch) and are masked by row < n at use.
+template <int RT, bool TABLE>
+__device__ __forceinline__ int4 row_raw(const Args& a, TileHead th, int row) {
+  const int pos = th.T + (row < th.n ? row : 0);
+  if constexpr (TABLE) return a.rows[pos];
+  const int s = a.src ? (int)a.src[pos] : pos;
+  const int q = a.rev ? (int)a.rev[pos] : -1;
+  return int4{pos, s, q, kFlagStart | kFlagEnd};
 }
 
-__device__ __forceinline__ RowSrc row_src(const Args& a, int e) {  // level 3
-  RowSrc rs{-1, -1};
-  if (e >= 0) {
-    const int64_t s = a.src ? a.src[e] : e, q = a.rev ? a.rev[e] : -1;
-    rs.soff = (s >= 0 && s < a.V) ? (int)s * a.hv : -1;
-    rs.qoff = (q >= 0 && q < a.E) ? (int)q * a.hv : -1;
-  }
-  return rs;
+// float4 offsets of the S[src] and H[rev] rows (-1: none / row past the tile)
+__device__ __forceinline__ int2 row_offsets(const Args& a, int4 raw, bool valid) {
+  const bool sok = valid && raw.y >= 0 && raw.y < a.V, qok = valid && raw.z >= 0 && raw.z < a.E;
+  return int2{sok ? raw.y * a.hv : -1, qok ? raw.z * a.hv : -1};
+}
+
+// emap entry {edge (-1 past the tile), node, flags, 0}
+__device__ __forceinline__ int4 row_entry(int4 raw, bool valid) {
+  return valid ? int4{raw.x, raw.w >> 2, raw.w & 3, 0} : int4{-1, -1, kFlagStart | kFlagEnd, 0};
 }
 
 // --------------------------------------------------------------------------- kernel
@@ -197,6 +185,7 @@ struct State {
   static constexpr int kPartB = RT * 1024;  // one fp16 part of a k-slice
   static constexpr int kBufB = 2 * kPartB;  // both parts
   f32x4 acc[RT][CT];
+  f32x4 bias[CT];      // bias of the thread's 4 columns per column tile, for the next epilogue
   uint4 wb[2][CT][2];  // W fragments (parity, column tile, part)
   f32x4 gs[GD][PPT], gq[GD][PPT];  // staged pieces, GD k-steps ahead
   int gso[GD], gqo[GD];  // their row sources
@@ -215,13 +204,15 @@ __device__ __forceinline__ void fk_gather(State<RT, CT, GD>& st, const Args& a, 
   st.gqo[P] = qoff;
   const int sb = soff >= 0 ? soff : 0, qb = qoff >= 0 ? qoff : 0;
   const f32x4* S4 = reinterpret_cast<const f32x4*>(a.S);
-  const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H);
+  // no H (dense mode): read S's first rows instead (qoff is -1, the piece is masked at the split),
+  // so the load is unconditional and the compiler's vmcnt waits stay counted
+  const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H ? a.H : a.S);
 #pragma unroll
   for (int u = 0; u < State<RT, CT, GD>::PPT; ++u) {
     int p = 8 * s + st.kp0 + u;
     p = p < st.hv ? p : 0;
     st.gs[P][u] = S4[sb + p];
-    st.gq[P][u] = H4 ? H4[qb + p] : f32x4{0.f, 0.f, 0.f, 0.f};
+    st.gq[P][u] = H4[qb + p];
   }
 }
 
@@ -273,14 +264,15 @@ template <int RT, int CT, int P, int GD>
 __device__ __forceinline__ void fk_load_w(State<RT, CT, GD>& st, int c, int s) {
 #pragma unroll
   for (int j = 0; j < CT; ++j) {
+    // unconditional (no branch around vector-memory ops keeps the compiler's vmcnt waits counted):
+    // a column tile past NT reads beyond the buffer's range, which returns zeros
     const int ct = c * st.CTC + st.wave + 8 * j;
-    if (ct < st.NT) {
-      const int soff = __builtin_amdgcn_readfirstlane(kImgHdr + ((s * st.NT + ct) * 2) * 1024);
-      st.wb[P][j][0] = __builtin_bit_cast(
-          uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff, 0));
-      st.wb[P][j][1] = __builtin_bit_cast(
-          uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff + 1024, 0));
-    }
+    const int soff = __builtin_amdgcn_readfirstlane(ct < st.NT ? kImgHdr + ((s * st.NT + ct) * 2) * 1024
+                                                               : 0x7fff0000);
+    st.wb[P][j][0] = __builtin_bit_cast(
+        uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff, 0));
+    st.wb[P][j][1] = __builtin_bit_cast(
+        uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff + 1024, 0));
   }
 }
 
@@ -333,6 +325,16 @@ __device__ __forceinline__ void fk_resid_load(State<RT, CT, GD>& st, const Args&
     const int e = st.emap[(i % kEmaps) * St::ROWS + 16 * rt + st.fr].x;
     st.acc[rt][j] = H4[(int64_t)(e >= 0 ? e : 0) * st.hv + pc];
   }
+}
+
+// Bias of chunk c, column tile j: an unconditional load (no bias: S's first row, zeroed at use),
+// issued a whole chunk before the epilogue that uses it.
+template <int RT, int CT, int GD>
+__device__ __forceinline__ void fk_bias_load(State<RT, CT, GD>& st, const Args& a, int c, int j) {
+  const f32x4* b4 = reinterpret_cast<const f32x4*>(a.bias ? a.bias : a.S);
+  int pc = 4 * (c * st.CTC + st.wave + 8 * j) + st.g16;
+  pc = (pc < st.hv && a.bias) ? pc : 0;
+  st.bias[j] = b4[pc];
 }
 
 template <int RT, int CT, int GD>
@@ -426,12 +428,14 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD>& st, const Args& a,
   if (ct < st.NT) {
     const int pc = 4 * ct + st.g16;
     const bool pok = pc < st.hv;
-    const f32x4 bj = (x0.b4 && pok) ? x0.b4[pc] : f32x4{0.f, 0.f, 0.f, 0.f};
+    const f32x4 bj = (x0.b4 && pok) ? st.bias[J] : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 carry = f32x4{0.f, 0.f, 0.f, 0.f};
     float ccnt = 0.f;
     fk_epi_row<0, J, RT, CT, AACT, SUMONLY, MAXL, GD>(st, a, x0, pc, pok, bj, carry, ccnt);
   }
-  // column tile J is stored: its accumulators start the next (tile, chunk)
+  // column tile J is stored: its accumulators start the next (tile, chunk) (after the last tile the
+  // loads re-read this tile's rows and go unused)
+  if (c_next != c) fk_bias_load(st, a, c_next, J);  // column chunks: the next chunk's bias
   if (load_next) {
     fk_resid_load(st, a, i_next, c_next, J);
   } else {
@@ -461,6 +465,8 @@ __device__ __forceinline__ void fk_barrier() {
 
 template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL, int GD = 2>
 __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
+  // fused variants (MAXL > 1) read their rows from the row table, plain ones from src / rev
+  constexpr bool TABLE = MAXL > 1;
   using St = State<RT, CT, GD>;
   constexpr int ROWS = St::ROWS;
   constexpr int kEmapB = kEmaps * ROWS * 16;
@@ -479,6 +485,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
     ntl = (a.ntiles - t0 + tstride - 1) / tstride;
   }
   if (ntl <= 0) return;
+  auto tile = [&](int i) __attribute__((always_inline)) { return t0 + (i < ntl ? i : ntl - 1) * tstride; };
 
   St st;
   const int tid = threadIdx.x;
@@ -505,42 +512,38 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   st.sAW = st.sA * sW;
   st.inv = 1.f / st.sAW;  // exact: a power of two
   const bool resid = a.residual && a.H != nullptr;
-#pragma unroll
-  for (int r = 0; r < RT; ++r)
-#pragma unroll
-    for (int j = 0; j < CT; ++j) st.acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   const bool info_writer = st.g16 == 0 && (RT == 8 || st.wave < 4);
   const int SPT = a.nchunks * a.KS;  // steps per tile
   const int G = ntl * SPT;
 
-  // ---- tile info pipeline: cur (tile i), nxt (i + 1), prog (tile i + 2, built over three steps)
-  int cur_s, cur_q, nxt_s = -1, nxt_q = -1;
-  TileHead pth{0, 0};
-  RowIdx pri{-1, -1, 3};
-  int prs_s = -1, prs_q = -1;
-  int n_cur, n_nxt = 0;
+  // ---- tile info: cur (tile i) and nxt (i + 1) row offsets, raw row of tile i + 2 in flight
+  int2 cur, nxt;
+  int n_cur, n_nxt;
+  int4 raw2;
+  TileHead h2, h3;  // h3: bounds of tile i + 3, loaded a tile before its row is
   {
-    const TileHead h0 = tile_head<RT>(a, t0);
-    const RowIdx r0 = row_idx<RT>(a, h0, st.grow);
-    const RowSrc s0 = row_src(a, r0.e);
-    cur_s = s0.soff;
-    cur_q = s0.qoff;
-    if (info_writer) st.emap[0 * ROWS + st.grow] = int4{r0.e, r0.v, r0.flags, 0};
-    if (h0.n > ROWS && tid == 0) atomicOr(&g_pk_timeout, 2u);
-    n_cur = h0.n < ROWS ? h0.n : ROWS;
-    if (ntl > 1) {
-      const TileHead h1 = tile_head<RT>(a, t0 + tstride);
-      const RowIdx r1 = row_idx<RT>(a, h1, st.grow);
-      const RowSrc s1 = row_src(a, r1.e);
-      nxt_s = s1.soff;
-      nxt_q = s1.qoff;
-      if (info_writer) st.emap[1 * ROWS + st.grow] = int4{r1.e, r1.v, r1.flags, 0};
-      if (h1.n > ROWS && tid == 0) atomicOr(&g_pk_timeout, 2u);
-      n_nxt = h1.n < ROWS ? h1.n : ROWS;
+    const TileHead h0 = tile_head<RT, TABLE>(a, tile(0));
+    const int4 r0 = row_raw<RT, TABLE>(a, h0, st.grow);
+    const TileHead h1 = tile_head<RT, TABLE>(a, tile(1));
+    const int4 r1 = row_raw<RT, TABLE>(a, h1, st.grow);
+    h2 = tile_head<RT, TABLE>(a, tile(2));
+    raw2 = row_raw<RT, TABLE>(a, h2, st.grow);
+    h3 = tile_head<RT, TABLE>(a, tile(3));
+    const bool v0 = st.grow < h0.n, v1 = st.grow < h1.n;
+    cur = row_offsets(a, r0, v0);
+    nxt = row_offsets(a, r1, v1);
+    if (info_writer) {
+      st.emap[0 * ROWS + st.grow] = row_entry(r0, v0);
+      st.emap[1 * ROWS + st.grow] = row_entry(r1, v1);
     }
-    if (ntl > 2) pth = tile_head<RT>(a, t0 + 2 * tstride);
+    if ((h0.n > ROWS || (ntl > 1 && h1.n > ROWS)) && tid == 0) atomicOr(&g_pk_timeout, 2u);
+    n_cur = h0.n < ROWS ? h0.n : ROWS;
+    n_nxt = h1.n < ROWS ? h1.n : ROWS;
   }
+#pragma unroll
+  for (int r = 0; r < RT; ++r)
+#pragma unroll
+    for (int j = 0; j < CT; ++j) st.acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   // ---- prologue: steps 0 and 1 staged, W of step 0, slice 0 split into buffer 0
   __syncthreads();  // emap of tiles 0 and 1
@@ -548,85 +551,67 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
 #pragma unroll
     for (int j = 0; j < CT; ++j) fk_resid_load(st, a, 0, 0, j);
   }
-  fk_gather<RT, CT, ACT, 0>(st, a, cur_s, cur_q, 0);
-  if constexpr (GD == 2) {
-    if (G > 1) {
-      if (SPT > 1) fk_gather<RT, CT, ACT, 1>(st, a, cur_s, cur_q, 1 % a.KS);
-      else fk_gather<RT, CT, ACT, 1>(st, a, nxt_s, nxt_q, 0);
-    }
-  }
+#pragma unroll
+  for (int j = 0; j < CT; ++j) fk_bias_load(st, a, 0, j);
+  fk_gather<RT, CT, ACT, 0>(st, a, cur.x, cur.y, 0);
+  if constexpr (GD == 2) fk_gather<RT, CT, ACT, 1>(st, a, cur.x, cur.y, 1);  // SPT >= 2
   fk_load_w<RT, CT, 0>(st, 0, 0);
   fk_split<RT, CT, ACT, 0, 0>(st, a, 0);
   fk_barrier();
 
-  const int l2 = SPT > 1 ? 1 : 0, l3 = SPT > 2 ? 2 : l2;
+  // ---- main loop: one 32-deep k-step per iteration, two iterations per trip (register parity)
   int g = 0, i = 0, k = 0;  // global step, tile-local index, step within the tile
   while (g < G) {
 #pragma unroll
     for (int P = 0; P < 2; ++P) {
-      if (g < G) {
+      if (P == 0 || g < G) {
         const int c = k / a.KS, s = k - c * a.KS;
-        // (1) tile-info pipeline: rows of tile i + 2 (level 2 at step l2, level 3 at step l3)
-        if (i + 2 < ntl) {
-          if (k == l2) pri = row_idx<RT>(a, pth, st.grow);
-          if (k == l3) {
-            const RowSrc rs = row_src(a, pri.e);
-            prs_s = rs.soff;
-            prs_q = rs.qoff;
-          }
-        }
-        // (2) stage step g + GD (its register slot was split at step g - 1)
-        if (g + GD < G) {
+        // (1) stage step g + GD (its register slot was split at step g - 1); every vector-memory
+        // op of a step is unconditional, so the compiler's vmcnt waits count exactly
+        {
+          // the launcher keeps KS >= 2, so step g + GD lies in tile i or i + 1
           const int k2 = k + GD;
-          const int adv = k2 >= SPT ? (k2 >= 2 * SPT ? 2 : 1) : 0;
+          const int adv = k2 >= SPT ? 1 : 0;
           const int s2 = (k2 - adv * SPT) % a.KS;
-          const int so = adv == 0 ? cur_s : (adv == 1 ? nxt_s : prs_s);
-          const int qo = adv == 0 ? cur_q : (adv == 1 ? nxt_q : prs_q);
+          const int so = adv == 0 ? cur.x : nxt.x, qo = adv == 0 ? cur.y : nxt.y;
           if (GD == 1 || P == 0) fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s2);
           else fk_gather<RT, CT, ACT, GD - 1>(st, a, so, qo, s2);
         }
-        // (3) W fragments of step g + 1
+        // (2) W fragments of step g + 1
         const int k1 = k + 1 < SPT ? k + 1 : 0;
         const int c1 = k1 / a.KS, s1 = k1 - c1 * a.KS;
-        if (g + 1 < G) {
-          if (P == 0) fk_load_w<RT, CT, 1>(st, c1, s1);
-          else fk_load_w<RT, CT, 0>(st, c1, s1);
-        }
-        // (4) residual rows (loaded by the previous epilogue) into the accumulators' scale
+        if (P == 0) fk_load_w<RT, CT, 1>(st, c1, s1);
+        else fk_load_w<RT, CT, 0>(st, c1, s1);
+        // (3) residual rows (loaded by the previous epilogue) into the accumulators' scale
         if (resid && s == 0) fk_resid_scale(st);
-        // (5) MFMAs of step g
+        // (4) MFMAs of step g
         if (P == 0) fk_mfma<RT, CT, 0>(st, c, (n_cur + 15) >> 4);
         else fk_mfma<RT, CT, 1>(st, c, (n_cur + 15) >> 4);
-        // (6) split step g + 1's staged piece into the other buffer
-        if (g + 1 < G) {
-          if (P == 0) fk_split<RT, CT, ACT, GD - 1, 1>(st, a, s1);
-          else fk_split<RT, CT, ACT, 0, 0>(st, a, s1);
-        }
+        // (5) split step g + 1's staged piece into the other buffer
+        if (P == 0) fk_split<RT, CT, ACT, GD - 1, 1>(st, a, s1);
+        else fk_split<RT, CT, ACT, 0, 0>(st, a, s1);
         fk_barrier();
-        // (7) epilogue at the chunk's last k-step; it starts the next (tile, chunk)'s residual loads
+        // (6) epilogue at the chunk's last k-step; it starts the next (tile, chunk)'s residual loads
         if (s == a.KS - 1) {
           const bool last_c = c + 1 == a.nchunks;
-          const int i_next = last_c ? i + 1 : i, c_next = last_c ? 0 : c + 1;
-          fk_epilogue<RT, CT, AACT, SUMONLY, MAXL>(st, a, i, c, n_cur, resid && i_next < ntl, i_next, c_next);
+          const int i_next = last_c ? (i + 1 < ntl ? i + 1 : i) : i, c_next = last_c ? 0 : c + 1;
+          fk_epilogue<RT, CT, AACT, SUMONLY, MAXL>(st, a, i, c, n_cur, resid, i_next, c_next);
         }
-        // (8) advance
+        // (7) advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
         ++g;
         if (++k == SPT) {
           k = 0;
           ++i;
-          if (i < ntl) {
-            cur_s = nxt_s;
-            cur_q = nxt_q;
-            n_cur = n_nxt;
-            if (i + 1 < ntl) {  // tile i + 1 was built during tile i - 1: publish its rows
-              nxt_s = prs_s;
-              nxt_q = prs_q;
-              if (info_writer) st.emap[((i + 1) % kEmaps) * ROWS + st.grow] = int4{pri.e, pri.v, pri.flags, 0};
-              if (pth.n > ROWS && tid == 0) atomicOr(&g_pk_timeout, 2u);
-              n_nxt = pth.n < ROWS ? pth.n : ROWS;
-              if (i + 2 < ntl) pth = tile_head<RT>(a, t0 + (i + 2) * tstride);
-            }
-          }
+          cur = nxt;
+          n_cur = n_nxt;
+          const bool v2 = st.grow < h2.n;
+          nxt = row_offsets(a, raw2, v2);
+          if (info_writer) st.emap[((i + 1) % kEmaps) * ROWS + st.grow] = row_entry(raw2, v2);
+          if (h2.n > ROWS && i + 1 < ntl && tid == 0) atomicOr(&g_pk_timeout, 2u);
+          n_nxt = h2.n < ROWS ? h2.n : ROWS;
+          h2 = h3;
+          raw2 = row_raw<RT, TABLE>(a, h2, st.grow);
+          h3 = tile_head<RT, TABLE>(a, tile(i + 3));
         }
       }
     }
@@ -637,6 +622,24 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
       atomic_max_abs(a.amax_out, mh);
       if (a.SO) atomic_max_abs(a.amax_out + 1, ms);
     }
+  }
+}
+
+// Row table of a fused plan (one 16-B entry per dst-sorted position, so the layer kernel reaches a
+// tile's rows in one dependent load): {edge, src[edge] (-1 if out of range), rev[edge] (-1 if out of
+// range), (node << 2) | start | end << 1} with start / end = first / last in-edge of its node.
+__global__ void __launch_bounds__(256) row_table_kernel(const int32_t* __restrict__ perm,
+                                                        const int32_t* __restrict__ dsts,
+                                                        const int64_t* __restrict__ src,
+                                                        const int64_t* __restrict__ rev, int64_t V,
+                                                        int64_t E, int4* __restrict__ out) {
+  for (int64_t p = blockIdx.x * 256LL + threadIdx.x; p < E; p += (int64_t)gridDim.x * 256) {
+    const int e = perm[p];
+    const int64_t s = src[e], q = rev[e];
+    const int v = dsts[p];
+    const bool start = p == 0 || dsts[p - 1] != v, end = p + 1 == E || dsts[p + 1] != v;
+    out[p] = int4{e, (s >= 0 && s < V) ? (int)s : -1, (q >= 0 && q < E) ? (int)q : -1,
+                  (v << 2) | (start ? kFlagStart : 0) | (end ? kFlagEnd : 0)};
   }
 }
 

@@ -784,11 +784,10 @@ int fk_tile_rows(int64_t h, int act, int reduce, int aact, bool fused) {
 
 int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in, float* amax_out,
                      const int32_t* tile_ptr, int64_t ntiles, int tile_rows, int max_in_degree,
-                     const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
-                     float* S_out) {
+                     const void* row_table, int reduce, int aact, float aalpha, float* S_out) {
   const bool fused = tile_ptr != nullptr;
   NT_REQUIRE(fused == (S_out != nullptr), NT_EINVAL, "S_out must be given exactly with a tile plan");
-  NT_REQUIRE(!fused || (perm && dsts), NT_EINVAL, "fused mode needs perm and dst_sorted");
+  NT_REQUIRE(!fused || row_table, NT_EINVAL, "fp32 fused mode needs the row table (nt_dmpnn_row_table)");
   NT_REQUIRE(amax_in != nullptr, NT_EINVAL, "fp32 update needs amax_in (max|H|, max|S| on the device)");
   NT_REQUIRE(u.h % 4 == 0, NT_EUNSUPPORTED, "fp32 update needs h % 4 == 0");
   NT_REQUIRE((u.E * u.h) / 4 < (int64_t(1) << 31) && (u.V * u.h) / 4 < (int64_t(1) << 31),
@@ -811,14 +810,15 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   a.E = u.E;
   a.h = (int)u.h;
   a.hv = (int)(u.h / 4);
-  a.KS = fk::ks_for(u.h);
+  // at least two k-steps per tile (the kernel's staging runs two steps ahead within one tile's
+  // neighbour); a k-step past the image reads zeros (buffer range) and masked-off pieces
+  a.KS = fk::ks_for(u.h) < 2 ? 2 : fk::ks_for(u.h);
   a.NT = fk::nt_for(u.h);
   a.residual = u.residual;
   a.act = u.act;
   a.alpha = u.alpha;
   a.tile_ptr = tile_ptr;
-  a.perm = perm;
-  a.dsts = dsts;
+  a.rows = fused ? (const int4*)row_table : nullptr;
   a.reduce = reduce;
   a.aact = aact;
   a.aalpha = aalpha;
@@ -848,6 +848,14 @@ int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_
   const int64_t slots = (int64_t)KS * NT * 2 * 64;
   dim3 grid((unsigned)((slots + 255) / 256), (unsigned)nlayers);
   fk::pack_fk_kernel<<<grid, 256, 0, stream>>>(W, h, KS, NT, w_stride, img_stride, (char*)img);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+int fk_row_table(const int32_t* perm, const int32_t* dsts, const int64_t* src, const int64_t* rev, int64_t V,
+                 int64_t E, void* out, hipStream_t stream) {
+  if (E <= 0) return NT_OK;
+  fk::row_table_kernel<<<grid_for(E, 256, 256 * 16), 256, 0, stream>>>(perm, dsts, src, rev, V, E, (int4*)out);
   NT_LAUNCH_CHECK();
   return NT_OK;
 }

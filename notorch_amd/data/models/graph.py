@@ -65,6 +65,8 @@ class DeviceLayout:
     plan_wide: object = None
     # backward CSRs (src -> nodes, rev_index -> edges), built lazily by _engine.backward_layout
     bwd: object = None
+    # the fp32 layer kernel's row table (key, rev_index, E x 4 int32), built lazily by _engine.row_table
+    row_table: object = None
     # host-computed statistics the collate ships with the CSR, so a fresh batch needs no
     # device -> host sync: (max, min) in-degree, largest molecule, (min, max) type index of the
     # node / edge feature columns when they are integer type matrices

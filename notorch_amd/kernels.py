@@ -24,6 +24,7 @@ __all__ = [
     "tile_stride",
     "fused_tile_rows",
     "absmax",
+    "dmpnn_row_table",
     "fused_supported",
     "dmpnn_update_fused",
     "act_code",
@@ -400,9 +401,10 @@ def tile_stride(E: int, max_in_degree: int, rows: int, ncu: int = PLAN_NCU) -> i
 
 
 def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int, rows: int = 64,
-              ncu: int = PLAN_NCU) -> tuple[Tensor, int, Tensor]:
+              ncu: int = 0) -> tuple[Tensor, int, Tensor]:
     """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) for nt_dmpnn_update_fused: node-aligned tiles of
-    at most `rows` rows (max_in_degree <= 32), balanced to whole rounds of ncu tiles."""
+    at most `rows` rows (max_in_degree <= 32), balanced to whole rounds of ncu tiles (ncu = 0: the
+    largest tiles; the engine's 128-row plans use PLAN_NCU)."""
     dev = _require_device(dst_ptr)
     if dst_ptr.dtype != torch.int32:
         raise TypeError("dst_ptr must be int32")
@@ -438,6 +440,7 @@ def dmpnn_update_fused(
     zero_fill: bool = False,
     amax_in: Tensor | None = None,
     amax_out: Tensor | None = None,
+    row_table: Tensor | None = None,
     out: Tensor | None = None,
     S_out: Tensor | None = None,
 ) -> tuple[Tensor, Tensor | None]:
@@ -446,6 +449,8 @@ def dmpnn_update_fused(
 
     fp32: ``amax_in`` = (max|H|, max|S|) on the device (computed here with nt_absmax when not given);
     ``amax_out`` (2 zero-filled floats) receives max|H_out|, max|S_out| for the next layer.
+    ``row_table`` (fp32 with a plan): nt_dmpnn_row_table of (perm, dst_sorted, src, rev), built here
+    when not given (cache it per graph).
     ``zero_fill`` must be True when some node has no in-edge (its S_out row is then 0)."""
     dev = _require_device(H, S, src, rev, Wp, bias, out, S_out, perm, amax_in, amax_out)
     code = _require_feat("H", H)
@@ -479,6 +484,8 @@ def dmpnn_update_fused(
     else:
         perm = None
         S_out = None
+    if H.dtype == torch.float32 and plan is not None and row_table is None and E > 0:
+        row_table = dmpnn_row_table(perm, dsts, src, rev, V)
     if H.dtype == torch.float32 and amax_in is None and E > 0:
         amax_in = torch.zeros(2, dtype=torch.float32, device=dev)
         absmax(H.contiguous(), amax_in[0:1])
@@ -487,9 +494,22 @@ def dmpnn_update_fused(
     _run(dev, lib.nt_dmpnn_update_fused,
          _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
          act[0], act[1], _ptr(tile_ptr), ntiles, int(tile_rows), int(max_in_degree), _ptr(perm), _ptr(dsts),
-         reduce_code(reduce), agg_act[0], agg_act[1], code, _ptr(amax_in), _ptr(amax_out), _ptr(out),
-         _ptr(S_out), _stream(dev))
+         _ptr(row_table), reduce_code(reduce), agg_act[0], agg_act[1], code, _ptr(amax_in), _ptr(amax_out),
+         _ptr(out), _ptr(S_out), _stream(dev))
     return out, S_out
+
+
+def dmpnn_row_table(perm: Tensor, dst_sorted: Tensor, src: Tensor, rev: Tensor, V: int) -> Tensor:
+    """E x 4 int32: {edge, src, rev, (node << 2) | start | end << 1} per dst-sorted position (the fp32
+    layer kernel's one-load view of a fused plan's rows)."""
+    dev = _require_device(perm, dst_sorted, src, rev)
+    _require_i64("src", src)
+    _require_i64("rev_index", rev)
+    E = perm.numel()
+    out = torch.empty(max(E, 1), 4, dtype=torch.int32, device=dev)[:E]
+    _run(dev, _lib.load().nt_dmpnn_row_table, _ptr(perm), _ptr(dst_sorted), _ptr(src), _ptr(rev), V, E, _ptr(out),
+         _stream(dev))
+    return out
 
 
 def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None, *, kernel: str = "fk") -> Tensor:

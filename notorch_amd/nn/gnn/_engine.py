@@ -181,7 +181,7 @@ def fused_plan(lay: DeviceLayout, V: int, E: int, rows: int = 64):
     if rows <= 64:
         return lay.plan
     if lay.plan_wide is None:  # node-aligned tiles of <= 128 rows, balanced over the CUs
-        tile_ptr, ntiles, _ = K.tile_plan(lay.dst_ptr, E, _degree_range(lay)[0], rows=128)
+        tile_ptr, ntiles, _ = K.tile_plan(lay.dst_ptr, E, _degree_range(lay)[0], rows=128, ncu=K.PLAN_NCU)
         lay.plan_wide = (tile_ptr, ntiles)
     return lay.plan_wide[0], lay.plan_wide[1], lay.plan[2], lay.plan[3]
 
@@ -385,9 +385,21 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
     return node, H, states
 
 
+def row_table(lay: DeviceLayout, dsts: Tensor, src: Tensor, rev: Tensor, V: int) -> Tensor:
+    """The fp32 layer kernel's row table of this graph (nt_dmpnn_row_table), cached on the layout
+    (keyed on the src storage and the rev_index tensor, like backward_layout)."""
+    key = (src.data_ptr(), src.numel(), rev.data_ptr(), rev.numel(), V)
+    hit = getattr(lay, "row_table", None)
+    if hit is None or hit[0] != key or hit[1] is not rev:
+        hit = (key, rev, K.dmpnn_row_table(lay.dst_perm, dsts, src, rev, V))
+        lay.row_table = hit
+    return hit[2]
+
+
 def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, residual, keep_states, amax):
     tile_ptr, ntiles, dsts, zero_fill = plan
     d = len(Wps)
+    rt = row_table(lay, dsts, src, rev, S.shape[0]) if H.dtype == torch.float32 else None
     states = []
     spare_H: Optional[Tensor] = None
     spare_S: Optional[Tensor] = None
@@ -406,7 +418,7 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
             residual=residual, act=act, plan=(tile_ptr, ntiles, dsts), tile_rows=rows, max_in_degree=maxdeg,
             perm=lay.dst_perm, reduce=reduce, agg_act=_IDENTITY if last else act, zero_fill=zero_fill,
             amax_in=None if amax is None else amax[l], amax_out=None if amax is None else amax[l + 1],
-            out=spare_H, S_out=None if last else spare_S,
+            row_table=rt, out=spare_H, S_out=None if last else spare_S,
         )
         if timer is not None:
             ev[1].record()

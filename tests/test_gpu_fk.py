@@ -32,7 +32,7 @@ def _layout(G, rows):
     dst_ptr, perm = K.csr_build(G.edge_index[1].contiguous().to(DEV), G.num_nodes)
     deg = (dst_ptr[1:] - dst_ptr[:-1]).cpu()
     maxdeg = int(deg.max())
-    plan = K.tile_plan(dst_ptr, G.num_edges, maxdeg, rows=rows)
+    plan = K.tile_plan(dst_ptr, G.num_edges, maxdeg, rows=rows, ncu=K.PLAN_NCU if rows == 128 else 0)
     return perm, plan, maxdeg, bool((deg == 0).any())
 
 
@@ -202,7 +202,7 @@ def test_engine_uses_wide_plan_and_amax_chain():
     h = 300
     G = _graph("qm9", 512, seed=4)
     lay = G._nt_layout
-    d_tp, d_n, _ = K.tile_plan(lay.dst_ptr.to(DEV), G.num_edges, lay.deg_range[0], rows=128)
+    d_tp, d_n, _ = K.tile_plan(lay.dst_ptr.to(DEV), G.num_edges, lay.deg_range[0], rows=128, ncu=K.PLAN_NCU)
     assert d_n == lay.plan_wide[1] and torch.equal(d_tp.cpu(), lay.plan_wide[0])
     torch.manual_seed(0)
     Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
