@@ -79,6 +79,7 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-embedded", action="store_true", help="skip embedded / fresh / end-to-end legs")
     p.add_argument("--no-secondary", action="store_true", help="skip the config-3 / config-5 keys")
+    p.add_argument("--no-training", action="store_true", help="skip the training key (N=1 only)")
     p.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                    help="process group for the bench bookkeeping (nccl = RCCL; gloo only to rehearse "
                    "the N>1 path with --same-device on a one-GPU box)")
@@ -498,6 +499,38 @@ def pipeline_leg(res, dev, workers, n_batches=24, warm=4):
             "value": job.E * job.depth / t, "unit": "edge-messages/s"}
 
 
+def training_leg(args, timeout_s=300):
+    """Config-2 training step (ChempropBlock + Sum, forward + backward, kernel backward) with each
+    weight-grad path, each in a fresh child process (tools/train_bench.py --json: 10 warm-ups, median
+    of 30 event-timed steps)."""
+    import subprocess
+
+    script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "train_bench.py")
+    out = {"step": "config 2 batch (4096 qm9-shaped molecules, seed 1000), ChempropBlock depth=3 h=300 + Sum, "
+                   "forward + backward of sum(readout^2) w.r.t. weights and input features, fp32; "
+                   "one fresh process per weight-grad path; median of 30 after 10 warm-ups",
+           "unit": "edge-messages/s"}
+    for wgrad in ("kernel", "library"):
+        env = dict(os.environ, NT_WGRAD=wgrad)
+        try:
+            r = subprocess.run([sys.executable, script, "--json", "--modes", "kernel", "--steps", "30",
+                                "--warmup", "10"], env=env, capture_output=True, text=True, timeout=timeout_s)
+        except subprocess.TimeoutExpired:
+            out[wgrad] = {"error": f"timed out after {timeout_s} s"}
+            continue
+        if r.returncode != 0:
+            out[wgrad] = {"error": f"exit {r.returncode}: {r.stderr.strip().splitlines()[-1:]}"}
+            continue
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        out[wgrad] = {"train_ms": d["ms"]["train[kernel]"], "forward_ms": d["ms"]["fwd"],
+                      "value": d["edge_messages_per_s"]["train[kernel]"]}
+    ok = [k for k in ("kernel", "library") if "train_ms" in out.get(k, {})]
+    if ok:
+        best = min(ok, key=lambda k: out[k]["train_ms"])
+        out.update(weight_grad=best, train_ms=out[best]["train_ms"], value=out[best]["value"])
+    return out
+
+
 def summary(res, args, env, pmc_csv=None):
     jobs = res["jobs"]
     info = res["info"]
@@ -592,6 +625,10 @@ def main():
             }
             del r2
 
+    training = None
+    if not args.no_training and env.world_size == 1 and args.workload == "qm9-4096":
+        training = training_leg(args)
+
     cpu = None
     if not args.no_cpu_baseline and env.rank == 0:
         cpu = cpu_baseline(job, res["embedding"], args.cpu_seconds)
@@ -632,6 +669,7 @@ def main():
             "fresh_batch": fresh,
             "embedded_encoder": embedded,
             "end_to_end": e2e,
+            "training": training,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -114,6 +114,14 @@ struct Reducer4 {
   }
 };
 
+// *p = max(*p, v) for non-negative floats (they order like their bit patterns).  The relaxed read
+// first skips the atomic when it cannot raise the value, so the thousands of waves of a launch do not
+// serialise on one L2 line (a stale read only costs an unneeded atomic: *p never decreases).
+__device__ __forceinline__ void atomic_max_nonneg(float* p, float v) {
+  if (!(v <= __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)))
+    atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
+}
+
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 inline int grid_for(int64_t work, int block, int cap = 256 * 16) {

@@ -223,8 +223,8 @@ __global__ void __launch_bounds__(LDS ? kLdsThreads : 256, LDS ? 2 : 1) init_emb
       ms = fmaxf(ms, __shfl_xor(ms, o));
     }
     if ((threadIdx.x & 63) == 0) {
-      atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(mh));
-      atomicMax(reinterpret_cast<unsigned int*>(amax + 1), __float_as_uint(ms));
+      atomic_max_nonneg(amax, mh);
+      atomic_max_nonneg(amax + 1, ms);
     }
   }
 }

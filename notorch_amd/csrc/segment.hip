@@ -139,8 +139,8 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
       ms = fmaxf(ms, __shfl_xor(ms, o));
     }
     if (lane == 0) {
-      atomicMax(reinterpret_cast<unsigned int*>(amax), __float_as_uint(mh));
-      atomicMax(reinterpret_cast<unsigned int*>(amax + 1), __float_as_uint(ms));
+      atomic_max_nonneg(amax, mh);
+      atomic_max_nonneg(amax + 1, ms);
     }
   }
 }

@@ -39,7 +39,7 @@ constexpr int kWaves = 4;
 
 // kernel selection for A/B runs (read per call):
 //   NT_UPDATE_KERNEL = as (default: A-stationary bf16x6) | x6 (LDS-ring bf16x6)
-//                      | ring | stream | tile (exact fp32 MFMA)
+//                      | stream | tile (exact fp32 MFMA)
 static char update_kernel_choice() {
 #ifdef NT_DIAG
   const char* v = getenv("NT_UPDATE_KERNEL");
@@ -634,13 +634,6 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                  stream};
     return launch_update_x6(a);
   }
-#ifdef NT_DIAG
-  if (vec && choice == 'r' && g.NT <= 24) {
-    UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
-                 g.KB, g.NT, residual, act, act_alpha, (float*)H_out, stream};
-    return launch_update_ring(a);
-  }
-#endif
   // 64-edge tiles while two workgroups still fit one CU's LDS (h <= 304), else 32-edge tiles.
   if (lds_bytes<64>(g) <= 80 * 1024)
     return dispatch_cpw<64>((const float*)H, (const float*)S, src, rev, (const float4*)Wp,

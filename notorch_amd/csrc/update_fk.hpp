@@ -102,7 +102,7 @@ __device__ __forceinline__ float act_bound(float m, int act, float alpha) {
 
 __device__ __forceinline__ void atomic_max_abs(float* p, float v) {
   // non-negative floats order like their bit patterns
-  atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
+  atomic_max_nonneg(p, v);
 }
 
 __device__ __forceinline__ float wave_max(float v) {
@@ -360,7 +360,7 @@ struct EpiCtx {
   int n;
 };
 
-template <int RTI, int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD>
+template <int RTI, int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL>
 __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD>& st, const Args& a, const EpiCtx& x0, int pc,
                                            bool pok, const f32x4& bj, f32x4& carry, float& ccnt) {
   if (16 * RTI < x0.n) {
@@ -370,7 +370,7 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD>& st, const Args& a,
 #pragma unroll
     for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[RTI][J][q], st.inv, bj[q]);
     const bool rok = ri.x >= 0 && pok;
-    if (rok) {
+    if (rok && (ABL & 64) == 0) {
       x0.O4[(int64_t)ri.x * hv + pc] = o;
       st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
     }
@@ -407,7 +407,7 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD>& st, const Args& a,
           cnt = start ? 1.f : yc + 1.f;
         }
       }
-      if ((ri.z & kFlagEnd) && rok) {
+      if ((ri.z & kFlagEnd) && rok && (ABL & 128) == 0) {
         f32x4 r = x;
         if (!SUMONLY && a.reduce == NT_MEAN) r = x / cnt;
         x0.SO4[(int64_t)ri.y * hv + pc] = r;
@@ -418,10 +418,10 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD>& st, const Args& a,
     }
   }
   if constexpr (RTI + 1 < RT)
-    fk_epi_row<RTI + 1, J, RT, CT, AACT, SUMONLY, MAXL, GD>(st, a, x0, pc, pok, bj, carry, ccnt);
+    fk_epi_row<RTI + 1, J, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, pc, pok, bj, carry, ccnt);
 }
 
-template <int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD>
+template <int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL>
 __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD>& st, const Args& a, const EpiCtx& x0, int i, int c,
                                            bool load_next, int i_next, int c_next) {
   const int ct = c * st.CTC + st.wave + 8 * J;
@@ -431,7 +431,7 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD>& st, const Args& a,
     const f32x4 bj = (x0.b4 && pok) ? st.bias[J] : f32x4{0.f, 0.f, 0.f, 0.f};
     f32x4 carry = f32x4{0.f, 0.f, 0.f, 0.f};
     float ccnt = 0.f;
-    fk_epi_row<0, J, RT, CT, AACT, SUMONLY, MAXL, GD>(st, a, x0, pc, pok, bj, carry, ccnt);
+    fk_epi_row<0, J, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, pc, pok, bj, carry, ccnt);
   }
   // column tile J is stored: its accumulators start the next (tile, chunk) (after the last tile the
   // loads re-read this tile's rows and go unused)
@@ -443,10 +443,10 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD>& st, const Args& a,
     for (int rt = 0; rt < RT; ++rt) st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
   if constexpr (J + 1 < CT)
-    fk_epi_col<J + 1, RT, CT, AACT, SUMONLY, MAXL, GD>(st, a, x0, i, c, load_next, i_next, c_next);
+    fk_epi_col<J + 1, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, i, c, load_next, i_next, c_next);
 }
 
-template <int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD>
+template <int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL>
 __device__ __forceinline__ void fk_epilogue(State<RT, CT, GD>& st, const Args& a, int i, int c, int n,
                                             bool load_next, int i_next, int c_next) {
   EpiCtx x0;
@@ -455,7 +455,7 @@ __device__ __forceinline__ void fk_epilogue(State<RT, CT, GD>& st, const Args& a
   x0.SO4 = reinterpret_cast<f32x4*>(a.SO);
   x0.em = st.emap + (i % kEmaps) * State<RT, CT, GD>::ROWS;
   x0.n = n;
-  fk_epi_col<0, RT, CT, AACT, SUMONLY, MAXL, GD>(st, a, x0, i, c, load_next, i_next, c_next);
+  fk_epi_col<0, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, i, c, load_next, i_next, c_next);
 }
 
 __device__ __forceinline__ void fk_barrier() {
@@ -463,7 +463,10 @@ __device__ __forceinline__ void fk_barrier() {
   __syncthreads();
 }
 
-template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL, int GD = 2>
+// ABL (diagnostic builds only, 0 in the shipping library): timing ablations, results invalid --
+// 1 gathers read row 0, 2 no MFMA, 4 no split, 8 no epilogue, 16 no per-step barrier, 32 no residual,
+// 64 no H_out stores, 128 no S_out stores.
+template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL, int GD = 2, int ABL = 0>
 __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   // fused variants (MAXL > 1) read their rows from the row table, plain ones from src / rev
   constexpr bool TABLE = MAXL > 1;
@@ -511,7 +514,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   const float sW = *reinterpret_cast<const float*>(a.Wimg);
   st.sAW = st.sA * sW;
   st.inv = 1.f / st.sAW;  // exact: a power of two
-  const bool resid = a.residual && a.H != nullptr;
+  const bool resid = (ABL & 32) == 0 && a.residual && a.H != nullptr;
   const bool info_writer = st.g16 == 0 && (RT == 8 || st.wave < 4);
   const int SPT = a.nchunks * a.KS;  // steps per tile
   const int G = ntl * SPT;
@@ -566,36 +569,43 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
     for (int P = 0; P < 2; ++P) {
       if (P == 0 || g < G) {
         const int c = k / a.KS, s = k - c * a.KS;
-        // (1) stage step g + GD (its register slot was split at step g - 1); every vector-memory
+        // (1) W fragments of step g + 1, issued before this step's gathers: the MFMAs of step g wait
+        // (in-order vmcnt) for W(g) only, i.e. for loads issued up to the gathers of step g, and
+        // overlap the flight of step g + 1's gathers
+        const int k1 = k + 1 < SPT ? k + 1 : 0;
+        const int c1 = k1 / a.KS, s1 = k1 - c1 * a.KS;
+        if (P == 0) fk_load_w<RT, CT, 1>(st, c1, s1);
+        else fk_load_w<RT, CT, 0>(st, c1, s1);
+        // (2) stage step g + GD (its register slot was split at step g - 1); every vector-memory
         // op of a step is unconditional, so the compiler's vmcnt waits count exactly
         {
           // the launcher keeps KS >= 2, so step g + GD lies in tile i or i + 1
           const int k2 = k + GD;
           const int adv = k2 >= SPT ? 1 : 0;
           const int s2 = (k2 - adv * SPT) % a.KS;
-          const int so = adv == 0 ? cur.x : nxt.x, qo = adv == 0 ? cur.y : nxt.y;
+          int so = adv == 0 ? cur.x : nxt.x, qo = adv == 0 ? cur.y : nxt.y;
+          if constexpr ((ABL & 1) != 0) so = qo = 0;
           if (GD == 1 || P == 0) fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s2);
           else fk_gather<RT, CT, ACT, GD - 1>(st, a, so, qo, s2);
         }
-        // (2) W fragments of step g + 1
-        const int k1 = k + 1 < SPT ? k + 1 : 0;
-        const int c1 = k1 / a.KS, s1 = k1 - c1 * a.KS;
-        if (P == 0) fk_load_w<RT, CT, 1>(st, c1, s1);
-        else fk_load_w<RT, CT, 0>(st, c1, s1);
         // (3) residual rows (loaded by the previous epilogue) into the accumulators' scale
         if (resid && s == 0) fk_resid_scale(st);
         // (4) MFMAs of step g
-        if (P == 0) fk_mfma<RT, CT, 0>(st, c, (n_cur + 15) >> 4);
-        else fk_mfma<RT, CT, 1>(st, c, (n_cur + 15) >> 4);
+        if constexpr ((ABL & 2) == 0) {
+          if (P == 0) fk_mfma<RT, CT, 0>(st, c, (n_cur + 15) >> 4);
+          else fk_mfma<RT, CT, 1>(st, c, (n_cur + 15) >> 4);
+        }
         // (5) split step g + 1's staged piece into the other buffer
-        if (P == 0) fk_split<RT, CT, ACT, GD - 1, 1>(st, a, s1);
-        else fk_split<RT, CT, ACT, 0, 0>(st, a, s1);
-        fk_barrier();
+        if constexpr ((ABL & 4) == 0) {
+          if (P == 0) fk_split<RT, CT, ACT, GD - 1, 1>(st, a, s1);
+          else fk_split<RT, CT, ACT, 0, 0>(st, a, s1);
+        }
+        if constexpr ((ABL & 16) == 0) fk_barrier();
         // (6) epilogue at the chunk's last k-step; it starts the next (tile, chunk)'s residual loads
-        if (s == a.KS - 1) {
+        if ((ABL & 8) == 0 && s == a.KS - 1) {
           const bool last_c = c + 1 == a.nchunks;
           const int i_next = last_c ? (i + 1 < ntl ? i + 1 : i) : i, c_next = last_c ? 0 : c + 1;
-          fk_epilogue<RT, CT, AACT, SUMONLY, MAXL>(st, a, i, c, n_cur, resid, i_next, c_next);
+          fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
         }
         // (7) advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
         ++g;

@@ -42,6 +42,7 @@ __device__ unsigned long long g_pk_stamps[10];
 // the fp16x3 layer kernel (shares g_pk_timeout: bit 1 = bounded wait gave up, bit 2 = a tile larger
 // than the fk kernel's row capacity)
 #include "update_fk.hpp"
+#include "update_fk2.hpp"
 
 namespace nt {
 
@@ -752,6 +753,63 @@ int launch_fk_wide(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
                    : launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 16>(a, grid, stream);
 }
 
+// fk2 (64-row tiles, output staged in LDS and written during the next tile): h <= 384, any layer
+template <int ACT, int AACT, bool SUMONLY, bool TABLE>
+int launch_fk2_t(const fk::Args& a, int grid, hipStream_t stream) {
+  fk::update_fk2_kernel<3, ACT, AACT, SUMONLY, TABLE><<<grid, fk::kThreads, 0, stream>>>(a);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+int launch_fk2(const fk::Args& a, int grid, hipStream_t stream) {
+  const bool relu = a.act == NT_ACT_RELU, ident = a.act == NT_ACT_IDENTITY;
+  if (a.SO == nullptr) {  // plain / dense: no aggregation
+    if (relu) return launch_fk2_t<NT_ACT_RELU, NT_ACT_IDENTITY, true, false>(a, grid, stream);
+    if (ident) return launch_fk2_t<NT_ACT_IDENTITY, NT_ACT_IDENTITY, true, false>(a, grid, stream);
+    return launch_fk2_t<-1, NT_ACT_IDENTITY, true, false>(a, grid, stream);
+  }
+  const bool sum = a.reduce == NT_SUM;
+#ifdef NT_DIAG
+  if (relu && sum && a.aact == NT_ACT_RELU) {
+    const char* e = getenv("NT_FK_ABL");
+    switch (e ? atoi(e) : 0) {
+#define NT_FK2_ABL_CASE(n)                                                                                  \
+  case n:                                                                                                   \
+    fk::update_fk2_kernel<3, NT_ACT_RELU, NT_ACT_RELU, true, true, 2, n><<<grid, fk::kThreads, 0, stream>>>(a); \
+    NT_LAUNCH_CHECK();                                                                                      \
+    return NT_OK;
+      NT_FK2_ABL_CASE(1)
+      NT_FK2_ABL_CASE(2)
+      NT_FK2_ABL_CASE(6)
+      NT_FK2_ABL_CASE(8)
+      NT_FK2_ABL_CASE(16)
+      NT_FK2_ABL_CASE(32)
+      NT_FK2_ABL_CASE(64)
+      NT_FK2_ABL_CASE(70)
+      NT_FK2_ABL_CASE(102)
+      NT_FK2_ABL_CASE(71)
+      NT_FK2_ABL_CASE(24)
+#undef NT_FK2_ABL_CASE
+      default:
+        break;
+    }
+  }
+#endif
+  if (relu && sum && a.aact == NT_ACT_RELU) return launch_fk2_t<NT_ACT_RELU, NT_ACT_RELU, true, true>(a, grid, stream);
+  if (relu && sum && a.aact == NT_ACT_IDENTITY)
+    return launch_fk2_t<NT_ACT_RELU, NT_ACT_IDENTITY, true, true>(a, grid, stream);
+  return launch_fk2_t<-1, -1, false, true>(a, grid, stream);
+}
+
+// which fp32 layer kernel runs: fk2 for h <= 384 (diagnostic builds: NT_FK=1 selects update_fk_kernel)
+bool fk2_selected(int64_t h) {
+#ifdef NT_DIAG
+  const char* e = getenv("NT_FK");
+  if (e && e[0] == '1') return false;
+#endif
+  return h <= fk::kFk2MaxH;
+}
+
 // 64-row tiles: every other combination (any reduce, any aggregation act) and h > 384
 template <int CT>
 int launch_fk_narrow(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
@@ -777,6 +835,7 @@ int launch_fk_narrow(const fk::Args& a, int maxl, int grid, hipStream_t stream) 
 // whose act is relu / identity, or with no aggregation (fused < 0); else 64.  (The other variants
 // need more registers than two waves per SIMD hold at 128 rows.)
 int fk_tile_rows(int64_t h, int act, int reduce, int aact, bool fused) {
+  if (fk2_selected(h)) return 64;
   const bool wide_ok =
       !fused || (act == NT_ACT_RELU && reduce == NT_SUM && (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY));
   return (fk::nt_for(h) <= 24 && wide_ok) ? 128 : 64;
@@ -829,6 +888,10 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   if (a.ntiles == 0) return NT_OK;
   const int grid = a.ntiles < cu_count() ? a.ntiles : cu_count();
   const int maxl = max_in_degree - 1;  // scan rounds needed within a 16-row tile
+  if (fk2_selected(u.h)) {
+    a.nchunks = 1;
+    return launch_fk2(a, grid, u.stream);
+  }
   // up to 3 column tiles per wave (NT <= 24, one chunk); waves past NT skip theirs at run time
   if (cap == 128) {
     a.nchunks = 1;

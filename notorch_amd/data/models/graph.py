@@ -521,7 +521,7 @@ CHUNK_ROWS = 32  # rows per chunk of nt_segment_reduce_chunked
 
 
 PLAN_NCU = 256  # kernels.PLAN_NCU: the CU count the balanced plans are cut for
-WIDE_TILE_ROWS = 128  # rows of the fp32 layer kernel's tiles (nt_dmpnn_fused_tile_rows, h <= 384)
+WIDE_TILE_ROWS = 128  # rows of the diagnostic build's update_fk_kernel tiles (the shipping kernels: 64)
 
 
 def host_tile_stride(E: int, max_in_degree: int, rows: int, ncu: int) -> int:
@@ -582,7 +582,7 @@ def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional
     V = len(deg)
     maxdeg, mindeg = lay.deg_range
     if E > 0 and V > 0 and maxdeg <= MAX_FUSED_IN_DEGREE:
-        tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg)
+        tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg, rows=64, ncu=PLAN_NCU)
         lay.plan = (tile_ptr, ntiles, dsts, mindeg == 0)
         lay.plan_wide = host_tile_ptr(dst_ptr, E, host_tile_stride(E, maxdeg, WIDE_TILE_ROWS, PLAN_NCU))
     elif E > 0 and V > 0:

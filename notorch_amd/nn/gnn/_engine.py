@@ -57,20 +57,24 @@ UPDATE_EVENTS: Optional[list] = None
 LAST_UPDATE_INFO: dict = {}
 
 
+FK2_MAX_H = 384  # update_fk2_kernel's hidden-size limit (larger sizes: column-chunked update_fk_kernel)
+
+
 def _note_update(kind: str, dtype: torch.dtype, h: int) -> None:
     kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
     if dtype == torch.bfloat16:
         info = dict(kernel="update_bf16_kernel (64-edge tiles, bf16 16x16x32 MFMA, fp32 accumulate)",
                     kernel_short="update_bf16", numerics="bf16 storage, bf16 MFMA, fp32 accumulate",
                     products=1)
-    elif kind == "fused":
-        info = dict(kernel="update_fk_kernel (persistent, 128-row node-aligned tiles, two-part fp16 split on "
-                           "16x16x32 fp16 MFMA, aggregation of the next layer fused)", kernel_short="update_fk",
-                    numerics="fp32 via scaled two-part fp16 split (3 fp16 MFMA products, fp32 accumulate)",
-                    products=3)
-    elif kind == "persistent":
-        info = dict(kernel="update_fk_kernel without tile plan (hub graph: aggregation by the chunked "
-                           "segment reduce)", kernel_short="update_fk",
+    elif kind in ("fused", "persistent"):
+        fk2 = h <= FK2_MAX_H
+        name = "update_fk2_kernel" if fk2 else "update_fk_kernel"
+        shape = ("64-row node-aligned tiles, output staged in LDS and stored during the next tile's K loop"
+                 if fk2 else "64-row node-aligned tiles, column-chunked (h > 384)")
+        tail = ("aggregation of the next layer fused" if kind == "fused"
+                else "no tile plan: hub graph, aggregation by the chunked segment reduce")
+        info = dict(kernel=f"{name} (persistent, {shape}, two-part fp16 split on 16x16x32 fp16 MFMA, {tail})",
+                    kernel_short=name[:-len("_kernel")],
                     numerics="fp32 via scaled two-part fp16 split (3 fp16 MFMA products, fp32 accumulate)",
                     products=3)
     else:
@@ -165,7 +169,8 @@ def _degree_range(lay: DeviceLayout) -> tuple[int, int]:
 
 
 def fused_plan(lay: DeviceLayout, V: int, E: int, rows: int = 64):
-    """Tile plan of the fused update for this layout with tiles of at most ``rows`` (64 or 128) rows,
+    """Tile plan of the fused update for this layout with tiles of at most ``rows`` (64, or 128 for the
+    diagnostic build's update_fk_kernel) rows, balanced to whole rounds over PLAN_NCU CUs,
     as (tile_ptr, ntiles, dst_sorted, zero_fill), cached on it; None when some node has more than 32
     in-edges (polymer hubs): those graphs take the unfused path.  One sync per layout."""
     if lay.plan is None:
@@ -173,7 +178,7 @@ def fused_plan(lay: DeviceLayout, V: int, E: int, rows: int = 64):
         if E > 0 and V > 0:
             maxdeg, mindeg = _degree_range(lay)
             if maxdeg <= 32:
-                tile_ptr, ntiles, dsts = K.tile_plan(lay.dst_ptr, E, maxdeg, rows=64, ncu=0)
+                tile_ptr, ntiles, dsts = K.tile_plan(lay.dst_ptr, E, maxdeg, rows=64, ncu=K.PLAN_NCU)
                 plan = (tile_ptr, ntiles, dsts, mindeg == 0)
         lay.plan = plan
     if not lay.plan:

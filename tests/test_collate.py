@@ -176,20 +176,21 @@ def test_host_tile_stride_matches_library():
                 assert host_tile_stride(E, maxdeg, rows, ncu) == lib.nt_dmpnn_tile_stride(E, maxdeg, rows, ncu)
 
 
-def test_collate_ships_balanced_wide_plan():
-    """The collate's 128-row plan: node-aligned tiles of <= 128 rows, cut to whole rounds of 256 tiles
-    (config 2: about 3 tiles per CU), next to the 64-row plan of the bf16 kernel."""
+def test_collate_ships_balanced_plans():
+    """The collate's plans: the 64-row plan of the shipping kernels (update_fk2 / bf16) and the 128-row
+    plan of the diagnostic update_fk_kernel, node-aligned, cut to whole rounds of 256 tiles (config 2:
+    about 5 and 3 tiles per CU)."""
     import numpy as np
 
     from notorch_amd.data.synth import make_batch
 
     G = make_batch("qm9", 4096, seed=1000).collate("nodes")
     lay = G._nt_layout
-    tile_ptr, ntiles = lay.plan_wide
-    tp = tile_ptr.numpy().astype(np.int64)
-    sizes = np.diff(tp)
-    assert tp[0] == 0 and tp[-1] == G.num_edges and sizes.max() <= 128 and sizes.min() > 0
     starts = set(lay.dst_ptr.numpy().tolist())
-    assert all(int(t) in starts for t in tp)  # every cut is a node boundary
-    assert 2 * 256 < ntiles <= 3 * 256
-    assert lay.plan[1] > ntiles  # the 64-row plan has more, smaller tiles
+    for (tile_ptr, ntiles), rows, rounds in ((lay.plan[:2], 64, 5), (lay.plan_wide, 128, 3)):
+        tp = tile_ptr.numpy().astype(np.int64)
+        sizes = np.diff(tp)
+        assert tp[0] == 0 and tp[-1] == G.num_edges and sizes.max() <= rows and sizes.min() > 0
+        assert all(int(t) in starts for t in tp)  # every cut is a node boundary
+        assert (rounds - 1) * 256 < ntiles <= rounds * 256, (rows, ntiles)
+    assert lay.plan[1] > lay.plan_wide[1]  # the 64-row plan has more, smaller tiles

@@ -1,7 +1,8 @@
-"""GPU parity of the fp32 layer kernel on the two-part fp16 split (update_fk_kernel): 128-row balanced
-tile plans, both scan-round variants, the amax chain that scales the split, operands far from unit
-magnitude, hidden sizes beyond 512 (the reference accepts any hidden_dim, chemprop.py:54), and the
-kernel's row-capacity check.  Oracle: fp64 evaluation of chemprop.py:36-43 / residual.py:27-28 and
+"""GPU parity of the fp32 layer kernels on the two-part fp16 split: update_fk2_kernel (h <= 384: 64-row
+balanced tile plans, output staged in LDS and stored during the next tile) and the column-chunked
+update_fk_kernel (h > 384), every aggregation variant, the amax chain that scales the split, operands
+far from unit magnitude, hidden sizes beyond 512 (the reference accepts any hidden_dim,
+chemprop.py:54), and the kernels' row-capacity check.  Oracle: fp64 evaluation of chemprop.py:36-43 / residual.py:27-28 and
 the CPU scatter of the kernel's own H_out (chemprop.py:37-39, :86); fp32 contract FP32_NORM_TOL."""
 import pytest
 import torch
@@ -32,7 +33,7 @@ def _layout(G, rows):
     dst_ptr, perm = K.csr_build(G.edge_index[1].contiguous().to(DEV), G.num_nodes)
     deg = (dst_ptr[1:] - dst_ptr[:-1]).cpu()
     maxdeg = int(deg.max())
-    plan = K.tile_plan(dst_ptr, G.num_edges, maxdeg, rows=rows, ncu=K.PLAN_NCU if rows == 128 else 0)
+    plan = K.tile_plan(dst_ptr, G.num_edges, maxdeg, rows=rows, ncu=K.PLAN_NCU)
     return perm, plan, maxdeg, bool((deg == 0).any())
 
 
@@ -48,9 +49,9 @@ def _ref_layer(G, H, S, W, b, residual, act, agg_act, reduce="sum"):
 @pytest.mark.parametrize("h", [300, 256, 128, 36])
 @pytest.mark.parametrize("exact_deg", [True, False])
 def test_wide_plan_fused_layer(h, rev_offset, exact_deg):
-    """128-row tiles (plan balanced over the CUs); exact_deg passes the true max in-degree (3-round
-    scan variant for molecules), else 32 (16-round variant): same H_out, node sums bit-identical to
-    the CPU scatter of the kernel's own H_out."""
+    """Tiles of the kernel's capacity (plan balanced over the CUs); exact_deg passes the true max
+    in-degree, else 32: same H_out, node sums bit-identical to the CPU scatter of the kernel's own
+    H_out (phase B sums each node's rows left to right)."""
     K = _K()
     G = _graph("qm9", 300, seed=h, rev_offset=rev_offset)
     E, V = G.num_edges, G.num_nodes
@@ -58,13 +59,15 @@ def test_wide_plan_fused_layer(h, rev_offset, exact_deg):
     H, S = torch.randn(E, h, generator=g), torch.randn(V, h, generator=g)
     lin = nn.Linear(h, h)
     W, b = lin.weight.detach(), lin.bias.detach()
-    perm, plan, maxdeg, zf = _layout(G, 128)
-    assert max(int(x) for x in (plan[0][1:] - plan[0][:-1]).cpu()) <= 128
     relu = K.act_code(nn.ReLU())
+    cap = K.fused_tile_rows(h, torch.float32, relu, "sum", relu)
+    assert cap == 64
+    perm, plan, maxdeg, zf = _layout(G, cap)
+    assert max(int(x) for x in (plan[0][1:] - plan[0][:-1]).cpu()) <= cap
     amax_out = torch.zeros(2, device=DEV)
     Hn, Sn = K.dmpnn_update_fused(
         H.to(DEV), S.to(DEV), G.edge_index[0].to(DEV), G.rev_index.to(DEV), K.pack_weights(W.to(DEV)), b.to(DEV),
-        residual=True, act=relu, plan=plan, tile_rows=128, max_in_degree=maxdeg if exact_deg else 32, perm=perm,
+        residual=True, act=relu, plan=plan, tile_rows=cap, max_in_degree=maxdeg if exact_deg else 32, perm=perm,
         reduce="sum", agg_act=relu, zero_fill=zf, amax_out=amax_out,
     )
     rH, rS = _ref_layer(G, H, S, W, b, True, torch.relu, torch.relu)
@@ -88,12 +91,12 @@ def test_split_scaling_far_from_unit_magnitude(scale):
     g = torch.Generator().manual_seed(11)
     H, S = torch.randn(E, h, generator=g) * scale, torch.randn(V, h, generator=g) * scale
     W = torch.randn(h, h, generator=g) / h ** 0.5 * (1e-3 if scale > 1 else 1e3)
-    perm, plan, maxdeg, zf = _layout(G, 128)
+    perm, plan, maxdeg, zf = _layout(G, 64)
     relu = K.act_code(nn.ReLU())
     ident = K.act_code(nn.Identity())
     Hn, Sn = K.dmpnn_update_fused(
         H.to(DEV), S.to(DEV), G.edge_index[0].to(DEV), G.rev_index.to(DEV), K.pack_weights(W.to(DEV)), None,
-        residual=True, act=relu, plan=plan, tile_rows=128, max_in_degree=maxdeg, perm=perm, reduce="sum",
+        residual=True, act=relu, plan=plan, tile_rows=64, max_in_degree=maxdeg, perm=perm, reduce="sum",
         agg_act=ident, zero_fill=zf,
     )
     rH, rS = _ref_layer(G, H, S, W, None, True, torch.relu, lambda x: x)
@@ -103,12 +106,13 @@ def test_split_scaling_far_from_unit_magnitude(scale):
 
 @pytest.mark.parametrize("reduce", ["mean", "max", "min"])
 def test_narrow_generic_reduce(reduce):
-    """mean / max / min aggregation: 64-row capacity (nt_dmpnn_fused_tile_rows), generic variant."""
+    """mean / max / min aggregation (the generic fk2 variant), node values bit-identical to the CPU
+    scatter of the kernel's H_out."""
     K = _K()
     h = 300
     relu = K.act_code(nn.ReLU())
     assert K.fused_tile_rows(h, torch.float32, relu, reduce, relu) == 64
-    assert K.fused_tile_rows(h, torch.float32, relu, "sum", relu) == 128
+    assert K.fused_tile_rows(h, torch.float32, relu, "sum", relu) == 64
     G = _graph("qm9", 90, seed=7)
     E, V = G.num_edges, G.num_nodes
     g = torch.Generator().manual_seed(5)
@@ -192,9 +196,9 @@ def test_block_wide_hidden_gradients():
         assert_parity(m.linear.weight.grad, W64[i].grad, FP32_NORM_TOL, f"dW{i}")
 
 
-def test_engine_uses_wide_plan_and_amax_chain():
-    """The block at config-2 shape runs the 128-row plan (one launch per layer) and matches the
-    oracle; the plan the collate shipped equals the device planner's."""
+def test_engine_uses_balanced_plan_and_amax_chain():
+    """The block at config-2 shape runs fk2 on the balanced 64-row plan (one launch per layer) and
+    matches the oracle; the plan the collate shipped equals the device planner's."""
     from notorch_amd.nn import ChempropBlock
     from notorch_amd.nn.gnn import _engine
 
@@ -202,8 +206,8 @@ def test_engine_uses_wide_plan_and_amax_chain():
     h = 300
     G = _graph("qm9", 512, seed=4)
     lay = G._nt_layout
-    d_tp, d_n, _ = K.tile_plan(lay.dst_ptr.to(DEV), G.num_edges, lay.deg_range[0], rows=128, ncu=K.PLAN_NCU)
-    assert d_n == lay.plan_wide[1] and torch.equal(d_tp.cpu(), lay.plan_wide[0])
+    d_tp, d_n, _ = K.tile_plan(lay.dst_ptr.to(DEV), G.num_edges, lay.deg_range[0], rows=64, ncu=K.PLAN_NCU)
+    assert d_n == lay.plan[1] and torch.equal(d_tp.cpu(), lay.plan[0])
     torch.manual_seed(0)
     Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
     blk = ChempropBlock(hidden_dim=h, depth=3).eval()
@@ -216,6 +220,51 @@ def test_engine_uses_wide_plan_and_amax_chain():
             out = blk.to(DEV)(G.update(node_feats=Xv, edge_feats=Xe).to(DEV))
     finally:
         _engine.UPDATE_EVENTS = None
-    assert len(events) == 3 and _engine.LAST_UPDATE_INFO["kernel_short"] == "update_fk"
+    assert len(events) == 3 and _engine.LAST_UPDATE_INFO["kernel_short"] == "update_fk2"
     assert_parity(out.edge_feats, ref_e, FP32_NORM_TOL, "edge")
     assert_parity(out.node_feats, ref_n, FP32_NORM_TOL, "node")
+
+
+@pytest.mark.parametrize("h", [300, 36])
+def test_plain_layer_without_aggregation(h):
+    """No tile plan (the layerwise / hub path): fixed 64-row tiles in edge order, H_out only."""
+    K = _K()
+    G = _graph("qm9", 200, seed=h + 5)
+    E, V = G.num_edges, G.num_nodes
+    g = torch.Generator().manual_seed(h)
+    H, S = torch.randn(E, h, generator=g), torch.randn(V, h, generator=g)
+    lin = nn.Linear(h, h)
+    W, b = lin.weight.detach(), lin.bias.detach()
+    relu = K.act_code(nn.ReLU())
+    Hn, Sn = K.dmpnn_update_fused(H.to(DEV), S.to(DEV), G.edge_index[0].to(DEV), G.rev_index.to(DEV),
+                                  K.pack_weights(W.to(DEV)), b.to(DEV), residual=True, act=relu)
+    assert Sn is None
+    rH, _ = _ref_layer(G, H, S, W, b, True, torch.relu, torch.relu)
+    assert_parity(Hn, rH, FP32_NORM_TOL, f"H h={h}")
+
+
+@pytest.mark.parametrize("agg", ["relu", "identity", "tanh"])
+def test_fused_aggregation_acts(agg):
+    """Aggregation activations: relu / identity (fast fk2 variants) and a generic one (tanh)."""
+    K = _K()
+    h = 300
+    acts = {"relu": (nn.ReLU(), torch.relu), "identity": (nn.Identity(), lambda x: x), "tanh": (nn.Tanh(), torch.tanh)}
+    mod, fn = acts[agg]
+    G = _graph("qm9", 120, seed=21)
+    E, V = G.num_edges, G.num_nodes
+    g = torch.Generator().manual_seed(21)
+    H, S = torch.randn(E, h, generator=g), torch.randn(V, h, generator=g)
+    W = torch.randn(h, h, generator=g) / h ** 0.5
+    relu = K.act_code(nn.ReLU())
+    perm, plan, maxdeg, zf = _layout(G, 64)
+    Hn, Sn = K.dmpnn_update_fused(
+        H.to(DEV), S.to(DEV), G.edge_index[0].to(DEV), G.rev_index.to(DEV), K.pack_weights(W.to(DEV)), None,
+        residual=True, act=relu, plan=plan, tile_rows=64, max_in_degree=maxdeg, perm=perm, reduce="sum",
+        agg_act=K.act_code(mod), zero_fill=zf,
+    )
+    rH, rS = _ref_layer(G, H, S, W, None, True, torch.relu, fn)
+    assert_parity(Hn, rH, FP32_NORM_TOL, f"H {agg}")
+    assert_parity(Sn, rS, FP32_NORM_TOL, f"S {agg}")
+    if agg != "tanh":  # device tanh may differ from the CPU's by an ulp
+        exact = dmpnn_ref.scatter(fn(Hn.cpu()), G.edge_index[1], V, "sum")
+        assert torch.equal(Sn.cpu(), exact), agg

@@ -1,5 +1,6 @@
-"""Micro-benchmark of the individual kernels (device time via torch.cuda events, interleaved
-rounds in one process).  Usage: python tools/kbench.py [--mols 4096] [--h 300]"""
+"""Micro-benchmark of the individual fp32 forward kernels on one qm9-shaped batch (device time via
+torch.cuda events, interleaved rounds in one process).  Also the driver for the per-kernel PMC passes
+(tools/pmc_update.sh).  Usage: python tools/kbench.py [--mols 4096] [--h 300] [--only fk_fused,init]"""
 import argparse
 import os
 import statistics
@@ -31,133 +32,77 @@ def main():
     p.add_argument("--h", type=int, default=300)
     p.add_argument("--only", default="", help="comma list of kernels to time")
     p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--abl", default="", help="NT_LIB=diag: comma list of NT_FK_ABL ablations of fk_fused")
     a = p.parse_args()
     G = make_batch(a.kind, a.mols, seed=0).collate("nodes").to("cuda")
     V, E, h = G.num_nodes, G.num_edges, a.h
     lay = G._nt_layout
-    H = torch.randn(E, h, device="cuda")
-    S = torch.randn(V, h, device="cuda")
-    Xv = torch.randn(V, h, device="cuda")
-    W = torch.randn(h, h, device="cuda") / 17
-    b = torch.randn(h, device="cuda")
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    H = torch.randn(E, h, device="cuda", generator=gen)
+    S = torch.randn(V, h, device="cuda", generator=gen)
+    Xv = torch.randn(V, h, device="cuda", generator=gen)
+    W = torch.randn(h, h, device="cuda", generator=gen) / 17
+    b = torch.randn(h, device="cuda", generator=gen)
     Wp = K.pack_weights(W)
     src, rev = G.edge_index[0].contiguous(), G.rev_index
     out = torch.empty_like(H)
-    relu = K.act_code(torch.nn.ReLU())
-    def upd(variant, cfg="a", mode="0"):
-        def f():
-            os.environ["NT_UPDATE_KERNEL"] = variant
-            os.environ["NT_X6_CFG"] = cfg
-            os.environ["NT_PC_MODE"] = mode
-            K.dmpnn_update(H, S, src, rev, Wp, b, act=relu, out=out)
-        return f
-
-    deg = (lay.dst_ptr[1:] - lay.dst_ptr[:-1]).max().item()
-    plan = K.tile_plan(lay.dst_ptr, E, int(deg))
     S2 = torch.empty_like(S)
+    relu = K.act_code(torch.nn.ReLU())
+    amax = torch.zeros(2, device="cuda")
+    K.absmax(H, amax[0:1])
+    K.absmax(S, amax[1:2])
+    amax_out = torch.zeros(2, device="cuda")
+    deg = int((lay.dst_ptr[1:] - lay.dst_ptr[:-1]).max().item())
+    plans = {}
+    for rows in (64, 128):
+        plan = K.tile_plan(lay.dst_ptr, E, deg, rows=rows, ncu=K.PLAN_NCU)
+        rt = K.dmpnn_row_table(lay.dst_perm, plan[2], src, rev, V)
+        plans[rows] = (plan, rt)
 
-    ident = torch.arange(E, dtype=torch.int32, device="cuda")
-    fake_d = (ident.long() * V // E).to(torch.int32)  # monotone, < V: timing stand-in only
-    eplan = (torch.arange(0, E + 64, 64, dtype=torch.int32, device="cuda").clamp_(max=E), (E + 63) // 64, fake_d)
+    def fk(rows, abl=None):
+        plan, rt = plans[rows]
 
-    def fused_edge_order():
-        os.environ["NT_PS_ABL"] = "0"
-        K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=eplan, perm=ident, agg_act=relu,
-                             out=out, S_out=S2)
-
-    def fused(kmid=None, with_plan=True, abl=0, kern="pk", pkabl=0):
         def f():
-            os.environ["NT_FUSED_KERNEL"] = kern
-            os.environ["NT_PS_ABL"] = str(abl)
-            os.environ["NT_PK_ABL"] = str(pkabl)
-            if kmid is not None:
-                os.environ["NT_PS_KMID"] = str(kmid)
-            else:
-                os.environ.pop("NT_PS_KMID", None)
-            K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=plan if with_plan else None,
-                                 perm=lay.dst_perm, agg_act=relu, out=out,
-                                 S_out=S2 if with_plan else None)
+            os.environ["NT_FK_ABL"] = str(abl or 0)
+            K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=plan, tile_rows=rows, max_in_degree=deg,
+                                 perm=lay.dst_perm, agg_act=relu, amax_in=amax, amax_out=amax_out,
+                                 row_table=rt, out=out, S_out=S2)
         return f
+
+    def fk_plain():
+        K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, amax_in=amax, amax_out=amax_out, out=out)
 
     fns = {
-        "fused": fused(),
-        "fused_ps": fused(kern="ps"),
-        "pk_unfused": fused(with_plan=False),
-        "pk_noprod": fused(pkabl=1),
-        "pk_noprod_noW": fused(pkabl=3),
-        "pk_noprod_nores": fused(pkabl=5),
-        "pk_noprod_noW_nores": fused(pkabl=7),
-        "pk_noprod_nomfma": fused(pkabl=9),
-        "pk_noprod_all": fused(pkabl=15),
-        "fused_edgeorder": fused_edge_order,
-        "fused_k0": fused(0, kern="ps"),
-        "fused_k3": fused(3, kern="ps"),
-        "fused_k7": fused(7, kern="ps"),
-        "ps": fused(with_plan=False, kern="ps"),
-        "ps_noprod": fused(with_plan=False, abl=1, kern="ps"),
-        "ps_nomfma": fused(with_plan=False, abl=2, kern="ps"),
-        "ps_noW": fused(with_plan=False, abl=4, kern="ps"),
-        "ps_nosplit": fused(with_plan=False, abl=8, kern="ps"),
-        "ps_noprod_noW": fused(with_plan=False, abl=5, kern="ps"),
-        "ps_noprod_nosplit": fused(with_plan=False, abl=9, kern="ps"),
-        "ps_noprod_noW_nosplit": fused(with_plan=False, abl=13, kern="ps"),
-        "ps_noprod_nomfma": fused(with_plan=False, abl=3, kern="ps"),
-        "ps_nomfma_noW": fused(with_plan=False, abl=6, kern="ps"),
-        "fused_noprod": fused(abl=1, kern="ps"),
-        "fused_noHres": fused(abl=32, kern="ps"),
-        "fused_nostore": fused(abl=64, kern="ps"),
-        "fused_noHres_nostore": fused(abl=96, kern="ps"),
-        "fused_nomfma_noHres": fused(abl=34, kern="ps"),
-        "fused_nomfma_noHres_nostore": fused(abl=98, kern="ps"),
-        "fused_nomfma": fused(abl=2, kern="ps"),
-        "update": upd("as"),
-        "update_pc": upd("pc"),
-        "pc_noW": upd("pc", mode="2"),
-        "pc_oneW": upd("pc", mode="4"),
-        "pc_noW_oneW": upd("pc", mode="6"),
-        "pc_noMFMA": upd("pc", mode="8"),
-        "pc_noW_noMFMA": upd("pc", mode="10"),
-        "update_x6": upd("x6"),
-        "update_x6b": upd("x6", "b"),
-        "update_x6c": upd("x6", "c"),
-        "update_x6d": upd("x6", "d"),
-        "update_resacc": upd("x6", "r"),
-        "abl_noW": upd("x6", "1"),
-        "abl_noSH": upd("x6", "2"),
-        "abl_noDMA": upd("x6", "3"),
-        "abl_noMFMA": upd("x6", "4"),
-        "abl_none": upd("x6", "7"),
-        "update_glds": upd("glds"),
-        "update_ring": upd("ring"),
-        "update_stream": upd("stream"),
-        "update_tile": upd("tile"),
-        "aggregate": lambda: K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V, act=relu, out=S),
-        "init_fused": lambda: K.dmpnn_init(Xv, H, src, lay.dst_ptr, lay.dst_perm, act=relu),
-        "node_scatter": lambda: K.segment_reduce(H, lay.dst_ptr, lay.dst_perm, V),
+        "fk_fused": fk(128),
+        "fk_fused64": fk(64),
+        "fk_plain": fk_plain,
+        "init": lambda: K.dmpnn_init(Xv, H, src, lay.dst_ptr, lay.dst_perm, act=relu, amax=amax_out),
+        "absmax": lambda: K.absmax(H, amax_out[0:1]),
         "pack": lambda: K.pack_weights(W),
     }
+    for n in filter(None, a.abl.split(",")):
+        fns[f"fk_abl{n}"] = fk(64, int(n))
     if a.only:
-        keep = a.only.split(",")
+        keep = a.only.split(",") + [k for k in fns if k.startswith("fk_abl")]
         fns = {k: v for k, v in fns.items() if k in keep}
     for f in fns.values():
         f()
     torch.cuda.synchronize()
-    print(f"V={V} E={E} h={h}")
+    print(f"V={V} E={E} h={h} max_in_degree={deg} tiles128={plans[128][0][1]} tiles64={plans[64][0][1]}")
     res = {n: [] for n in fns}
     for _ in range(a.rounds):  # interleaved rounds
         for name, f in fns.items():
             res[name].append(timeit(f, 10))
-    for name, f in fns.items():
+    for name in fns:
         med = statistics.median(r[0] for r in res[name])
         mn = min(r[1] for r in res[name])
         extra = ""
-        if name.startswith(("update", "abl", "pc_", "fused", "ps", "pk")):
-            extra = f"  {2 * E * h * h / (med * 1e-6) / 1e12:.1f} TF/s"
-        else:
-            rows = {"aggregate": E + V, "init_fused": 3 * E + V, "node_scatter": E + V, "pack": 0}[name]
-            if rows:
-                extra = f"  {rows * h * 4 / (med * 1e-6) / 1e9:.0f} GB/s alg"
-        print(f"{name:14s} median {med:8.1f} us  min {mn:8.1f} us{extra}")
+        if name.startswith("fk"):
+            extra = f"  {2 * E * h * h / (med * 1e-6) / 1e12:.1f} TF/s fp32-equivalent"
+        elif name in ("init", "absmax"):
+            rows = {"init": 3 * E + V, "absmax": E}[name]
+            extra = f"  {rows * h * 4 / (med * 1e-6) / 1e9:.0f} GB/s alg"
+        print(f"{name:12s} median {med:8.1f} us  min {mn:8.1f} us{extra}")
 
 
 if __name__ == "__main__":

@@ -1,8 +1,12 @@
-"""Training-step timing of ChempropBlock + Sum readout (forward + backward) at config 2:
-kernel backward (default) vs the recompute-in-torch backward (NT_BWD=torch).
+"""Training-step timing of ChempropBlock + Sum readout (forward + backward) at config 2.
+
+Modes: `kernel` (the kernel backward, the weight grad per NT_WGRAD) and `torch` (the
+recompute-in-torch backward, NT_BWD=torch).  bench.py's `training` key runs this once per weight-grad
+path (NT_WGRAD=kernel / library), each in a fresh process, with --json.
 Usage: python tools/train_bench.py [--kind qm9] [--mols 4096] [--h 300] [--depth 3] [--dtype f32|bf16]
-                                  [--steps 20]"""
+                                  [--steps 30] [--warmup 10] [--modes kernel,torch] [--json]"""
 import argparse
+import json
 import os
 import statistics
 import sys
@@ -19,13 +23,19 @@ def main():
     p.add_argument("--kind", default="qm9")
     p.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     p.add_argument("--mols", type=int, default=4096)
+    p.add_argument("--seed", type=int, default=1000, help="batch seed (bench.py rank 0: 1000)")
     p.add_argument("--h", type=int, default=300)
     p.add_argument("--depth", type=int, default=3)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=30)
+    p.add_argument("--warmup", type=int, default=10)
     p.add_argument("--modes", default="kernel,torch")
+    p.add_argument("--json", action="store_true", help="print one JSON object instead of the table")
     a = p.parse_args()
+    from notorch_amd import _lib
+
+    _lib.load()  # fail loudly if the HIP extension is missing
     dt = {"f32": torch.float32, "bf16": torch.bfloat16}[a.dtype]
-    G = make_batch(a.kind, a.mols, seed=0).collate("nodes")
+    G = make_batch(a.kind, a.mols, seed=a.seed).collate("nodes")
     torch.manual_seed(0)
     ev = torch.nn.EmbeddingBag(42, a.h, mode="sum")
     ee = torch.nn.EmbeddingBag(13, a.h, mode="sum")
@@ -52,7 +62,7 @@ def main():
     for mode in a.modes.split(","):
         os.environ["NT_BWD"] = mode
         for name, fn in (("fwd", fwd), (f"train[{mode}]", step)):
-            for _ in range(3):
+            for _ in range(a.warmup):
                 fn()
             torch.cuda.synchronize()
             ts = []
@@ -64,6 +74,13 @@ def main():
                 e.synchronize()
                 ts.append(s.elapsed_time(e))
             res[name] = statistics.median(ts)
+    if a.json:
+        print(json.dumps({
+            "V": G.num_nodes, "E": E, "h": a.h, "depth": a.depth, "dtype": a.dtype,
+            "weight_grad": os.environ.get("NT_WGRAD", "default"), "warmup": a.warmup, "steps": a.steps,
+            "ms": res, "edge_messages_per_s": {k: E * a.depth / (v * 1e-3) for k, v in res.items()},
+        }), flush=True)
+        return
     print(f"{a.kind} V={G.num_nodes} E={E} h={a.h} depth={a.depth} {a.dtype}")
     for k, v in res.items():
         print(f"{k:14s} {v:8.3f} ms/step  {E * a.depth / (v * 1e-3):.3e} edge-msg/s")
