@@ -35,11 +35,13 @@ namespace fk {
 constexpr int kStageV = 97;  // float4 per staged row: odd row stride >= hv (h <= 384)
 constexpr int kFk2MaxH = 384;
 constexpr int kNodeInfo = 68;  // ints per tile: [0] node count, [1 + k] first row of node k, then n
-constexpr int kPre = 4;        // residual rows prefetched per item (nodes with more rows load the rest inline)
+constexpr int kPre = 3;        // residual rows prefetched per item (nodes with more rows load the rest inline)
 
 template <int CT, int GD>
 struct State2 : State<4, CT, GD> {
   f32x4 rres[kPre];  // residual pieces of the thread's first item of the next batch
+  int it_e[kPre];    // ... its rows' edges (first kPre rows), node, float4 column, first row, row count
+  int it_v, it_p, it_r0, it_n;
   f32x4* stage;      // 64 x hsv float4
   f32x4* sbias;      // bias (zeros without one), hv float4
   int* ninfo;        // kEmaps x kNodeInfo
@@ -80,26 +82,32 @@ __device__ __forceinline__ void fk2_node_list(const int4* emap, int* ni, int lan
   }
 }
 
-// residual pieces of the first item of batch b of the staged tile (slot x): unconditional loads
-// (rows past the node read S's first row), masked at use
+// the thread's first item of batch b of the staged tile (slot x, nn nodes): its rows' edges, node,
+// column and residual pieces (unconditional loads: rows past the node read S's first row)
 template <int CT, int GD>
-__device__ __forceinline__ void fk2_prefetch(State2<CT, GD>& st, const Args& a, bool resid, int x, int b) {
+__device__ __forceinline__ void fk2_prefetch(State2<CT, GD>& st, const Args& a, bool resid, int x, int nn, int b) {
   const int* ni = st.ninfo + x * kNodeInfo;
-  int k0, cnt;
-  fk2_batch(ni, st.KS, b, k0, cnt);
-  const bool valid = resid && st.tid < cnt * st.hv;
+  const int4* em = st.emap + x * 64;
+  const int nb = (nn + st.KS - 1) / st.KS, k0 = b * nb;
+  const int cnt = nn - k0 < 0 ? 0 : (nn - k0 < nb ? nn - k0 : nb);
+  const bool ok = st.tid < cnt * st.hv;
   int k, p;
-  fk2_item(valid ? st.tid : 0, st.hv, st.rhv, k, p);
-  const int kk = valid ? k0 + k : 0;
-  const int r0 = valid ? ni[1 + kk] : 0, r1 = valid ? ni[2 + kk] : 0;
+  fk2_item(ok ? st.tid : 0, st.hv, st.rhv, k, p);
+  const int kk = ok ? k0 + k : 0;
+  const int r0 = ok ? ni[1 + kk] : 0, r1 = ok ? ni[2 + kk] : 0;
   const f32x4* R4 = reinterpret_cast<const f32x4*>(resid ? a.H : a.S);
 #pragma unroll
   for (int u = 0; u < kPre; ++u) {
-    const int r = r0 + u;
-    const int e = st.emap[x * 64 + (r < 64 ? r : 63)].x;
-    const int64_t off = (r < r1 && e >= 0) ? (int64_t)e * st.hv + p : 0;
+    const int r = r0 + u < 64 ? r0 + u : 63;
+    const int4 ri = em[r];
+    if (u == 0) st.it_v = ri.y;
+    st.it_e[u] = ri.x;
+    const int64_t off = (resid && r0 + u < r1 && ri.x >= 0) ? (int64_t)ri.x * st.hv + p : 0;
     st.rres[u] = R4[off];
   }
+  st.it_p = p;
+  st.it_r0 = r0;
+  st.it_n = r1 - r0;  // 0: no item
 }
 
 // one row of an item: x = stage + residual -> H_out, folded into the node's reduction
@@ -123,51 +131,56 @@ __device__ __forceinline__ void fk2_row(const Args& a, const f32x4& sx, const f3
   }
 }
 
-// batch b of the staged tile (slot x): H_out of its nodes' rows, S_out of its nodes
+// batch b of the staged tile (slot x, nn nodes): H_out of its nodes' rows, S_out of its nodes.  The
+// thread's first item comes from the prefetch; a second one (batches of more than 512 items) is
+// looked up here
 template <int AACT, bool SUMONLY, bool FUSED, bool STORE = true, int CT, int GD>
-__device__ __forceinline__ void fk2_trickle(State2<CT, GD>& st, const Args& a, bool resid, int x, int b) {
-  const int* ni = st.ninfo + x * kNodeInfo;
+__device__ __forceinline__ void fk2_trickle(State2<CT, GD>& st, const Args& a, bool resid, int x, int nn, int b) {
   const int4* em = st.emap + x * 64;
-  int k0, cnt;
-  fk2_batch(ni, st.KS, b, k0, cnt);
-  const int items = cnt * st.hv;
   const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H);
+  const f32x4 z4 = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (st.it_n > 0) {
+    const int p = st.it_p, r0 = st.it_r0, n = st.it_n;
+    f32x4 acc = z4;
+    float c = 0.f;
+    f32x4 sx[kPre];
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    const int q = st.tid + 512 * m;
-    if (q < items) {
-      int k, p;
-      fk2_item(q, st.hv, st.rhv, k, p);
-      const int r0 = ni[1 + k0 + k], r1 = ni[2 + k0 + k];
-      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
-      float n = 0.f;
-      // rows r0 .. r0 + kPre - 1: stage reads issued together, residual from the prefetch (item 0)
-      f32x4 sx[kPre];
-      int e[kPre];
+    for (int u = 0; u < kPre; ++u) sx[u] = st.stage[(u < n ? r0 + u : r0) * st.hsv + p];
 #pragma unroll
-      for (int u = 0; u < kPre; ++u) {
-        const int r = r0 + u < r1 ? r0 + u : r0;
-        sx[u] = st.stage[r * st.hsv + p];
-        e[u] = em[r].x;
-      }
-#pragma unroll
-      for (int u = 0; u < kPre; ++u) {
-        if (r0 + u < r1) {
-          const f32x4 rv = m == 0 ? st.rres[u] : (resid ? H4[(int64_t)e[u] * st.hv + p] : f32x4{0.f, 0.f, 0.f, 0.f});
-          fk2_row<AACT, SUMONLY, FUSED, STORE>(a, sx[u], rv, resid, e[u], st.hv, p, u == 0, acc, n, st.mxH);
-        }
-      }
-      for (int r = r0 + kPre; r < r1; ++r) {  // hub rows (> kPre in-edges)
-        const int er = em[r].x;
-        const f32x4 rv = resid ? H4[(int64_t)er * st.hv + p] : f32x4{0.f, 0.f, 0.f, 0.f};
-        fk2_row<AACT, SUMONLY, FUSED, STORE>(a, st.stage[r * st.hsv + p], rv, resid, er, st.hv, p, false, acc, n,
-                                             st.mxH);
-      }
-      if constexpr (FUSED) {
-        if (!SUMONLY && a.reduce == NT_MEAN) acc = acc / n;
-        if constexpr (STORE) reinterpret_cast<f32x4*>(a.SO)[(int64_t)em[r0].y * st.hv + p] = acc;
-        st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(acc[0]), fabsf(acc[1])), fmaxf(fabsf(acc[2]), fabsf(acc[3]))));
-      }
+    for (int u = 0; u < kPre; ++u)
+      if (u < n) fk2_row<AACT, SUMONLY, FUSED, STORE>(a, sx[u], st.rres[u], resid, st.it_e[u], st.hv, p, u == 0, acc, c, st.mxH);
+    for (int r = r0 + kPre; r < r0 + n; ++r) {  // rows past the prefetched ones (in-degree > kPre)
+      const int er = em[r].x;
+      const f32x4 rv = resid ? H4[(int64_t)er * st.hv + p] : z4;
+      fk2_row<AACT, SUMONLY, FUSED, STORE>(a, st.stage[r * st.hsv + p], rv, resid, er, st.hv, p, false, acc, c, st.mxH);
+    }
+    if constexpr (FUSED) {
+      if (!SUMONLY && a.reduce == NT_MEAN) acc = acc / c;
+      if constexpr (STORE) reinterpret_cast<f32x4*>(a.SO)[(int64_t)st.it_v * st.hv + p] = acc;
+      st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(acc[0]), fabsf(acc[1])), fmaxf(fabsf(acc[2]), fabsf(acc[3]))));
+    }
+  }
+  // second item (q = tid + 512)
+  const int nb = (nn + st.KS - 1) / st.KS, k0 = b * nb;
+  const int cnt = nn - k0 < 0 ? 0 : (nn - k0 < nb ? nn - k0 : nb);
+  const int q = st.tid + 512;
+  if (q < cnt * st.hv) {
+    const int* ni = st.ninfo + x * kNodeInfo;
+    int k, p;
+    fk2_item(q, st.hv, st.rhv, k, p);
+    const int r0 = ni[1 + k0 + k], r1 = ni[2 + k0 + k];
+    f32x4 acc = z4;
+    float c = 0.f;
+    for (int r = r0; r < r1; ++r) {
+      const int er = em[r].x;
+      const f32x4 rv = resid ? H4[(int64_t)er * st.hv + p] : z4;
+      fk2_row<AACT, SUMONLY, FUSED, STORE>(a, st.stage[r * st.hsv + p], rv, resid, er, st.hv, p, r == r0, acc, c,
+                                           st.mxH);
+    }
+    if constexpr (FUSED) {
+      if (!SUMONLY && a.reduce == NT_MEAN) acc = acc / c;
+      if constexpr (STORE) reinterpret_cast<f32x4*>(a.SO)[(int64_t)em[r0].y * st.hv + p] = acc;
+      st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(acc[0]), fabsf(acc[1])), fmaxf(fabsf(acc[2]), fabsf(acc[3]))));
     }
   }
 }
@@ -217,7 +230,9 @@ __device__ __forceinline__ void fk2_stage_one(State2<CT, GD>& st) {
 
 // ABL (diagnostic builds only, 0 in the shipping library): timing ablations, results invalid --
 // 1 gathers read row 0, 2 no MFMA, 4 no split, 8 no trickle stores, 16 no residual prefetch,
-// 32 no W loads, 64 no trickle at all.
+// 32 no W loads, 64 no trickle at all, 128 per-phase cycle stamps summed into g_pk_stamps
+// ([0] W + gather issue, [1] MFMA, [2] split, [3] trickle + prefetch, [4] barrier, [5] tile end,
+// [6] whole loop, [7] waves).
 // TABLE: fused (rows from the row table, S_out) or plain / dense (fixed 64-row tiles in edge order)
 template <int CT, int ACT, int AACT, bool SUMONLY, bool TABLE, int GD = 2, int ABL = 0>
 __global__ void __launch_bounds__(kThreads, 2) update_fk2_kernel(Args a) {
@@ -314,8 +329,12 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk2_kernel(Args a) {
   // tile yet" during tile 0
   if (tid < kEmaps) st.ninfo[tid * kNodeInfo] = 0;
 #pragma unroll
-  for (int u = 0; u < kPre; ++u) st.rres[u] = f32x4{0.f, 0.f, 0.f, 0.f};
-  int x_prv = kEmaps - 1;
+  for (int u = 0; u < kPre; ++u) {
+    st.rres[u] = f32x4{0.f, 0.f, 0.f, 0.f};
+    st.it_e[u] = 0;
+  }
+  st.it_v = st.it_p = st.it_r0 = st.it_n = 0;
+  int x_prv = kEmaps - 1, nn_prv = 0;  // staged tile: emap slot, node count
 
   // ---- prologue: node lists of tiles 0 and 1, steps 0 and 1 staged, W of step 0, slice 0 split
   __syncthreads();  // emap of tiles 0 and 1
@@ -330,6 +349,16 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk2_kernel(Args a) {
   fk_barrier();
 
   // ---- main loop: one 32-deep k-step per iteration, two iterations per trip (register parity)
+  constexpr bool STAMP = (ABL & 128) != 0;
+  unsigned long long tacc[6] = {0, 0, 0, 0, 0, 0}, tp = 0, tb = 0;
+  if constexpr (STAMP) tb = tp = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](int slot) __attribute__((always_inline)) {
+    if constexpr (STAMP) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      tacc[slot] += t - tp;
+      tp = t;
+    }
+  };
   int g = 0, i = 0, k = 0;
   while (g < G) {
 #pragma unroll
@@ -352,34 +381,42 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk2_kernel(Args a) {
           if (GD == 1 || P == 0) fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s2);
           else fk_gather<RT, CT, ACT, GD - 1>(st, a, so, qo, s2);
         }
+        stamp(0);
         // (3) MFMAs of step g
         if constexpr ((ABL & 2) == 0) {
           if (P == 0) fk_mfma<RT, CT, 0>(st, 0, (n_cur + 15) >> 4);
           else fk_mfma<RT, CT, 1>(st, 0, (n_cur + 15) >> 4);
         }
+        stamp(1);
         // (4) split step g + 1's staged piece into the other buffer
         if constexpr ((ABL & 4) == 0) {
           if (P == 0) fk2_split<CT, ACT, GD - 1, 1>(st, a, s1);
           else fk2_split<CT, ACT, 0, 0>(st, a, s1);
         }
+        stamp(2);
         // (5) batch s of the staged tile; then the residual rows of the next batch (batch s + 1, or
         // batch 0 of this tile, which is staged at this step's end)
         if constexpr ((ABL & 64) == 0) {
-          fk2_trickle<AACT, SUMONLY, TABLE, (ABL & 8) == 0>(st, a, resid, x_prv, s);
+          fk2_trickle<AACT, SUMONLY, TABLE, (ABL & 8) == 0>(st, a, resid, x_prv, nn_prv, s);
           if constexpr ((ABL & 16) == 0) {
             const bool last = s + 1 == KS;
-            fk2_prefetch(st, a, resid, last ? i % kEmaps : x_prv, last ? 0 : s + 1);
+            const int xc = i % kEmaps;
+            const int nn_c = last ? __builtin_amdgcn_readfirstlane(st.ninfo[xc * kNodeInfo]) : nn_prv;
+            fk2_prefetch(st, a, resid, last ? xc : x_prv, nn_c, last ? 0 : s + 1);
           }
         }
         // node list of tile i + 1 (its emap was written at the last advance, before a barrier)
         if (s == 1 && st.wave == 0)
           fk2_node_list(st.emap + ((i + 1) % kEmaps) * ROWS, st.ninfo + ((i + 1) % kEmaps) * kNodeInfo, st.lane);
+        stamp(3);
         fk_barrier();
+        stamp(4);
         // (6) end of the tile's K loop: stage this tile (the previous one is finished)
         ++g;
         if (++k == KS) {
           fk2_stage_one<0, 0, CT, GD>(st);
           x_prv = i % kEmaps;
+          nn_prv = __builtin_amdgcn_readfirstlane(st.ninfo[x_prv * kNodeInfo]);
           fk_barrier();
           // advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
           k = 0;
@@ -394,14 +431,23 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk2_kernel(Args a) {
           h2 = h3;
           raw2 = row_raw<RT, TABLE>(a, h2, st.grow);
           h3 = tile_head<RT, TABLE>(a, tile(i + 3));
+          stamp(5);
         }
       }
     }
   }
+  if constexpr (STAMP) {
+    if (st.lane == 0) {
+#pragma unroll
+      for (int q = 0; q < 6; ++q) atomicAdd(&g_pk_stamps[q], tacc[q]);
+      atomicAdd(&g_pk_stamps[6], __builtin_amdgcn_s_memtime() - tb);
+      atomicAdd(&g_pk_stamps[7], 1ull);
+    }
+  }
   // ---- tail: finish the last staged tile (batches 0 .. KS - 1, one barrier each)
   for (int s = 0; s < KS; ++s) {
-    fk2_trickle<AACT, SUMONLY, TABLE>(st, a, resid, x_prv, s);
-    fk2_prefetch(st, a, resid, x_prv, s + 1);
+    fk2_trickle<AACT, SUMONLY, TABLE>(st, a, resid, x_prv, nn_prv, s);
+    fk2_prefetch(st, a, resid, x_prv, nn_prv, s + 1);
     fk_barrier();
   }
   if (a.amax_out) {

@@ -42,7 +42,9 @@ __device__ unsigned long long g_pk_stamps[10];
 // the fp16x3 layer kernel (shares g_pk_timeout: bit 1 = bounded wait gave up, bit 2 = a tile larger
 // than the fk kernel's row capacity)
 #include "update_fk.hpp"
-#include "update_fk2.hpp"
+#ifdef NT_DIAG
+#include "update_fk2.hpp"  // A/B: LDS-staged output variant (NT_FK=2)
+#endif
 
 namespace nt {
 
@@ -753,6 +755,7 @@ int launch_fk_wide(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
                    : launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 16>(a, grid, stream);
 }
 
+#ifdef NT_DIAG
 // fk2 (64-row tiles, output staged in LDS and written during the next tile): h <= 384, any layer
 template <int ACT, int AACT, bool SUMONLY, bool TABLE>
 int launch_fk2_t(const fk::Args& a, int grid, hipStream_t stream) {
@@ -789,6 +792,8 @@ int launch_fk2(const fk::Args& a, int grid, hipStream_t stream) {
       NT_FK2_ABL_CASE(102)
       NT_FK2_ABL_CASE(71)
       NT_FK2_ABL_CASE(24)
+      NT_FK2_ABL_CASE(128)
+      NT_FK2_ABL_CASE(198)
 #undef NT_FK2_ABL_CASE
       default:
         break;
@@ -801,13 +806,18 @@ int launch_fk2(const fk::Args& a, int grid, hipStream_t stream) {
   return launch_fk2_t<-1, -1, false, true>(a, grid, stream);
 }
 
-// which fp32 layer kernel runs: fk2 for h <= 384 (diagnostic builds: NT_FK=1 selects update_fk_kernel)
+#endif  // NT_DIAG
+
+// which fp32 layer kernel runs: update_fk_kernel; diagnostic builds: NT_FK=2 selects the LDS-staged
+// update_fk2_kernel for h <= 384
 bool fk2_selected(int64_t h) {
 #ifdef NT_DIAG
   const char* e = getenv("NT_FK");
-  if (e && e[0] == '1') return false;
+  return e && e[0] == '2' && h <= fk::kFk2MaxH;
+#else
+  (void)h;
+  return false;
 #endif
-  return h <= fk::kFk2MaxH;
 }
 
 // 64-row tiles: every other combination (any reduce, any aggregation act) and h > 384
@@ -888,10 +898,12 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   if (a.ntiles == 0) return NT_OK;
   const int grid = a.ntiles < cu_count() ? a.ntiles : cu_count();
   const int maxl = max_in_degree - 1;  // scan rounds needed within a 16-row tile
+#ifdef NT_DIAG
   if (fk2_selected(u.h)) {
     a.nchunks = 1;
     return launch_fk2(a, grid, u.stream);
   }
+#endif
   // up to 3 column tiles per wave (NT <= 24, one chunk); waves past NT skip theirs at run time
   if (cap == 128) {
     a.nchunks = 1;

@@ -57,9 +57,6 @@ UPDATE_EVENTS: Optional[list] = None
 LAST_UPDATE_INFO: dict = {}
 
 
-FK2_MAX_H = 384  # update_fk2_kernel's hidden-size limit (larger sizes: column-chunked update_fk_kernel)
-
-
 def _note_update(kind: str, dtype: torch.dtype, h: int) -> None:
     kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
     if dtype == torch.bfloat16:
@@ -67,14 +64,11 @@ def _note_update(kind: str, dtype: torch.dtype, h: int) -> None:
                     kernel_short="update_bf16", numerics="bf16 storage, bf16 MFMA, fp32 accumulate",
                     products=1)
     elif kind in ("fused", "persistent"):
-        fk2 = h <= FK2_MAX_H
-        name = "update_fk2_kernel" if fk2 else "update_fk_kernel"
-        shape = ("64-row node-aligned tiles, output staged in LDS and stored during the next tile's K loop"
-                 if fk2 else "64-row node-aligned tiles, column-chunked (h > 384)")
+        rows = 128 if h <= 384 else 64
         tail = ("aggregation of the next layer fused" if kind == "fused"
                 else "no tile plan: hub graph, aggregation by the chunked segment reduce")
-        info = dict(kernel=f"{name} (persistent, {shape}, two-part fp16 split on 16x16x32 fp16 MFMA, {tail})",
-                    kernel_short=name[:-len("_kernel")],
+        info = dict(kernel=f"update_fk_kernel (persistent, {rows}-row node-aligned tiles, two-part fp16 split on "
+                           f"16x16x32 fp16 MFMA, {tail})", kernel_short="update_fk",
                     numerics="fp32 via scaled two-part fp16 split (3 fp16 MFMA products, fp32 accumulate)",
                     products=3)
     else:

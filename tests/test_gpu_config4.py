@@ -10,6 +10,8 @@ QM9 batch is cut into 8 edge-balanced contiguous shards (shard.edge_balanced_ran
   sub-batch of config 4) against the oracle the same way.
 * the shard's forward is deterministic (bit-identical on a re-run).
 """
+import copy
+
 import pytest
 import torch
 import torch.nn as nn
@@ -50,7 +52,7 @@ def _forward(G, model):
 
     emb, blk = model
     with torch.no_grad():
-        out = blk(emb(G.to(DEV)))
+        out = blk(emb(copy.copy(G).to(DEV)))  # Graph.to moves in place: keep the host graph
         return out, Sum()(out)
 
 

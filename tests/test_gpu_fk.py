@@ -1,6 +1,6 @@
-"""GPU parity of the fp32 layer kernels on the two-part fp16 split: update_fk2_kernel (h <= 384: 64-row
-balanced tile plans, output staged in LDS and stored during the next tile) and the column-chunked
-update_fk_kernel (h > 384), every aggregation variant, the amax chain that scales the split, operands
+"""GPU parity of the fp32 layer kernel on the two-part fp16 split (update_fk_kernel): 128-row balanced
+tile plans (h <= 384, relu layers with a sum aggregation), 64-row plans for the other variants and the
+column-chunked h > 384 path, every aggregation variant, the amax chain that scales the split, operands
 far from unit magnitude, hidden sizes beyond 512 (the reference accepts any hidden_dim,
 chemprop.py:54), and the kernels' row-capacity check.  Oracle: fp64 evaluation of chemprop.py:36-43 / residual.py:27-28 and
 the CPU scatter of the kernel's own H_out (chemprop.py:37-39, :86); fp32 contract FP32_NORM_TOL."""
@@ -51,7 +51,7 @@ def _ref_layer(G, H, S, W, b, residual, act, agg_act, reduce="sum"):
 def test_wide_plan_fused_layer(h, rev_offset, exact_deg):
     """Tiles of the kernel's capacity (plan balanced over the CUs); exact_deg passes the true max
     in-degree, else 32: same H_out, node sums bit-identical to the CPU scatter of the kernel's own
-    H_out (phase B sums each node's rows left to right)."""
+    H_out (the segmented scan sums each node's rows left to right)."""
     K = _K()
     G = _graph("qm9", 300, seed=h, rev_offset=rev_offset)
     E, V = G.num_edges, G.num_nodes
@@ -61,7 +61,7 @@ def test_wide_plan_fused_layer(h, rev_offset, exact_deg):
     W, b = lin.weight.detach(), lin.bias.detach()
     relu = K.act_code(nn.ReLU())
     cap = K.fused_tile_rows(h, torch.float32, relu, "sum", relu)
-    assert cap == 64
+    assert cap == 128
     perm, plan, maxdeg, zf = _layout(G, cap)
     assert max(int(x) for x in (plan[0][1:] - plan[0][:-1]).cpu()) <= cap
     amax_out = torch.zeros(2, device=DEV)
@@ -106,13 +106,13 @@ def test_split_scaling_far_from_unit_magnitude(scale):
 
 @pytest.mark.parametrize("reduce", ["mean", "max", "min"])
 def test_narrow_generic_reduce(reduce):
-    """mean / max / min aggregation (the generic fk2 variant), node values bit-identical to the CPU
+    """mean / max / min aggregation (the generic 64-row variant), node values bit-identical to the CPU
     scatter of the kernel's H_out."""
     K = _K()
     h = 300
     relu = K.act_code(nn.ReLU())
     assert K.fused_tile_rows(h, torch.float32, relu, reduce, relu) == 64
-    assert K.fused_tile_rows(h, torch.float32, relu, "sum", relu) == 64
+    assert K.fused_tile_rows(h, torch.float32, relu, "sum", relu) == 128
     G = _graph("qm9", 90, seed=7)
     E, V = G.num_edges, G.num_nodes
     g = torch.Generator().manual_seed(5)
@@ -196,9 +196,9 @@ def test_block_wide_hidden_gradients():
         assert_parity(m.linear.weight.grad, W64[i].grad, FP32_NORM_TOL, f"dW{i}")
 
 
-def test_engine_uses_balanced_plan_and_amax_chain():
-    """The block at config-2 shape runs fk2 on the balanced 64-row plan (one launch per layer) and
-    matches the oracle; the plan the collate shipped equals the device planner's."""
+def test_engine_uses_wide_plan_and_amax_chain():
+    """The block at config-2 shape runs the 128-row plan (one launch per layer) and matches the
+    oracle; the plan the collate shipped equals the device planner's."""
     from notorch_amd.nn import ChempropBlock
     from notorch_amd.nn.gnn import _engine
 
@@ -206,8 +206,8 @@ def test_engine_uses_balanced_plan_and_amax_chain():
     h = 300
     G = _graph("qm9", 512, seed=4)
     lay = G._nt_layout
-    d_tp, d_n, _ = K.tile_plan(lay.dst_ptr.to(DEV), G.num_edges, lay.deg_range[0], rows=64, ncu=K.PLAN_NCU)
-    assert d_n == lay.plan[1] and torch.equal(d_tp.cpu(), lay.plan[0])
+    d_tp, d_n, _ = K.tile_plan(lay.dst_ptr.to(DEV), G.num_edges, lay.deg_range[0], rows=128, ncu=K.PLAN_NCU)
+    assert d_n == lay.plan_wide[1] and torch.equal(d_tp.cpu(), lay.plan_wide[0])
     torch.manual_seed(0)
     Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
     blk = ChempropBlock(hidden_dim=h, depth=3).eval()
@@ -220,7 +220,7 @@ def test_engine_uses_balanced_plan_and_amax_chain():
             out = blk.to(DEV)(G.update(node_feats=Xv, edge_feats=Xe).to(DEV))
     finally:
         _engine.UPDATE_EVENTS = None
-    assert len(events) == 3 and _engine.LAST_UPDATE_INFO["kernel_short"] == "update_fk2"
+    assert len(events) == 3 and _engine.LAST_UPDATE_INFO["kernel_short"] == "update_fk"
     assert_parity(out.edge_feats, ref_e, FP32_NORM_TOL, "edge")
     assert_parity(out.node_feats, ref_n, FP32_NORM_TOL, "node")
 
@@ -245,7 +245,7 @@ def test_plain_layer_without_aggregation(h):
 
 @pytest.mark.parametrize("agg", ["relu", "identity", "tanh"])
 def test_fused_aggregation_acts(agg):
-    """Aggregation activations: relu / identity (fast fk2 variants) and a generic one (tanh)."""
+    """Aggregation activations: relu / identity (fast variants) and a generic one (tanh)."""
     K = _K()
     h = 300
     acts = {"relu": (nn.ReLU(), torch.relu), "identity": (nn.Identity(), lambda x: x), "tanh": (nn.Tanh(), torch.tanh)}
