@@ -80,6 +80,7 @@ struct Args {
   float* O;
   float* SO;  // NULL: no aggregation
   int nxcd;
+  int stagger;  // diagnostic: start delay of workgroup b = stagger * ((b / nxcd) % 4) x 8k cycles (0)
 };
 
 // power-of-two scale that maps a magnitude bound to < 2^14 (exponent clamped to [-100, 24]);
@@ -489,6 +490,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   }
   if (ntl <= 0) return;
   auto tile = [&](int i) __attribute__((always_inline)) { return t0 + (i < ntl ? i : ntl - 1) * tstride; };
+  for (int q = a.stagger * (((int)blockIdx.x / (nx > 0 ? nx : 1)) & 3); q > 0; --q) __builtin_amdgcn_s_sleep(127);
 
   St st;
   const int tid = threadIdx.x;
@@ -556,58 +558,73 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   }
 #pragma unroll
   for (int j = 0; j < CT; ++j) fk_bias_load(st, a, 0, j);
-  fk_gather<RT, CT, ACT, 0>(st, a, cur.x, cur.y, 0);
-  if constexpr (GD == 2) fk_gather<RT, CT, ACT, 1>(st, a, cur.x, cur.y, 1);  // SPT >= 2
-  fk_load_w<RT, CT, 0>(st, 0, 0);
-  fk_split<RT, CT, ACT, 0, 0>(st, a, 0);
+  auto kcs = [&](int kk, int& cc, int& ss) __attribute__((always_inline)) {  // step in a tile -> chunk, k-step
+    cc = kk / a.KS;
+    ss = kk - cc * a.KS;
+  };
+  {  // steps 0, 1, 2 gathered, W of steps 0 and 1, slice 0 split (the launcher keeps SPT >= 3)
+    int c1, s1;
+    kcs(1, c1, s1);
+    fk_gather<RT, CT, ACT, 0>(st, a, cur.x, cur.y, 0);
+    fk_gather<RT, CT, ACT, 1>(st, a, cur.x, cur.y, 1 % a.KS);
+    fk_load_w<RT, CT, 0>(st, 0, 0);
+    fk_load_w<RT, CT, 1>(st, c1, s1);
+    fk_split<RT, CT, ACT, 0, 0>(st, a, 0);
+    fk_gather<RT, CT, ACT, 0>(st, a, cur.x, cur.y, 2 % a.KS);
+  }
   fk_barrier();
 
-  // ---- main loop: one 32-deep k-step per iteration, two iterations per trip (register parity)
+  // ---- main loop: one 32-deep k-step per iteration, two iterations per trip (register parity P: A
+  // buffer and W fragments of steps g and g + 2, gather slot of steps g + 1 and g + 3).  Every
+  // vector-memory op is unconditional and issued into registers the step has just freed: W two steps
+  // ahead, gathers three steps ahead, both before the epilogue's stores (vmcnt counts loads and
+  // stores in issue order, so the next two steps' waits do not cover the stores).
   int g = 0, i = 0, k = 0;  // global step, tile-local index, step within the tile
   while (g < G) {
 #pragma unroll
     for (int P = 0; P < 2; ++P) {
       if (P == 0 || g < G) {
-        const int c = k / a.KS, s = k - c * a.KS;
-        // (1) W fragments of step g + 1, issued before this step's gathers: the MFMAs of step g wait
-        // (in-order vmcnt) for W(g) only, i.e. for loads issued up to the gathers of step g, and
-        // overlap the flight of step g + 1's gathers
-        const int k1 = k + 1 < SPT ? k + 1 : 0;
-        const int c1 = k1 / a.KS, s1 = k1 - c1 * a.KS;
-        if (P == 0) fk_load_w<RT, CT, 1>(st, c1, s1);
-        else fk_load_w<RT, CT, 0>(st, c1, s1);
-        // (2) stage step g + GD (its register slot was split at step g - 1); every vector-memory
-        // op of a step is unconditional, so the compiler's vmcnt waits count exactly
-        {
-          // the launcher keeps KS >= 2, so step g + GD lies in tile i or i + 1
-          const int k2 = k + GD;
-          const int adv = k2 >= SPT ? 1 : 0;
-          const int s2 = (k2 - adv * SPT) % a.KS;
-          int so = adv == 0 ? cur.x : nxt.x, qo = adv == 0 ? cur.y : nxt.y;
-          if constexpr ((ABL & 1) != 0) so = qo = 0;
-          if (GD == 1 || P == 0) fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s2);
-          else fk_gather<RT, CT, ACT, GD - 1>(st, a, so, qo, s2);
-        }
-        // (3) residual rows (loaded by the previous epilogue) into the accumulators' scale
+        int c, s;
+        kcs(k, c, s);
+        // (1) residual rows (loaded by the previous epilogue) into the accumulators' scale
         if (resid && s == 0) fk_resid_scale(st);
-        // (4) MFMAs of step g
+        // (2) MFMAs of step g
         if constexpr ((ABL & 2) == 0) {
           if (P == 0) fk_mfma<RT, CT, 0>(st, c, (n_cur + 15) >> 4);
           else fk_mfma<RT, CT, 1>(st, c, (n_cur + 15) >> 4);
         }
-        // (5) split step g + 1's staged piece into the other buffer
-        if constexpr ((ABL & 4) == 0) {
-          if (P == 0) fk_split<RT, CT, ACT, GD - 1, 1>(st, a, s1);
-          else fk_split<RT, CT, ACT, 0, 0>(st, a, s1);
+        // (3) W fragments of step g + 2 into the registers step g used
+        {
+          int c2, s2;
+          kcs(k + 2 < SPT ? k + 2 : k + 2 - SPT, c2, s2);
+          if (P == 0) fk_load_w<RT, CT, 0>(st, c2, s2);
+          else fk_load_w<RT, CT, 1>(st, c2, s2);
+        }
+        // (4) split step g + 1's staged piece into the other buffer, then gather step g + 3 into the
+        // freed slot (tile i or i + 1)
+        {
+          const int k1 = k + 1 < SPT ? k + 1 : k + 1 - SPT;
+          const int s1 = k1 - (k1 / a.KS) * a.KS;
+          if constexpr ((ABL & 4) == 0) {
+            if (P == 0) fk_split<RT, CT, ACT, 1, 1>(st, a, s1);
+            else fk_split<RT, CT, ACT, 0, 0>(st, a, s1);
+          }
+          const int k3 = k + 3;
+          const int adv = k3 >= SPT ? 1 : 0;
+          const int s3 = (k3 - adv * SPT) % a.KS;
+          int so = adv == 0 ? cur.x : nxt.x, qo = adv == 0 ? cur.y : nxt.y;
+          if constexpr ((ABL & 1) != 0) so = qo = 0;
+          if (P == 0) fk_gather<RT, CT, ACT, 1>(st, a, so, qo, s3);
+          else fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s3);
         }
         if constexpr ((ABL & 16) == 0) fk_barrier();
-        // (6) epilogue at the chunk's last k-step; it starts the next (tile, chunk)'s residual loads
+        // (5) epilogue at the chunk's last k-step; it starts the next (tile, chunk)'s residual loads
         if ((ABL & 8) == 0 && s == a.KS - 1) {
           const bool last_c = c + 1 == a.nchunks;
           const int i_next = last_c ? (i + 1 < ntl ? i + 1 : i) : i, c_next = last_c ? 0 : c + 1;
           fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
         }
-        // (7) advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
+        // (6) advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
         ++g;
         if (++k == SPT) {
           k = 0;

@@ -879,9 +879,9 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   a.E = u.E;
   a.h = (int)u.h;
   a.hv = (int)(u.h / 4);
-  // at least two k-steps per tile (the kernel's staging runs two steps ahead within one tile's
-  // neighbour); a k-step past the image reads zeros (buffer range) and masked-off pieces
-  a.KS = fk::ks_for(u.h) < 2 ? 2 : fk::ks_for(u.h);
+  // at least three k-steps per tile (update_fk_kernel gathers three steps ahead, within the next
+  // tile at most); a k-step past the image reads zeros (buffer range) and masked-off pieces
+  a.KS = fk::ks_for(u.h) < 3 ? 3 : fk::ks_for(u.h);
   a.NT = fk::nt_for(u.h);
   a.residual = u.residual;
   a.act = u.act;
@@ -894,6 +894,10 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   a.O = u.H_out;
   a.SO = S_out;
   a.nxcd = xcd_count();
+  {
+    const char* e = getenv("NT_FK_STAGGER");  // timing experiments only
+    a.stagger = e ? atoi(e) : 0;
+  }
   a.ntiles = fused ? (int)ntiles : (int)((u.E + cap - 1) / cap);
   if (a.ntiles == 0) return NT_OK;
   const int grid = a.ntiles < cu_count() ? a.ntiles : cu_count();

@@ -69,6 +69,17 @@ def main():
                                  row_table=rt, out=out, S_out=S2)
         return f
 
+    def fk_stagger(n):
+        f0 = fk(128)
+
+        def f():
+            os.environ["NT_FK_STAGGER"] = str(n)
+            try:
+                f0()
+            finally:
+                os.environ["NT_FK_STAGGER"] = "0"
+        return f
+
     def fk_plain():
         K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, amax_in=amax, amax_out=amax_out, out=out)
 
@@ -76,6 +87,9 @@ def main():
         "fk_fused": fk(128),
         "fk_fused64": fk(64),
         "fk_plain": fk_plain,
+        "fk_stagger1": fk_stagger(1),
+        "fk_stagger2": fk_stagger(2),
+        "fk_stagger4": fk_stagger(4),
         "init": lambda: K.dmpnn_init(Xv, H, src, lay.dst_ptr, lay.dst_perm, act=relu, amax=amax_out),
         "absmax": lambda: K.absmax(H, amax_out[0:1]),
         "pack": lambda: K.pack_weights(W),
