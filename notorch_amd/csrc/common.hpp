@@ -122,6 +122,31 @@ __device__ __forceinline__ void atomic_max_nonneg(float* p, float v) {
     atomicMax(reinterpret_cast<unsigned int*>(p), __float_as_uint(v));
 }
 
+// Block-wide max of non-negative values into p[0] (and p[1]): wave shuffles, one LDS slot per wave,
+// one atomic per block.  Every thread of the block must call it (it holds a barrier).
+__device__ __forceinline__ void block_max_to(float* p, float a, float b = 0.f, bool two = false) {
+  __shared__ float sm[2][16];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) {
+    a = fmaxf(a, __shfl_xor(a, o));
+    b = fmaxf(b, __shfl_xor(b, o));
+  }
+  const int w = threadIdx.x >> 6, nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    sm[0][w] = a;
+    sm[1][w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < nw; ++i) {
+      a = fmaxf(a, sm[0][i]);
+      b = fmaxf(b, sm[1][i]);
+    }
+    atomic_max_nonneg(p, a);
+    if (two) atomic_max_nonneg(p + 1, b);
+  }
+}
+
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 inline int grid_for(int64_t work, int block, int cap = 256 * 16) {

@@ -216,17 +216,7 @@ __global__ void __launch_bounds__(LDS ? kLdsThreads : 256, LDS ? 2 : 1) init_emb
     }
     Piece<T, VEC>::store(S + v * h + c, y);
   }
-  if (amax) {  // one atomic max per wave (non-negative floats order like their bits)
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      mh = fmaxf(mh, __shfl_xor(mh, o));
-      ms = fmaxf(ms, __shfl_xor(ms, o));
-    }
-    if ((threadIdx.x & 63) == 0) {
-      atomic_max_nonneg(amax, mh);
-      atomic_max_nonneg(amax + 1, ms);
-    }
-  }
+  if (amax) block_max_to(amax, mh, ms, true);  // one atomic max per block
 }
 
 template <typename T, bool VEC>

@@ -132,17 +132,7 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
       ms = fmaxf(ms, fmaxf(fmaxf(fabsf(sv.x), fabsf(sv.y)), fmaxf(fabsf(sv.z), fabsf(sv.w))));
     }
   }
-  if (amax) {  // one atomic max per wave (non-negative floats order like their bits)
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) {
-      mh = fmaxf(mh, __shfl_xor(mh, o));
-      ms = fmaxf(ms, __shfl_xor(ms, o));
-    }
-    if (lane == 0) {
-      atomic_max_nonneg(amax, mh);
-      atomic_max_nonneg(amax + 1, ms);
-    }
-  }
+  if (amax) block_max_to(amax, mh, ms, true);  // one atomic max per block
 }
 
 template <int R, int ACT>
@@ -270,7 +260,7 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
     if (vec) {
       const int64_t hv = h / 4;
       if (hv >= 32) {  // rows of >= 32 pieces: a wave per node
-        const int grid = grid_for(V * 64, 256, 256 * 32);
+        const int grid = grid_for(V * 64, 256, 256 * 8);  // grid-stride: 32 waves per CU
         NT_DISPATCH_RA(reduce, act,
                        (init_aggregate_wave<R_, A_><<<grid, 256, 0, stream>>>(
                            (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,

@@ -723,8 +723,7 @@ __global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ X
   }
   for (int64_t q = 4 * n4 + blockIdx.x * 256LL + threadIdx.x; q < n; q += (int64_t)gridDim.x * 256)
     m = fmaxf(m, fabsf(X[q]));
-  m = wave_max(m);
-  if ((threadIdx.x & 63) == 0) atomic_max_abs(out, m);
+  block_max_to(out, m);
 }
 
 }  // namespace fk
