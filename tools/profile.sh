@@ -6,7 +6,7 @@ cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
 TAG=${1:-r1}; shift || true
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
-ARGS="--steps 20 --warmup 5 --no-cpu-baseline --no-secondary --no-embedded $*"
+ARGS="--steps 20 --warmup 5 --no-cpu-baseline --no-secondary --no-embedded --no-training $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/trace" -o run -- python3 bench.py $ARGS > "$OUT/trace.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$OUT/fetch" -o run -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -T --output-format csv -d "$OUT/write" -o run -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1

@@ -10,7 +10,7 @@ for W in $WORKLOADS; do
   tools/profile.sh "${TAG}_${W}" --workload "$W" || { echo "profile $W failed"; exit 3; }
   F=$(find "$D/fetch" -name "*counter_collection.csv" | head -1)
   Wr=$(find "$D/write" -name "*counter_collection.csv" | head -1)
-  timeout -k 10 300 python bench.py --workload "$W" --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --no-embedded \
+  timeout -k 10 300 python bench.py --workload "$W" --steps 20 --warmup 5 --no-cpu-baseline --no-secondary --no-embedded --no-training \
     --pmc-csv "$F,$Wr" > "$D/bench.log" 2>&1 || { tail -5 "$D/bench.log"; exit 4; }
   tail -1 "$D/bench.log" | cut -c1-400
 done

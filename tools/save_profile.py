@@ -48,7 +48,12 @@ write = glob.glob(f"{src}/write/*counter_collection.csv")
 if fetch and write:
     from bench import read_pmc_traffic
 
-    kern = os.environ.get("NT_PROFILE_KERNEL", "update_pk")
+    kern = os.environ.get("NT_PROFILE_KERNEL", "")
+    if not kern:  # the bench line's dominant kernel (e.g. update_fk_kernel -> update_fk)
+        for b in sys.argv[3:]:
+            k = json.loads(open(b).read().strip().splitlines()[-1])["roofline"]["kernel"].split()[0]
+            kern = k[: -len("_kernel")] if k.endswith("_kernel") else k
+    kern = kern or "update"
     traffic = read_pmc_traffic(f"{fetch[0]},{write[0]}", kern)
     if traffic is not None:
         commit = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True,
