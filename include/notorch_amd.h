@@ -183,6 +183,14 @@ NT_API int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, int d
                          void* stream);
 
 /*
+ * fp32 only: the part of nt_dmpnn_pack_weight's image that the fp32 layer kernel reads (its
+ * two-part fp16 image and scale), at the same offsets; the other parts of Wp are left untouched.
+ * Enough for nt_dmpnn_update_fused and nt_dmpnn_dense_matmul (the backward packs W^T this way
+ * every step).  Replaces the same call sites as nt_dmpnn_pack_weight (chemprop.py:26,41).
+ */
+NT_API int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h, void* Wp, void* stream);
+
+/*
  * One fused D-MPNN layer (ChempropLayer.forward, chemprop.py:28-43, wrapped by Residual,
  * residual.py:27-28), for every directed edge e:
  *   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b

@@ -574,6 +574,17 @@ extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, i
   return fk_pack((const float*)W, nlayers, h, h * h, (int64_t)per_layer, (char*)Wp + fk_offset(h), stream);
 }
 
+extern "C" int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h, void* Wp, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(nlayers >= 0 && h > 0 && h <= 8192, NT_EINVAL, "bad sizes (1 <= h <= 8192)");
+  if (nlayers == 0) return NT_OK;
+  NT_REQUIRE(W && Wp && aligned16(Wp), NT_EINVAL, "NULL or misaligned pointer");
+  const size_t per_layer = nt_dmpnn_packed_weight_bytes(h, NT_F32);
+  return fk_pack((const float*)W, nlayers, h, h * h, (int64_t)per_layer, (char*)Wp + fk_offset(h),
+                 as_stream(stream_));
+}
+
 extern "C" int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, int agg_act) {
   if (h <= 0) return 0;
   if (dtype == NT_BF16) return 64;

@@ -671,28 +671,36 @@ __global__ void __launch_bounds__(256) row_table_kernel(const int32_t* __restric
 }
 
 // --------------------------------------------------------------------------- packing
-// One thread per 16-B fragment slot: image block ((s NT + ct) 2 + p), lane l holds
-// W[16 ct + (l & 15)][32 s + 8 (l >> 4) + j], j < 8, part p of the scaled two-part fp16 split.
-// Every block first reduces max|W| of its layer (the scale is the same in every block).
+// Two launches: the layer scales, then one thread per 16-B fragment slot: image block
+// ((s NT + ct) 2 + p), lane l holds W[16 ct + (l & 15)][32 s + 8 (l >> 4) + j], j < 8, part p of the
+// scaled two-part fp16 split.
+// s_W of every layer into its image header: one 1024-thread block per layer reduces max|W|
+__global__ void __launch_bounds__(1024) pack_fk_scale_kernel(const float* __restrict__ W, int64_t h,
+                                                             int64_t w_stride, int64_t img_stride,
+                                                             char* __restrict__ img) {
+  const float* Wl = W + blockIdx.x * w_stride;
+  __shared__ float red[16];
+  float m = 0.f;
+  for (int64_t q = threadIdx.x; q < h * h; q += 1024) m = fmaxf(m, fabsf(Wl[q]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int i = 1; i < 16; ++i) m = fmaxf(m, red[i]);
+    *reinterpret_cast<float*>(img + blockIdx.x * img_stride) = ldexpf(1.f, scale_exp(m));
+  }
+}
+
+// fragment slots of every layer (after pack_fk_scale_kernel wrote the layer's s_W)
 __global__ void __launch_bounds__(256) pack_fk_kernel(const float* __restrict__ W, int64_t h, int KS,
                                                       int NT, int64_t w_stride, int64_t img_stride,
                                                       char* __restrict__ img) {
   const int layer = blockIdx.y;
   const float* Wl = W + layer * w_stride;
   char* out = img + layer * img_stride;
-  __shared__ float red[256];
-  float m = 0.f;
-  for (int64_t q = threadIdx.x; q < h * h; q += 256) m = fmaxf(m, fabsf(Wl[q]));
-  red[threadIdx.x] = m;
-  __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if ((int)threadIdx.x < o) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + o]);
-    __syncthreads();
-  }
-  const float sW = ldexpf(1.f, scale_exp(red[0]));
+  const float sW = *reinterpret_cast<const float*>(out);
   const int64_t slots = (int64_t)KS * NT * 2 * 64;
   const int64_t q = blockIdx.x * 256LL + threadIdx.x;
-  if (q == 0) *reinterpret_cast<float*>(out) = sW;
   if (q >= slots) return;
   const int l = (int)(q & 63);
   const int64_t blk = q >> 6;

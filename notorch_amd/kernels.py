@@ -318,10 +318,11 @@ def packed_weight_numel(h: int, dtype: torch.dtype = torch.float32) -> int:
     return _lib.load().nt_dmpnn_packed_weight_bytes(h, _DTYPE_CODES[dtype]) // 4
 
 
-def pack_weights(W: Tensor) -> Tensor:
+def pack_weights(W: Tensor, *, fk_only: bool = False) -> Tensor:
     """Pack one nn.Linear weight [h, h] (or a stack [L, h, h]) into the MFMA fragment image of its
-    dtype (fp32: bf16x3-split images; bf16: one bf16 fragment image).  The image is an opaque
-    float32-typed buffer; its dtype is recorded as ``Wp.nt_dtype``."""
+    dtype (fp32: the two-part fp16 image of the fp32 layer kernel plus the older bf16-split images;
+    bf16: one bf16 fragment image).  The image is an opaque float32-typed buffer.  fk_only (fp32):
+    only the part nt_dmpnn_update_fused / dense_matmul read (nt_dmpnn_pack_weight_fk)."""
     dev = _require_device(W)
     code = _require_feat("weight", W)
     if W.dim() == 2:
@@ -333,7 +334,11 @@ def pack_weights(W: Tensor) -> Tensor:
         raise ValueError(f"ChempropLayer weight must be square, got {tuple(W.shape)}")
     Wp = torch.empty(L, packed_weight_numel(h, W.dtype), dtype=torch.float32, device=dev)
     lib = _lib.load()
-    _run(dev, lib.nt_dmpnn_pack_weight, _ptr(W3), L, h, code, _ptr(Wp), _stream(dev))
+    if fk_only and W.dtype == torch.float32:
+        W3 = W3.contiguous()
+        _run(dev, lib.nt_dmpnn_pack_weight_fk, _ptr(W3), L, h, _ptr(Wp), _stream(dev))
+    else:
+        _run(dev, lib.nt_dmpnn_pack_weight, _ptr(W3), L, h, code, _ptr(Wp), _stream(dev))
     return Wp[0] if W.dim() == 2 else Wp
 
 

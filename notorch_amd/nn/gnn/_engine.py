@@ -632,7 +632,7 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             dbs[l] = Gu.sum(0)
             del A
         if Gu.dtype == torch.float32 and K.fused_supported(V, E, h, Gu.dtype):
-            dA = K.dense_matmul(Gu.contiguous(), K.pack_weights(W.t().contiguous()))  # fp16x3 MFMA
+            dA = K.dense_matmul(Gu.contiguous(), K.pack_weights(W.t().contiguous(), fk_only=True))
         else:
             dA = torch.mm(Gu, W)
         del Gu

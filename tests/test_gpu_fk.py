@@ -268,3 +268,17 @@ def test_fused_aggregation_acts(agg):
     if agg != "tanh":  # device tanh may differ from the CPU's by an ulp
         exact = dmpnn_ref.scatter(fn(Hn.cpu()), G.edge_index[1], V, "sum")
         assert torch.equal(Sn.cpu(), exact), agg
+
+
+def test_pack_fk_only_matches_full_pack():
+    """nt_dmpnn_pack_weight_fk writes the same fk image (scale header + fragments) as the full pack:
+    dense_matmul on either image gives the same bits."""
+    K = _K()
+    g = torch.Generator().manual_seed(3)
+    for h in (36, 300, 640):
+        W = (torch.randn(h, h, generator=g) * 0.05).to(DEV)
+        X = torch.randn(257, h, generator=g).to(DEV)
+        full, fk = K.pack_weights(W), K.pack_weights(W, fk_only=True)
+        a, b = K.dense_matmul(X, full), K.dense_matmul(X, fk)
+        assert torch.equal(a, b), h
+        assert_parity(a, X.double() @ W.double().t(), FP32_NORM_TOL, f"dense h={h}")
