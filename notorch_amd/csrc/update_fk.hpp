@@ -47,7 +47,7 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
-constexpr int kImgHdr = 256;  // image header bytes (float s_W at 0); fragment blocks follow
+constexpr int kImgHdr = 256;  // image header bytes (float s_W at 0, max|W| partials at 1..32); fragments follow
 constexpr int kEmaps = 4;     // row-info buffers (tile index mod 4)
 constexpr int kFlagStart = 1, kFlagEnd = 2;
 
@@ -674,31 +674,39 @@ __global__ void __launch_bounds__(256) row_table_kernel(const int32_t* __restric
 // Two launches: the layer scales, then one thread per 16-B fragment slot: image block
 // ((s NT + ct) 2 + p), lane l holds W[16 ct + (l & 15)][32 s + 8 (l >> 4) + j], j < 8, part p of the
 // scaled two-part fp16 split.
-// s_W of every layer into its image header: one 1024-thread block per layer reduces max|W|
-__global__ void __launch_bounds__(1024) pack_fk_scale_kernel(const float* __restrict__ W, int64_t h,
-                                                             int64_t w_stride, int64_t img_stride,
-                                                             char* __restrict__ img) {
-  const float* Wl = W + blockIdx.x * w_stride;
-  __shared__ float red[16];
+// max|W| of every layer in kScaleParts partial maxima (header floats 1 .. kScaleParts): grid
+// (kScaleParts, layers) of 256-thread blocks, each over a 1/kScaleParts slice of the layer
+constexpr int kScaleParts = 32;
+__global__ void __launch_bounds__(256) pack_fk_scale_kernel(const float* __restrict__ W, int64_t h,
+                                                            int64_t w_stride, int64_t img_stride,
+                                                            char* __restrict__ img) {
+  const float* Wl = W + blockIdx.y * w_stride;
+  const int64_t n = h * h, per = (n + kScaleParts - 1) / kScaleParts;
+  const int64_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  __shared__ float red[4];
   float m = 0.f;
-  for (int64_t q = threadIdx.x; q < h * h; q += 1024) m = fmaxf(m, fabsf(Wl[q]));
+  for (int64_t q = lo + threadIdx.x; q < hi; q += 256) m = fmaxf(m, fabsf(Wl[q]));
   m = wave_max(m);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int i = 1; i < 16; ++i) m = fmaxf(m, red[i]);
-    *reinterpret_cast<float*>(img + blockIdx.x * img_stride) = ldexpf(1.f, scale_exp(m));
-  }
+  if (threadIdx.x == 0)
+    reinterpret_cast<float*>(img + blockIdx.y * img_stride)[1 + blockIdx.x] =
+        fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
 }
 
-// fragment slots of every layer (after pack_fk_scale_kernel wrote the layer's s_W)
+// fragment slots of every layer (after pack_fk_scale_kernel wrote the layer's partial maxima); block 0
+// stores s_W in the header
 __global__ void __launch_bounds__(256) pack_fk_kernel(const float* __restrict__ W, int64_t h, int KS,
                                                       int NT, int64_t w_stride, int64_t img_stride,
                                                       char* __restrict__ img) {
   const int layer = blockIdx.y;
   const float* Wl = W + layer * w_stride;
   char* out = img + layer * img_stride;
-  const float sW = *reinterpret_cast<const float*>(out);
+  float mw = 0.f;
+#pragma unroll
+  for (int i = 1; i <= kScaleParts; ++i) mw = fmaxf(mw, reinterpret_cast<const float*>(out)[i]);
+  const float sW = ldexpf(1.f, scale_exp(mw));
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<float*>(out) = sW;
   const int64_t slots = (int64_t)KS * NT * 2 * 64;
   const int64_t q = blockIdx.x * 256LL + threadIdx.x;
   if (q >= slots) return;

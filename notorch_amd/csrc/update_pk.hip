@@ -925,7 +925,8 @@ int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_
             hipStream_t stream) {
   const int KS = fk::ks_for(h), NT = fk::nt_for(h);
   const int64_t slots = (int64_t)KS * NT * 2 * 64;
-  fk::pack_fk_scale_kernel<<<(unsigned)nlayers, 1024, 0, stream>>>(W, h, w_stride, img_stride, (char*)img);
+  fk::pack_fk_scale_kernel<<<dim3(fk::kScaleParts, (unsigned)nlayers), 256, 0, stream>>>(W, h, w_stride, img_stride,
+                                                                                         (char*)img);
   NT_LAUNCH_CHECK();
   dim3 grid((unsigned)((slots + 255) / 256), (unsigned)nlayers);
   fk::pack_fk_kernel<<<grid, 256, 0, stream>>>(W, h, KS, NT, w_stride, img_stride, (char*)img);

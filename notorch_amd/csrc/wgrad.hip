@@ -227,12 +227,230 @@ __global__ void __launch_bounds__(256) wgrad_kernel(WgArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// wgrad_wide_kernel (h <= 320, gathered A): one 512-thread workgroup computes dW[:, j0:j0+128] of
+// an edge chunk, i.e. every output row (all of G's columns) against a 128-column block of A, so the
+// chunk's G rows are read by ceil(h / 128) workgroups instead of 25 and A's by one (5h floats per
+// edge from L2 instead of 16h).  Per 32-edge step the workgroup stages G[32][NI * 16] and
+// A[32][128] (three bf16 parts each, [part][edge group][column] 16-B runs, as wgrad_kernel); wave w
+// owns i-tiles 5 (w % 4) .. +5 and j-tiles 4 (w / 4) .. +4 (20 accumulators).
+constexpr int kWI = 320;            // max rows (G columns) of the wide kernel
+constexpr int kWJ = 128;            // A columns per workgroup
+constexpr int kWGPart = 4 * kWI * 16;   // one bf16 part of the G slab
+constexpr int kWAPart = 4 * kWJ * 16;   // one bf16 part of the A slab
+constexpr int kWLds = 3 * (kWGPart + kWAPart);  // 84 KiB
+
+struct WwArgs {
+  const float* G;
+  const float* H;
+  const float* S;
+  const int64_t* src;
+  const int64_t* rev;
+  int64_t E, h;
+  int jblocks, ksplit, chunk_steps, xcds;
+  float alpha;
+  int act;
+  float* part;     // [ksplit][h][h]
+  float* part_db;  // [ksplit][h] or NULL
+};
+
+template <int ACT>
+__global__ void __launch_bounds__(512, 1) wgrad_wide_kernel(WwArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int nb = gridDim.x;
+  int w = blockIdx.x;
+  if (a.xcds > 1 && nb % a.xcds == 0) w = (w % a.xcds) * (nb / a.xcds) + w / a.xcds;
+  const int y = w / a.jblocks, jb = w - y * a.jblocks;
+  const int64_t h = a.h, j0 = (int64_t)jb * kWJ;
+  const int64_t e_beg = (int64_t)y * a.chunk_steps * kK;
+  const int64_t e_end0 = e_beg + (int64_t)a.chunk_steps * kK;
+  const int64_t e_end = e_end0 < a.E ? e_end0 : a.E;
+  const int nsteps = e_end > e_beg ? (int)((e_end - e_beg + kK - 1) / kK) : 0;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int ni16 = (int)((h + 15) / 16) * 16;  // G columns staged (multiple of 16, <= 320)
+  const bool want_db = a.part_db != nullptr && jb == 0;
+
+  // staging items: G (column cg, group gg) for q = t + 512 m < 4 ni16; A (column ca, group ga) = t
+  int cg[3], gg[3];
+  bool okg[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int q = t + 512 * m;
+    okg[m] = q < 4 * ni16;
+    const int qq = okg[m] ? q : 0;
+    gg[m] = qq / ni16;
+    cg[m] = qq - gg[m] * ni16;
+  }
+  const int ca = t & (kWJ - 1), ga = t >> 7;  // 128 columns x 4 groups = 512
+  const int64_t jc = j0 + ca < h ? j0 + ca : 0;
+  const unsigned mj = j0 + ca < h ? ~0u : 0u;
+  float dbacc[3] = {0.f, 0.f, 0.f};
+
+  // (src, rev) of the wave's 8 A edges (every wave's items share one edge group), fetched a step
+  // ahead as one vector load (lane r: src of edge r, lane 8 + r: its rev) and broadcast with readlane,
+  // so no index round trip sits in front of the row gathers
+  auto load_idx = [&](int s) __attribute__((always_inline)) -> int {
+    int64_t e = e_beg + (int64_t)s * kK + 8 * ga + (lane & 7);
+    e = e < e_end ? e : e_end - 1;
+    return lane >= 16 ? 0 : (int)(lane < 8 ? a.src[e] : a.rev[e]);
+  };
+  float xg[3][8], xs[8], xh[8];
+  int64_t eb_cur = 0;
+  auto load = [&](int s, int idxv) __attribute__((always_inline)) {
+    const int64_t eb = e_beg + (int64_t)s * kK;
+    eb_cur = eb;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int64_t col = cg[m] < h ? cg[m] : 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        int64_t e = eb + 8 * gg[m] + r;
+        e = e < e_end ? e : e_end - 1;
+        xg[m][r] = a.G[e * h + col];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int64_t se = __builtin_amdgcn_readlane(idxv, r), re = __builtin_amdgcn_readlane(idxv, 8 + r);
+      xs[r] = a.S[se * h + jc];
+      xh[r] = a.H[re * h + jc];
+    }
+  };
+  auto store = [&]() __attribute__((always_inline)) {
+    char* gbase = lds;
+    char* abase = lds + 3 * kWGPart;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      float gv[8];
+      const unsigned mc = (okg[m] && cg[m] < h) ? ~0u : 0u;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const unsigned ok = eb_cur + 8 * gg[m] + r < e_end ? ~0u : 0u;
+        gv[r] = __uint_as_float(__float_as_uint(xg[m][r]) & (ok & mc));
+      }
+      if (want_db) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) dbacc[m] += gv[r];
+      }
+      if (okg[m]) {
+        bf16x8 p0, p1, p2;
+        split3(gv, p0, p1, p2);
+        const int off = (gg[m] * kWI + cg[m]) * 16;
+        *reinterpret_cast<bf16x8*>(gbase + off) = p0;
+        *reinterpret_cast<bf16x8*>(gbase + kWGPart + off) = p1;
+        *reinterpret_cast<bf16x8*>(gbase + 2 * kWGPart + off) = p2;
+      }
+    }
+    float av[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const unsigned ok = eb_cur + 8 * ga + r < e_end ? ~0u : 0u;
+      const float v = xs[r] - act_t<ACT>(xh[r], a.act, a.alpha);
+      av[r] = __uint_as_float(__float_as_uint(v) & (ok & mj));
+    }
+    bf16x8 p0, p1, p2;
+    split3(av, p0, p1, p2);
+    const int off = (ga * kWJ + ca) * 16;
+    *reinterpret_cast<bf16x8*>(abase + off) = p0;
+    *reinterpret_cast<bf16x8*>(abase + kWAPart + off) = p1;
+    *reinterpret_cast<bf16x8*>(abase + 2 * kWAPart + off) = p2;
+  };
+
+  const int fr = lane & 15, g16 = lane >> 4;
+  const int wi = wave & 3, wj = wave >> 2;  // i-tiles 5 wi .. 5 wi + 4, j-tiles 4 wj .. 4 wj + 3
+  f32x4 acc[5][4];
+#pragma unroll
+  for (int x = 0; x < 5; ++x)
+#pragma unroll
+    for (int z = 0; z < 4; ++z) acc[x][z] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool iact = 16 * 5 * wi < ni16;  // waves whose i-tiles are all past h skip the MFMAs
+
+  int idx_next = 0;
+  if (nsteps > 0) {
+    load(0, load_idx(0));
+    if (nsteps > 1) idx_next = load_idx(1);
+    store();
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps;
+    if (more) {
+      load(s + 1, idx_next);
+      if (s + 2 < nsteps) idx_next = load_idx(s + 2);
+    }
+    if (iact) {
+      const char* gb = lds;
+      const char* ab = lds + 3 * kWGPart;
+      bf16x8 fb[4][3];
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int off_b = (g16 * kWJ + 16 * (4 * wj + z) + fr) * 16;
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fb[z][p] = *reinterpret_cast<const bf16x8*>(ab + p * kWAPart + off_b);
+      }
+#pragma unroll
+      for (int x = 0; x < 5; ++x) {
+        const int off_a = (g16 * kWI + 16 * (5 * wi + x) + fr) * 16;
+        bf16x8 fa[3];
+#pragma unroll
+        for (int p = 0; p < 3; ++p) fa[p] = *reinterpret_cast<const bf16x8*>(gb + p * kWGPart + off_a);
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          f32x4 cc = acc[x][z];
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[z][2], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[z][1], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[2], fb[z][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[z][1], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[1], fb[z][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[0], fb[z][0], cc, 0, 0, 0);
+          acc[x][z] = cc;
+        }
+      }
+    }
+    if (more) {
+      __syncthreads();  // every wave has read the slab
+      store();
+    }
+    __syncthreads();
+  }
+
+  float* P = a.part + (int64_t)y * h * h;
+#pragma unroll
+  for (int x = 0; x < 5; ++x)
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+      const int64_t col = j0 + 16 * (4 * wj + z) + fr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = 16 * (5 * wi + x) + 4 * g16 + q;
+        if (row < h && col < h) P[row * h + col] = acc[x][z][q];
+      }
+    }
+  if (want_db) {  // fixed-order column sums over the 4 edge groups (deterministic)
+    float* red = reinterpret_cast<float*>(lds);  // the slabs are dead after the last barrier
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+      if (okg[m]) red[gg[m] * kWI + cg[m]] = dbacc[m];
+    __syncthreads();
+    if (t < h) a.part_db[(int64_t)y * h + t] = ((red[t] + red[kWI + t]) + red[2 * kWI + t]) + red[3 * kWI + t];
+  }
+}
+
 // out[i] = sum_y part[y][i] in ascending y (fixed order: deterministic)
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int64_t n,
                                                            int ksplit, float* __restrict__ out) {
   for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
     float s = 0.f;
-    for (int y = 0; y < ksplit; ++y) s += part[(int64_t)y * n + i];
+    int y = 0;
+    for (; y + 8 <= ksplit; y += 8) {  // 8 loads in flight, summed in ascending y
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(y + u) * n + i];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; y < ksplit; ++y) s += part[(int64_t)y * n + i];
     out[i] = s;
   }
 }
@@ -258,6 +476,25 @@ Plan make_plan(int64_t E, int64_t h) {
   return p;
 }
 
+struct WPlan {
+  int ksplit, chunk_steps;
+};
+
+// one workgroup per CU: ksplit = CUs / jblocks chunks of the edge range
+WPlan make_wide_plan(int64_t E, int64_t h) {
+  WPlan p;
+  const int jblocks = (int)((h + kWJ - 1) / kWJ);
+  const int64_t steps = (E + kK - 1) / kK;
+  int64_t ks = (cu_count() > 0 ? cu_count() : 256) / jblocks;
+  if (ks < 1) ks = 1;
+  if (ks > steps) ks = steps > 0 ? steps : 1;
+  p.chunk_steps = (int)((steps + ks - 1) / ks);
+  if (p.chunk_steps < 1) p.chunk_steps = 1;
+  p.ksplit = (int)((steps + p.chunk_steps - 1) / p.chunk_steps);
+  if (p.ksplit < 1) p.ksplit = 1;
+  return p;
+}
+
 }  // namespace
 
 int xcd_count();  // csrc/update_ps.hip: the current device's XCD count, queried once per device
@@ -266,7 +503,9 @@ int xcd_count();  // csrc/update_ps.hip: the current device's XCD count, queried
 extern "C" int64_t nt_dmpnn_weight_grad_workspace(int64_t E, int64_t h) {
   if (E < 0 || h <= 0) return -1;
   const nt::Plan p = nt::make_plan(E, h);
-  return (int64_t)p.ksplit * (h * h + h) * (int64_t)sizeof(float);
+  const nt::WPlan q = nt::make_wide_plan(E, h);
+  const int64_t ks = p.ksplit > q.ksplit ? p.ksplit : q.ksplit;  // either kernel fits
+  return ks * (h * h + h) * (int64_t)sizeof(float);
 }
 
 extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S, const int64_t* src,
@@ -291,8 +530,8 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
   }
   NT_REQUIRE(G && S && (src == nullptr || H), NT_EINVAL, "NULL pointer");
   const Plan p = make_plan(E, h);
-  NT_REQUIRE(workspace && workspace_bytes >= (int64_t)p.ksplit * (h * h + h) * (int64_t)sizeof(float),
-             NT_EINVAL, "workspace too small (nt_dmpnn_weight_grad_workspace)");
+  NT_REQUIRE(workspace && workspace_bytes >= nt_dmpnn_weight_grad_workspace(E, h), NT_EINVAL,
+             "workspace too small (nt_dmpnn_weight_grad_workspace)");
   WgArgs a;
   a.G = (const float*)G;
   a.H = (const float*)H;
@@ -309,6 +548,41 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
   a.act = act;
   a.part = (float*)workspace;
   a.part_db = db_out ? a.part + (int64_t)p.ksplit * h * h : nullptr;
+  if (src && h <= kWI) {  // the wide kernel: 128-column blocks of A against all of G
+    const int jblocks = (int)((h + kWJ - 1) / kWJ);
+    const WPlan q = make_wide_plan(E, h);
+    WwArgs b;
+    b.G = (const float*)G;
+    b.H = (const float*)H;
+    b.S = (const float*)S;
+    b.src = src;
+    b.rev = rev;
+    b.E = E;
+    b.h = h;
+    b.jblocks = jblocks;
+    b.ksplit = q.ksplit;
+    b.chunk_steps = q.chunk_steps;
+    b.xcds = xcd_count();
+    b.alpha = act_alpha;
+    b.act = act;
+    b.part = (float*)workspace;
+    b.part_db = db_out ? b.part + (int64_t)q.ksplit * h * h : nullptr;
+    const int grid = jblocks * q.ksplit;
+    if (act == NT_ACT_IDENTITY)
+      wgrad_wide_kernel<NT_ACT_IDENTITY><<<grid, 512, kWLds, stream>>>(b);
+    else if (act == NT_ACT_RELU)
+      wgrad_wide_kernel<NT_ACT_RELU><<<grid, 512, kWLds, stream>>>(b);
+    else
+      wgrad_wide_kernel<-1><<<grid, 512, kWLds, stream>>>(b);
+    NT_LAUNCH_CHECK();
+    wgrad_reduce_kernel<<<grid_for(h * h, 256, 256 * 8), 256, 0, stream>>>(b.part, h * h, q.ksplit, (float*)dW_out);
+    NT_LAUNCH_CHECK();
+    if (db_out) {
+      wgrad_reduce_kernel<<<grid_for(h, 256, 64), 256, 0, stream>>>(b.part_db, h, q.ksplit, (float*)db_out);
+      NT_LAUNCH_CHECK();
+    }
+    return NT_OK;
+  }
   const int grid = p.tiles * p.ksplit;
   const size_t lds = kBufs * 2 * kSlabB;
   if (!src)
