@@ -220,6 +220,38 @@ NT_API int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, int6
                               int32_t* tile_ptr, int64_t ntiles, int32_t* dst_sorted, void* stream);
 
 /*
+ * nt_dmpnn_tile_plan for graphs with hub nodes (in-degree > hub_degree, e.g. polymer hubs,
+ * BASELINE config 5): the same plan, except that a target k * stride inside a hub's in-edges cuts
+ * the tile there instead of rounding up to the next node.  stride = nt_dmpnn_tile_stride with
+ * max_in_degree = the largest in-degree among the non-hub nodes (<= hub_degree <= 32).  The fused
+ * layer then takes the row table marked by nt_dmpnn_mark_hub_rows and leaves the hubs' S_out rows
+ * to nt_dmpnn_hub_aggregate.  Replaces the segmentation of scatter(..., dest) (chemprop.py:39, :86)
+ * for the hub nodes.  nt_dmpnn_tile_plan = this with hub_degree = INT32_MAX.
+ */
+NT_API int nt_dmpnn_tile_plan_hubs(const int32_t* dst_ptr, int64_t V, int64_t E, int64_t stride,
+                                   int hub_degree, int32_t* tile_ptr, int64_t ntiles, int32_t* dst_sorted,
+                                   void* stream);
+
+/*
+ * Marks the hub rows of a row table (nt_dmpnn_row_table) in place: every dst-sorted position whose
+ * node has more than hub_degree in-edges (dst_ptr: the dst CSR) becomes a segment start without a
+ * segment end, so nt_dmpnn_update_fused stores those rows' H_out but none of the hub's S_out.
+ */
+NT_API int nt_dmpnn_mark_hub_rows(void* row_table, int64_t E, const int32_t* dst_ptr, int64_t V,
+                                  int hub_degree, void* stream);
+
+/*
+ * The hubs' share of a fused layer's aggregation (chemprop.py:37-39, :86; torch_scatter semantics):
+ *   out[v] = reduce_{p in [seg_ptr[v], seg_ptr[v+1])} act(X[perm[p]])   for v in hubs[0 .. nhub)
+ * (rows of other nodes untouched).  amax_out (may be NULL): one device float raised to max|out[v]|
+ * (the fused layer's max|S_out| slot).  fp32, h % 4 == 0, 16-byte aligned X / out; deterministic
+ * (eight contiguous row ranges per hub, combined in order).
+ */
+NT_API int nt_dmpnn_hub_aggregate(const void* X, const int32_t* perm, const int32_t* seg_ptr,
+                                  const int32_t* hubs, int64_t nhub, int64_t h, int reduce, int act,
+                                  float act_alpha, int dtype, float* amax_out, void* out, void* stream);
+
+/*
  * Row capacity of one nt_dmpnn_update_fused tile for a layer of hidden size h, activation act and
  * aggregation (reduce, agg_act): the plan passed with that layer must have tiles of at most this
  * many rows.  fp32: 128 for h <= 384 with act = relu, reduce = sum and agg_act in {relu,

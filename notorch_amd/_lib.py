@@ -81,6 +81,11 @@ SIGNATURES: dict[str, tuple] = {
     "nt_dmpnn_tile_stride": (_c_i64, [_c_i64, _c_int, _c_int, _c_int]),
     "nt_dmpnn_tile_count": (_c_i64, [_c_i64, _c_i64]),
     "nt_dmpnn_tile_plan": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _vp, _c_i64, _vp, _vp]),
+    "nt_dmpnn_tile_plan_hubs": (_c_int, [_vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _c_i64, _vp, _vp]),
+    "nt_dmpnn_mark_hub_rows": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_int, _vp]),
+    "nt_dmpnn_hub_aggregate": (
+        _c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp],
+    ),
     "nt_dmpnn_fused_tile_rows": (_c_int, [_c_i64, _c_int, _c_int, _c_int, _c_int]),
     "nt_dmpnn_update_fused": (
         _c_int,

@@ -521,23 +521,27 @@ __global__ void __launch_bounds__(kThreads, 1) update_ps_kernel(Args a) {
 
 namespace {
 
-// tile_ptr[k] = dst_ptr[first v with dst_ptr[v] >= k L], k < ntiles; tile_ptr[ntiles] = E.
+// tile_ptr[k] = dst_ptr[first v with dst_ptr[v] >= k L], k < ntiles; tile_ptr[ntiles] = E: the
+// target k L rounded up to the next node start, except inside a hub (a node with more than
+// hub_degree in-edges), where the tile is cut at k L itself.
 __global__ void tile_plan_kernel(const int32_t* __restrict__ dst_ptr, int64_t V, int64_t E, int L,
-                                 int ntiles, int32_t* __restrict__ tile_ptr) {
+                                 int ntiles, int hub_degree, int32_t* __restrict__ tile_ptr) {
   const int k = blockIdx.x * blockDim.x + threadIdx.x;
   if (k > ntiles) return;
   if (k == ntiles) {
     tile_ptr[k] = (int32_t)E;
     return;
   }
-  const int64_t target = (int64_t)k * L;
-  int64_t lo = 0, hi = V;  // first v in [0, V] with dst_ptr[v] >= target
+  const int64_t target = (int64_t)k * L;  // < E
+  int64_t lo = 0, hi = V;  // first v in [0, V] with dst_ptr[v] > target (exists: dst_ptr[V] = E)
   while (lo < hi) {
     const int64_t mid = (lo + hi) >> 1;
-    if (dst_ptr[mid] >= target) hi = mid;
+    if (dst_ptr[mid] > target) hi = mid;
     else lo = mid + 1;
   }
-  tile_ptr[k] = dst_ptr[lo];
+  const int64_t v = lo - 1;  // the node whose in-edges hold position target
+  const int32_t b = dst_ptr[v], e = dst_ptr[v + 1];
+  tile_ptr[k] = (b == target || e - b > hub_degree) ? (int32_t)target : e;
 }
 
 // dsts[p] = v for every position p in [dst_ptr[v], dst_ptr[v+1])
@@ -639,25 +643,32 @@ extern "C" int64_t nt_dmpnn_tile_count(int64_t E, int64_t stride) {
   return (E + stride - 1) / stride;
 }
 
-extern "C" int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, int64_t stride,
-                                  int32_t* tile_ptr, int64_t ntiles, int32_t* dst_sorted,
-                                  void* stream_) {
+extern "C" int nt_dmpnn_tile_plan_hubs(const int32_t* dst_ptr, int64_t V, int64_t E, int64_t stride,
+                                       int hub_degree, int32_t* tile_ptr, int64_t ntiles,
+                                       int32_t* dst_sorted, void* stream_) {
   using namespace nt;
   clear_error();
+  NT_REQUIRE(hub_degree >= 1, NT_EINVAL, "hub_degree must be >= 1");
   NT_REQUIRE(V >= 0 && E >= 0 && E < (int64_t(1) << 31), NT_EINVAL, "bad sizes");
   NT_REQUIRE(E == 0 || (stride >= 1 && stride < (int64_t(1) << 30)), NT_EINVAL, "bad stride");
   NT_REQUIRE(ntiles == nt_dmpnn_tile_count(E, stride), NT_EINVAL,
              "ntiles != nt_dmpnn_tile_count(E, stride)");
   NT_REQUIRE(dst_ptr && tile_ptr && (E == 0 || dst_sorted), NT_EINVAL, "NULL pointer");
   hipStream_t stream = as_stream(stream_);
-  tile_plan_kernel<<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, stream>>>(dst_ptr, V, E, (int)stride,
-                                                                            (int)ntiles, tile_ptr);
+  tile_plan_kernel<<<(unsigned)((ntiles + 1 + 255) / 256), 256, 0, stream>>>(
+      dst_ptr, V, E, (int)stride, (int)ntiles, hub_degree, tile_ptr);
   NT_LAUNCH_CHECK();
   if (E > 0 && V > 0) {
     dst_sorted_kernel<<<grid_for(V, 256), 256, 0, stream>>>(dst_ptr, V, dst_sorted);
     NT_LAUNCH_CHECK();
   }
   return NT_OK;
+}
+
+extern "C" int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, int64_t stride,
+                                  int32_t* tile_ptr, int64_t ntiles, int32_t* dst_sorted,
+                                  void* stream_) {
+  return nt_dmpnn_tile_plan_hubs(dst_ptr, V, E, stride, INT32_MAX, tile_ptr, ntiles, dst_sorted, stream_);
 }
 
 namespace nt {

@@ -77,6 +77,9 @@ class DeviceLayout:
     dst_chunks: object = None
     mol_chunks: object = None
     type_src: object = None  # (weakref node_feats, weakref edge_feats) type_range was taken from
+    # hub nodes of the dst CSR (in-degree > MAX_FUSED_IN_DEGREE): (hub ids int32, count, largest
+    # non-hub in-degree), False when there are none; the fp32 fused plans then cut hubs at the stride
+    hubs: object = None
 
     def __getstate__(self):
         # weak references do not pickle (DataLoader workers ship collated graphs): mark the type
@@ -89,7 +92,8 @@ class DeviceLayout:
     def tensors(self) -> list:
         """Every tensor the layout owns (CSR arrays, plans, chunk plans)."""
         out = [t for t in (self.dst_ptr, self.dst_perm, self.mol_ptr, self.mol_perm) if t is not None]
-        for p in (self.plan, self.plan_wide, self.dst_chunks, self.mol_chunks[1] if self.mol_chunks else None):
+        for p in (self.plan, self.plan_wide, self.dst_chunks, self.mol_chunks[1] if self.mol_chunks else None,
+                  self.hubs):
             if p:
                 out += [x for x in p if isinstance(x, Tensor)]
         return out
@@ -116,6 +120,7 @@ class DeviceLayout:
         new.plan_wide = mv_plan(self.plan_wide)
         new.deg_range, new.mol_max, new.type_range = self.deg_range, self.mol_max, self.type_range
         new.dst_chunks = mv_plan(self.dst_chunks)
+        new.hubs = mv_plan(self.hubs)
         if self.mol_chunks is not None and new.mol_ptr is not None:
             new.mol_chunks = (new.mol_ptr, mv_plan(self.mol_chunks[1]))
         return new
@@ -515,7 +520,8 @@ def host_layout(
 
 
 # ---- host-side plans (numpy restatements of the device planners; same arrays, no device sync) ----
-MAX_FUSED_IN_DEGREE = 32  # nt_dmpnn_tile_plan's limit (larger in-degrees take the unfused path)
+MAX_FUSED_IN_DEGREE = 32  # nt_dmpnn_tile_plan's limit; nodes with more in-edges are hubs (fp32: cut at the
+# stride by nt_dmpnn_tile_plan_hubs and aggregated by nt_dmpnn_hub_aggregate; bf16: the unfused path)
 LONG_SEGMENT = 64  # segments longer than this aggregate through the chunked reduce
 CHUNK_ROWS = 32  # rows per chunk of nt_segment_reduce_chunked
 
@@ -536,23 +542,32 @@ def host_tile_stride(E: int, max_in_degree: int, rows: int, ncu: int) -> int:
     return max(1, min(L, lmax))
 
 
-def host_tile_ptr(dst_ptr: np.ndarray, E: int, stride: int) -> tuple:
+def host_tile_ptr(dst_ptr: np.ndarray, E: int, stride: int, hub_degree: int = 0) -> tuple:
     """(tile_ptr[ntiles+1], ntiles) as nt_dmpnn_tile_plan builds them: tile k starts at
-    dst_ptr[first v with dst_ptr[v] >= k stride]."""
+    dst_ptr[first v with dst_ptr[v] >= k stride]; with hub_degree > 0 as nt_dmpnn_tile_plan_hubs
+    (a target inside a node with more in-edges is kept as the cut)."""
     ntiles = (E + stride - 1) // stride if E > 0 else 0
     tile_ptr = np.empty(ntiles + 1, dtype=np.int32)
     if ntiles:
-        v = np.searchsorted(dst_ptr, np.arange(ntiles, dtype=np.int64) * stride, side="left")
-        tile_ptr[:ntiles] = dst_ptr[v]
+        t = np.arange(ntiles, dtype=np.int64) * stride
+        if hub_degree > 0:
+            v = np.searchsorted(dst_ptr, t, side="right") - 1  # the node holding position t
+            b, e = dst_ptr[v].astype(np.int64), dst_ptr[v + 1].astype(np.int64)
+            tile_ptr[:ntiles] = np.where((b == t) | (e - b > hub_degree), t, e)
+        else:
+            v = np.searchsorted(dst_ptr, t, side="left")
+            tile_ptr[:ntiles] = dst_ptr[v]
     tile_ptr[ntiles] = E
     return torch.from_numpy(tile_ptr), ntiles
 
 
-def host_tile_plan(dst_ptr: np.ndarray, E: int, max_in_degree: int, rows: int = 64, ncu: int = 0):
-    """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) exactly as nt_dmpnn_tile_plan builds them with the
-    stride of nt_dmpnn_tile_stride(E, max_in_degree, rows, ncu)."""
+def host_tile_plan(dst_ptr: np.ndarray, E: int, max_in_degree: int, rows: int = 64, ncu: int = 0,
+                   hub_degree: int = 0):
+    """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) exactly as nt_dmpnn_tile_plan (hub_degree > 0:
+    nt_dmpnn_tile_plan_hubs) builds them with the stride of nt_dmpnn_tile_stride(E, max_in_degree,
+    rows, ncu)."""
     stride = host_tile_stride(E, max_in_degree, rows, ncu) if E > 0 else 1
-    tile_ptr, ntiles = host_tile_ptr(dst_ptr, E, stride)
+    tile_ptr, ntiles = host_tile_ptr(dst_ptr, E, stride, hub_degree)
     counts = np.diff(dst_ptr.astype(np.int64))
     dsts = np.repeat(np.arange(len(counts), dtype=np.int32), counts)
     return tile_ptr, ntiles, torch.from_numpy(dsts)
@@ -581,14 +596,19 @@ def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional
     lay.deg_range = (int(deg.max()), int(deg.min())) if deg.size else (0, 0)
     V = len(deg)
     maxdeg, mindeg = lay.deg_range
-    if E > 0 and V > 0 and maxdeg <= MAX_FUSED_IN_DEGREE:
-        tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg, rows=64, ncu=PLAN_NCU)
+    hub = 0
+    lay.hubs = False
+    if E > 0 and V > 0 and maxdeg > MAX_FUSED_IN_DEGREE:  # hubs: cut at the stride (fp32 plans)
+        is_hub = deg > MAX_FUSED_IN_DEGREE
+        ids = np.nonzero(is_hub)[0].astype(np.int32)
+        rest = deg[~is_hub]
+        lay.hubs = (torch.from_numpy(ids), int(ids.size), int(rest.max()) if rest.size else 0)
+        hub, maxdeg = MAX_FUSED_IN_DEGREE, lay.hubs[2]
+    if E > 0 and V > 0:
+        tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg, rows=64, ncu=PLAN_NCU, hub_degree=hub)
         lay.plan = (tile_ptr, ntiles, dsts, mindeg == 0)
-        lay.plan_wide = host_tile_ptr(dst_ptr, E, host_tile_stride(E, maxdeg, WIDE_TILE_ROWS, PLAN_NCU))
-    elif E > 0 and V > 0:
-        lay.plan = False
-        lay.plan_wide = False
-    lay.dst_chunks = host_chunk_plan(dst_ptr) if maxdeg > LONG_SEGMENT else False
+        lay.plan_wide = host_tile_ptr(dst_ptr, E, host_tile_stride(E, maxdeg, WIDE_TILE_ROWS, PLAN_NCU), hub)
+    lay.dst_chunks = host_chunk_plan(dst_ptr) if lay.deg_range[0] > LONG_SEGMENT else False
     if mol_ptr is not None:
         n = np.diff(mol_ptr.astype(np.int64))
         lay.mol_max = int(n.max()) if n.size else 0

@@ -406,10 +406,12 @@ def tile_stride(E: int, max_in_degree: int, rows: int, ncu: int = PLAN_NCU) -> i
 
 
 def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int, rows: int = 64,
-              ncu: int = 0) -> tuple[Tensor, int, Tensor]:
+              ncu: int = 0, hub_degree: int = 0) -> tuple[Tensor, int, Tensor]:
     """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) for nt_dmpnn_update_fused: node-aligned tiles of
     at most `rows` rows (max_in_degree <= 32), balanced to whole rounds of ncu tiles (ncu = 0: the
-    largest tiles; the engine's 128-row plans use PLAN_NCU)."""
+    largest tiles; the engine's 128-row plans use PLAN_NCU).  hub_degree > 0: nodes with more
+    in-edges are hubs, cut at the stride (nt_dmpnn_tile_plan_hubs; max_in_degree is then the largest
+    non-hub in-degree)."""
     dev = _require_device(dst_ptr)
     if dst_ptr.dtype != torch.int32:
         raise TypeError("dst_ptr must be int32")
@@ -421,9 +423,41 @@ def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int, rows: int = 64,
     ntiles = int(lib.nt_dmpnn_tile_count(E, stride))
     tile_ptr = torch.empty(ntiles + 1, dtype=torch.int32, device=dev)
     dsts = torch.empty(max(E, 1), dtype=torch.int32, device=dev)[:E]
-    _run(dev, lib.nt_dmpnn_tile_plan,
-         _ptr(dst_ptr), V, E, stride, _ptr(tile_ptr), ntiles, _ptr(dsts), _stream(dev))
+    if hub_degree > 0:
+        _run(dev, lib.nt_dmpnn_tile_plan_hubs,
+             _ptr(dst_ptr), V, E, stride, int(hub_degree), _ptr(tile_ptr), ntiles, _ptr(dsts), _stream(dev))
+    else:
+        _run(dev, lib.nt_dmpnn_tile_plan,
+             _ptr(dst_ptr), V, E, stride, _ptr(tile_ptr), ntiles, _ptr(dsts), _stream(dev))
     return tile_ptr, ntiles, dsts
+
+
+def mark_hub_rows(row_table: Tensor, dst_ptr: Tensor, hub_degree: int) -> Tensor:
+    """In place: the row-table entries of nodes with more than hub_degree in-edges lose their
+    "last in-edge" flag (nt_dmpnn_mark_hub_rows), so the fused layer leaves their S_out rows to
+    hub_aggregate."""
+    dev = _require_device(row_table, dst_ptr)
+    if dst_ptr.dtype != torch.int32:
+        raise TypeError("dst_ptr must be int32")
+    _run(dev, _lib.load().nt_dmpnn_mark_hub_rows, _ptr(row_table), row_table.shape[0], _ptr(dst_ptr),
+         dst_ptr.numel() - 1, int(hub_degree), _stream(dev))
+    return row_table
+
+
+def hub_aggregate(X: Tensor, perm: Tensor, seg_ptr: Tensor, hubs: Tensor, out: Tensor, *, reduce: str = "sum",
+                  act: tuple[int, float] = (_lib.NT_ACT_IDENTITY, 0.0), amax: Tensor | None = None) -> Tensor:
+    """out[v] = reduce over the in-edges p of v of act(X[perm[p]]) for the nodes v in ``hubs`` (int32),
+    other rows of ``out`` untouched; amax (1 float, may be None) raised to max|out[hubs]|."""
+    dev = _require_device(X, perm, seg_ptr, hubs, out, amax)
+    _require_f32("X", X)
+    _require_f32("out", out)
+    if hubs.dtype != torch.int32 or seg_ptr.dtype != torch.int32 or perm.dtype != torch.int32:
+        raise TypeError("hubs, seg_ptr and perm must be int32")
+    if out.shape[1] != X.shape[1] or out.shape[0] != seg_ptr.numel() - 1:
+        raise ValueError("out must be nseg x h")
+    _run(dev, _lib.load().nt_dmpnn_hub_aggregate, _ptr(X), _ptr(perm), _ptr(seg_ptr), _ptr(hubs), hubs.numel(),
+         X.shape[1], reduce_code(reduce), act[0], act[1], NT_F32, _ptr(amax), _ptr(out), _stream(dev))
+    return out
 
 
 def dmpnn_update_fused(

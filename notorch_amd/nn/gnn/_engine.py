@@ -162,27 +162,57 @@ def _degree_range(lay: DeviceLayout) -> tuple[int, int]:
     return mm
 
 
-def fused_plan(lay: DeviceLayout, V: int, E: int, rows: int = 64):
-    """Tile plan of the fused update for this layout with tiles of at most ``rows`` (64, or 128 for the
-    diagnostic build's update_fk_kernel) rows, balanced to whole rounds over PLAN_NCU CUs,
-    as (tile_ptr, ntiles, dst_sorted, zero_fill), cached on it; None when some node has more than 32
-    in-edges (polymer hubs): those graphs take the unfused path.  One sync per layout."""
+HUB_DEGREE = 32  # nodes with more in-edges are hubs: no node-aligned tile holds them
+
+
+def hub_info(lay: DeviceLayout):
+    """(hub ids int32, count, largest non-hub in-degree) of the dst CSR, or None when no node has more
+    than HUB_DEGREE in-edges.  Cached on the layout (the host collate ships it); one sync otherwise."""
+    if lay.hubs is None:
+        hubs = False
+        if lay.dst_ptr.numel() > 1 and _degree_range(lay)[0] > HUB_DEGREE:
+            deg = lay.dst_ptr[1:] - lay.dst_ptr[:-1]
+            is_hub = deg > HUB_DEGREE
+            ids = torch.nonzero(is_hub).view(-1).to(torch.int32)
+            rest = int(torch.where(is_hub, torch.zeros_like(deg), deg).max())
+            hubs = (ids, ids.numel(), rest)
+        lay.hubs = hubs
+    return lay.hubs or None
+
+
+def fused_plan(lay: DeviceLayout, V: int, E: int, rows: int = 64, dtype: torch.dtype = torch.float32):
+    """Tile plan of the fused update for this layout with tiles of at most ``rows`` (64 or 128) rows,
+    balanced to whole rounds over PLAN_NCU CUs, as (tile_ptr, ntiles, dst_sorted, zero_fill), cached on
+    it.  Hub nodes (more than HUB_DEGREE in-edges, polymer graphs) are cut at the stride; the fp32
+    layer leaves their aggregation to nt_dmpnn_hub_aggregate (None for bf16: those graphs take the
+    unfused path).  One sync per layout."""
+    hubs = hub_info(lay) if E > 0 and V > 0 else None
+    if hubs is not None and dtype != torch.float32:
+        return None
+    hub, maxdeg = (HUB_DEGREE, hubs[2]) if hubs is not None else (0, None)
     if lay.plan is None:
         plan = False
         if E > 0 and V > 0:
-            maxdeg, mindeg = _degree_range(lay)
-            if maxdeg <= 32:
-                tile_ptr, ntiles, dsts = K.tile_plan(lay.dst_ptr, E, maxdeg, rows=64, ncu=K.PLAN_NCU)
-                plan = (tile_ptr, ntiles, dsts, mindeg == 0)
+            mx, mindeg = _degree_range(lay)
+            tile_ptr, ntiles, dsts = K.tile_plan(lay.dst_ptr, E, mx if maxdeg is None else maxdeg, rows=64,
+                                                 ncu=K.PLAN_NCU, hub_degree=hub)
+            plan = (tile_ptr, ntiles, dsts, mindeg == 0)
         lay.plan = plan
     if not lay.plan:
         return None
     if rows <= 64:
         return lay.plan
     if lay.plan_wide is None:  # node-aligned tiles of <= 128 rows, balanced over the CUs
-        tile_ptr, ntiles, _ = K.tile_plan(lay.dst_ptr, E, _degree_range(lay)[0], rows=128, ncu=K.PLAN_NCU)
+        mx = _degree_range(lay)[0] if maxdeg is None else maxdeg
+        tile_ptr, ntiles, _ = K.tile_plan(lay.dst_ptr, E, mx, rows=128, ncu=K.PLAN_NCU, hub_degree=hub)
         lay.plan_wide = (tile_ptr, ntiles)
     return lay.plan_wide[0], lay.plan_wide[1], lay.plan[2], lay.plan[3]
+
+
+def fused_max_in_degree(lay: DeviceLayout) -> int:
+    """The in-degree the fused kernel's segmented scan must cover: the largest non-hub in-degree."""
+    hubs = hub_info(lay)
+    return _degree_range(lay)[0] if hubs is None else hubs[2]
 
 
 def dst_chunks(lay: DeviceLayout):
@@ -340,7 +370,7 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
     if fusable and fp32:  # the fp32 kernel's tile capacity for every layer of this block
         rows = min(K.fused_tile_rows(h, H.dtype, act, reduce, act),
                    K.fused_tile_rows(h, H.dtype, act, reduce, _IDENTITY))
-    plan = fused_plan(lay, V, E, rows) if fusable else None
+    plan = fused_plan(lay, V, E, rows, H.dtype) if fusable else None
     if plan is not None:
         return _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, residual, keep_states,
                               amax)
@@ -390,7 +420,10 @@ def row_table(lay: DeviceLayout, dsts: Tensor, src: Tensor, rev: Tensor, V: int)
     key = (src.data_ptr(), src.numel(), rev.data_ptr(), rev.numel(), V)
     hit = getattr(lay, "row_table", None)
     if hit is None or hit[0] != key or hit[1] is not rev:
-        hit = (key, rev, K.dmpnn_row_table(lay.dst_perm, dsts, src, rev, V))
+        rt = K.dmpnn_row_table(lay.dst_perm, dsts, src, rev, V)
+        if hub_info(lay) is not None:
+            K.mark_hub_rows(rt, lay.dst_ptr, HUB_DEGREE)
+        hit = (key, rev, rt)
         lay.row_table = hit
     return hit[2]
 
@@ -403,7 +436,8 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
     spare_H: Optional[Tensor] = None
     spare_S: Optional[Tensor] = None
     timer = UPDATE_EVENTS
-    maxdeg = _degree_range(lay)[0]
+    maxdeg = fused_max_in_degree(lay)
+    hubs = hub_info(lay)
     _note_update("fused", H.dtype, H.shape[1])
     for l in range(d):
         last = l == d - 1
@@ -422,6 +456,10 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
         if timer is not None:
             ev[1].record()
             timer.append(ev)
+        if hubs is not None:  # the hubs' share of the aggregation the fused launch left out
+            K.hub_aggregate(Hn, lay.dst_perm, lay.dst_ptr, hubs[0], Sn, reduce=reduce,
+                            act=_IDENTITY if last else act,
+                            amax=None if (amax is None or last) else amax[l + 1, 1:2])
         if not keep_states:
             spare_H = H
             spare_S = S

@@ -142,7 +142,24 @@ def test_host_plans_ship_with_the_collate():
         assert types_in_range(lay, G.node_feats, G.edge_feats, 42, 13) is None
     P = make_batch("polymer", 2, seed=1).collate("nodes")
     lay = P._nt_layout
-    assert lay.plan is False and lay.deg_range[0] > 32
+    assert lay.deg_range[0] > 32
+    # hubs (in-degree > 32): listed, and the plans cut them at the stride while every other cut
+    # stays on a node boundary; tiles within the row capacity of the non-hub in-degree
+    dst_ptr = lay.dst_ptr.numpy().astype(np.int64)
+    deg = np.diff(dst_ptr)
+    ids, nhub, rest = lay.hubs
+    assert ids.dtype == torch.int32 and nhub == ids.numel() > 0
+    assert (ids.numpy() == np.nonzero(deg > 32)[0]).all() and rest == deg[deg <= 32].max()
+    hub_pos = np.zeros(P.num_edges + 1, dtype=bool)
+    for v in ids.numpy():
+        hub_pos[dst_ptr[v] + 1:dst_ptr[v + 1]] = True  # interior positions of a hub's in-edge range
+    starts = set(dst_ptr.tolist())
+    for (tile_ptr, ntiles), rows in ((lay.plan[:2], 64), (lay.plan_wide, 128)):
+        tp = tile_ptr.numpy().astype(np.int64)
+        assert tp[0] == 0 and tp[-1] == P.num_edges and len(tp) == ntiles + 1
+        assert np.diff(tp).max() <= rows and np.diff(tp).min() >= 0
+        assert all(int(t) in starts or hub_pos[t] for t in tp)
+        assert hub_pos[tp].any()  # some cut falls inside a hub
     chunk_pos, nchunks, chunk_ptr = lay.dst_chunks
     assert chunk_pos.numel() == nchunks + 1 and int(chunk_ptr[-1]) == nchunks
     assert (np.diff(chunk_pos.numpy()) <= 32).all()

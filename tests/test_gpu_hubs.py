@@ -1,0 +1,133 @@
+"""GPU: hub nodes (in-degree > 32, polymer graphs, BASELINE config 5) on the fused fp32 layer.
+
+The tile plan cuts hubs at the stride (nt_dmpnn_tile_plan_hubs), the fused kernel leaves the hubs'
+aggregation out (row table marked by nt_dmpnn_mark_hub_rows) and nt_dmpnn_hub_aggregate adds it
+(chemprop.py:37-39, :86 with torch_scatter semantics).  Checked against the oracle at 1e-5.
+"""
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from helpers import assert_parity
+from oracle import dmpnn_ref
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _polymer(n, seed, rev_offset="nodes"):
+    from notorch_amd.data.synth import make_batch
+
+    return make_batch("polymer", n, seed=seed).collate(rev_offset)
+
+
+def test_device_hub_plans_match_host():
+    """The device planners (hub info, nt_dmpnn_tile_plan_hubs) give the collate's host plans."""
+    from notorch_amd import kernels as K
+    from notorch_amd.data.models.graph import DeviceLayout
+    from notorch_amd.nn.gnn import _engine
+
+    P = _polymer(3, seed=7)
+    lay = P._nt_layout
+    ids, nhub, rest = lay.hubs
+    assert nhub > 0 and rest <= 32
+    for rows, (tile_ptr, ntiles) in ((64, lay.plan[:2]), (128, lay.plan_wide)):
+        tp, n, dsts = K.tile_plan(lay.dst_ptr.to(DEV), P.num_edges, rest, rows=rows, ncu=K.PLAN_NCU,
+                                  hub_degree=_engine.HUB_DEGREE)
+        assert n == ntiles and torch.equal(tp.cpu(), tile_ptr)
+        assert torch.equal(dsts.cpu(), lay.plan[2])
+    d = DeviceLayout(lay.dst_ptr.to(DEV), lay.dst_perm.to(DEV))
+    hub = _engine.hub_info(d)
+    assert torch.equal(hub[0].cpu(), ids) and hub[1:] == (nhub, rest)
+    # the row table marks exactly the hubs' rows: start flag, no end flag
+    rt = _engine.row_table(d, dsts, P.edge_index[0].to(DEV), P.rev_index.to(DEV), P.num_nodes).cpu()
+    flags, node = rt[:, 3] & 3, rt[:, 3] >> 2
+    is_hub = torch.zeros(P.num_nodes, dtype=torch.bool)
+    is_hub[ids.long()] = True
+    assert (flags[is_hub[node.long()]] == 1).all()
+    assert (flags[~is_hub[node.long()]] & 1).sum() == (~is_hub).sum() - (torch.diff(lay.dst_ptr) == 0).sum()
+
+
+_ACTS = {"relu": (nn.ReLU(), torch.relu), "identity": (nn.Identity(), lambda x: x), "silu": (nn.SiLU(), F.silu)}
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
+@pytest.mark.parametrize("act", ["relu", "identity", "silu"])
+def test_hub_aggregate_matches_scatter(reduce, act):
+    """nt_dmpnn_hub_aggregate writes the hub rows only, torch_scatter's reduce of act(X) over their
+    in-edges, and raises amax to their max |value|."""
+    from notorch_amd import kernels as K
+
+    P = _polymer(2, seed=3, rev_offset="edges")
+    lay = P._nt_layout
+    ids = lay.hubs[0]
+    E, V, h = P.num_edges, P.num_nodes, 300
+    X = torch.randn(E, h, generator=torch.Generator().manual_seed(1))
+    mod, fn = _ACTS[act]
+    out = torch.full((V, h), 7.0, device=DEV)
+    amax = torch.zeros(1, device=DEV)
+    K.hub_aggregate(X.to(DEV), lay.dst_perm.to(DEV), lay.dst_ptr.to(DEV), ids.to(DEV), out, reduce=reduce,
+                    act=K.act_code(mod), amax=amax)
+    ref = dmpnn_ref.scatter(fn(X.double()), P.edge_index[1], V, reduce)
+    o = out.cpu()
+    hub = ids.long()
+    assert_parity(o[hub], ref[hub], what=f"hubs {reduce} {act}")
+    rest = torch.ones(V, dtype=torch.bool)
+    rest[hub] = False
+    assert (o[rest] == 7.0).all()
+    assert amax.item() == o[hub].abs().max().item()
+
+
+@pytest.mark.parametrize("reduce,act,residual", [("sum", nn.ReLU, True), ("mean", nn.ReLU, True),
+                                                 ("max", nn.ReLU, False), ("sum", nn.SiLU, True)])
+def test_block_on_hubs_runs_fused(reduce, act, residual):
+    """A polymer block takes the fused path (d + 1 layer launches + one hub launch per layer) and
+    matches the oracle: 128-row plan for relu / sum, 64-row plan otherwise."""
+    from notorch_amd.nn import ChempropBlock
+    from notorch_amd.nn.gnn import _engine
+
+    G = _polymer(2, seed=11)
+    h = 64
+    torch.manual_seed(0)
+    Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
+    blk = ChempropBlock(hidden_dim=h, depth=3, act=act, reduce=reduce, residual=residual).eval()
+    Ws, bs = dmpnn_ref.block_params(blk)
+    ref_n, ref_e = dmpnn_ref.chemprop_block(Xv, Xe, G.edge_index, G.rev_index, Ws, bs, act=act(),
+                                            residual=residual, reduce=reduce)
+    with torch.no_grad():
+        out = blk.to(DEV)(G.update(node_feats=Xv, edge_feats=Xe).to(DEV))
+    assert _engine.LAST_UPDATE_INFO["fused"]
+    assert_parity(out.edge_feats, ref_e, what="edge")
+    assert_parity(out.node_feats, ref_n, what="node")
+
+
+def test_hub_block_deterministic_and_grads():
+    """Two forwards are bit-identical; training through the fused hub forward matches the oracle's
+    autograd (fp64)."""
+    from notorch_amd.nn import ChempropBlock, Sum
+
+    G = _polymer(2, seed=5)
+    h = 32
+    torch.manual_seed(1)
+    Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
+    blk = ChempropBlock(hidden_dim=h, depth=2, act=nn.SiLU).to(DEV)  # smooth: no relu'(0) ties
+    xv, xe = Xv.to(DEV).requires_grad_(), Xe.to(DEV).requires_grad_()
+    Gd = G.to(DEV).update(node_feats=xv, edge_feats=xe)
+    with torch.no_grad():
+        a = blk(Gd).node_feats.clone()
+        b = blk(Gd).node_feats.clone()
+    assert torch.equal(a, b)
+    out = Sum()(blk(Gd))
+    out.square().sum().backward()
+    Ws, bs = dmpnn_ref.block_params(blk)
+    Xv64, Xe64 = Xv.double().requires_grad_(), Xe.double().requires_grad_()
+    W64 = [w.double().requires_grad_() for w in Ws]
+    b64 = [x.double().requires_grad_() for x in bs]
+    rn, _ = dmpnn_ref.chemprop_block(Xv64, Xe64, G.edge_index, G.rev_index, W64, b64, act=F.silu)
+    dmpnn_ref.readout(rn, G.batch_node_index, len(G), "sum").square().sum().backward()
+    lin0 = blk.layers[0].module.update[0]
+    assert_parity(xv.grad, Xv64.grad, 1e-4, "dXv")
+    assert_parity(xe.grad, Xe64.grad, 1e-4, "dXe")
+    assert_parity(lin0.weight.grad, W64[0].grad, 1e-4, "dW0")
