@@ -109,6 +109,7 @@ def test_hub_block_deterministic_and_grads():
     from notorch_amd.nn import ChempropBlock, Sum
 
     G = _polymer(2, seed=5)
+    ei, rev, bni, B = G.edge_index.clone(), G.rev_index.clone(), G.batch_node_index.clone(), len(G)
     h = 32
     torch.manual_seed(1)
     Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
@@ -125,8 +126,8 @@ def test_hub_block_deterministic_and_grads():
     Xv64, Xe64 = Xv.double().requires_grad_(), Xe.double().requires_grad_()
     W64 = [w.double().requires_grad_() for w in Ws]
     b64 = [x.double().requires_grad_() for x in bs]
-    rn, _ = dmpnn_ref.chemprop_block(Xv64, Xe64, G.edge_index, G.rev_index, W64, b64, act=F.silu)
-    dmpnn_ref.readout(rn, G.batch_node_index, len(G), "sum").square().sum().backward()
+    rn, _ = dmpnn_ref.chemprop_block(Xv64, Xe64, ei, rev, W64, b64, act=F.silu)
+    dmpnn_ref.readout(rn, bni, B, "sum").square().sum().backward()
     lin0 = blk.layers[0].module.update[0]
     assert_parity(xv.grad, Xv64.grad, 1e-4, "dXv")
     assert_parity(xe.grad, Xe64.grad, 1e-4, "dXe")
