@@ -747,12 +747,15 @@ int launch_fk_wide(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
       return launch_fk_t<8, CT, NT_ACT_IDENTITY, NT_ACT_IDENTITY, true, 1>(a, grid, stream);
     return launch_fk_t<8, CT, -1, NT_ACT_IDENTITY, true, 1>(a, grid, stream);
   }
-  // fused (fk_tile_rows: act = relu): scan rounds 3 cover in-degree <= 4 (molecules), 16 every plan
+  // fused (fk_tile_rows: act = relu): scan rounds 3 cover in-degree <= 4 (molecules), 8 in-degree <= 9
+  // (the non-hub nodes of hub graphs, cut at HUB_CUT_DEGREE), 16 every plan
   if (a.aact == NT_ACT_RELU)
-    return maxl <= 3 ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 3>(a, grid, stream)
-                     : launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 16>(a, grid, stream);
-  return maxl <= 3 ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 3>(a, grid, stream)
-                   : launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 16>(a, grid, stream);
+    return maxl <= 3   ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 3>(a, grid, stream)
+           : maxl <= 8 ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 8>(a, grid, stream)
+                       : launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 16>(a, grid, stream);
+  return maxl <= 3   ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 3>(a, grid, stream)
+         : maxl <= 8 ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 8>(a, grid, stream)
+                     : launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_IDENTITY, true, 16>(a, grid, stream);
 }
 
 #ifdef NT_DIAG

@@ -520,8 +520,11 @@ def host_layout(
 
 
 # ---- host-side plans (numpy restatements of the device planners; same arrays, no device sync) ----
-MAX_FUSED_IN_DEGREE = 32  # nt_dmpnn_tile_plan's limit; nodes with more in-edges are hubs (fp32: cut at the
-# stride by nt_dmpnn_tile_plan_hubs and aggregated by nt_dmpnn_hub_aggregate; bf16: the unfused path)
+MAX_FUSED_IN_DEGREE = 32  # nt_dmpnn_tile_plan's limit; a graph with larger in-degrees has hubs
+# hub graphs: nodes with more than HUB_CUT_DEGREE in-edges are cut at the stride by nt_dmpnn_tile_plan_hubs
+# and aggregated by nt_dmpnn_hub_aggregate (fp32; bf16 takes the unfused path), so the rest of the plan
+# keeps node-aligned tiles of in-degree <= 9 (8 scan rounds) instead of 32
+HUB_CUT_DEGREE = 9
 LONG_SEGMENT = 64  # segments longer than this aggregate through the chunked reduce
 CHUNK_ROWS = 32  # rows per chunk of nt_segment_reduce_chunked
 
@@ -599,11 +602,11 @@ def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional
     hub = 0
     lay.hubs = False
     if E > 0 and V > 0 and maxdeg > MAX_FUSED_IN_DEGREE:  # hubs: cut at the stride (fp32 plans)
-        is_hub = deg > MAX_FUSED_IN_DEGREE
+        is_hub = deg > HUB_CUT_DEGREE
         ids = np.nonzero(is_hub)[0].astype(np.int32)
         rest = deg[~is_hub]
         lay.hubs = (torch.from_numpy(ids), int(ids.size), int(rest.max()) if rest.size else 0)
-        hub, maxdeg = MAX_FUSED_IN_DEGREE, lay.hubs[2]
+        hub, maxdeg = HUB_CUT_DEGREE, lay.hubs[2]
     if E > 0 and V > 0:
         tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg, rows=64, ncu=PLAN_NCU, hub_degree=hub)
         lay.plan = (tile_ptr, ntiles, dsts, mindeg == 0)

@@ -162,15 +162,17 @@ def _degree_range(lay: DeviceLayout) -> tuple[int, int]:
     return mm
 
 
-HUB_DEGREE = 32  # nodes with more in-edges are hubs: no node-aligned tile holds them
+MAX_FUSED_IN_DEGREE = 32  # larger in-degrees do not fit node-aligned tiles: the graph has hubs
+HUB_DEGREE = 9  # in a hub graph, nodes with more in-edges are cut at the stride and reduced separately
 
 
 def hub_info(lay: DeviceLayout):
-    """(hub ids int32, count, largest non-hub in-degree) of the dst CSR, or None when no node has more
-    than HUB_DEGREE in-edges.  Cached on the layout (the host collate ships it); one sync otherwise."""
+    """(hub ids int32, count, largest non-hub in-degree) of the dst CSR when some node has more than
+    MAX_FUSED_IN_DEGREE in-edges (hubs: every node with more than HUB_DEGREE), else None.  Cached on
+    the layout (the host collate ships it); one sync otherwise."""
     if lay.hubs is None:
         hubs = False
-        if lay.dst_ptr.numel() > 1 and _degree_range(lay)[0] > HUB_DEGREE:
+        if lay.dst_ptr.numel() > 1 and _degree_range(lay)[0] > MAX_FUSED_IN_DEGREE:
             deg = lay.dst_ptr[1:] - lay.dst_ptr[:-1]
             is_hub = deg > HUB_DEGREE
             ids = torch.nonzero(is_hub).view(-1).to(torch.int32)

@@ -149,7 +149,9 @@ def test_host_plans_ship_with_the_collate():
     deg = np.diff(dst_ptr)
     ids, nhub, rest = lay.hubs
     assert ids.dtype == torch.int32 and nhub == ids.numel() > 0
-    assert (ids.numpy() == np.nonzero(deg > 32)[0]).all() and rest == deg[deg <= 32].max()
+    from notorch_amd.data.models.graph import HUB_CUT_DEGREE
+
+    assert (ids.numpy() == np.nonzero(deg > HUB_CUT_DEGREE)[0]).all() and rest == deg[deg <= HUB_CUT_DEGREE].max()
     hub_pos = np.zeros(P.num_edges + 1, dtype=bool)
     for v in ids.numpy():
         hub_pos[dst_ptr[v] + 1:dst_ptr[v + 1]] = True  # interior positions of a hub's in-edge range

@@ -32,7 +32,7 @@ def test_device_hub_plans_match_host():
     P = _polymer(3, seed=7)
     lay = P._nt_layout
     ids, nhub, rest = lay.hubs
-    assert nhub > 0 and rest <= 32
+    assert nhub > 0 and rest <= _engine.HUB_DEGREE
     for rows, (tile_ptr, ntiles) in ((64, lay.plan[:2]), (128, lay.plan_wide)):
         tp, n, dsts = K.tile_plan(lay.dst_ptr.to(DEV), P.num_edges, rest, rows=rows, ncu=K.PLAN_NCU,
                                   hub_degree=_engine.HUB_DEGREE)
