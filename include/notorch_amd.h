@@ -404,6 +404,17 @@ NT_API int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S, con
                                 float act_alpha, int dtype, void* workspace, int64_t workspace_bytes,
                                 void* dW_out, void* db_out, void* stream);
 
+/* nt_dmpnn_weight_grad on the fp32 layer kernel's numerics (h <= 320, src and rev given): G and A
+ * scaled by powers of two from device bounds and split into two fp16 parts, three fp16 MFMA products
+ * per tile (fp32-accurate: the dropped term and the split roundings are ~2^-22 relative); half the
+ * MFMA work of the bf16x6 kernel.  amax_G: one device float >= max|G|; amax_HS: two device floats
+ * >= max|H|, max|S| (the forward's amax chain row of this layer).  Same workspace and outputs. */
+NT_API int nt_dmpnn_weight_grad_fk(const void* G, const void* H, const void* S, const int64_t* src,
+                                   const int64_t* rev, int64_t V, int64_t E, int64_t h, int act,
+                                   float act_alpha, const float* amax_G, const float* amax_HS, int dtype,
+                                   void* workspace, int64_t workspace_bytes, void* dW_out, void* db_out,
+                                   void* stream);
+
 /* Device status word of the calling device (no reference counterpart: the reference's ops cannot
  * hang).  The persistent fp32 update kernel hands work between its waves through bounded LDS waits;
  * a wait that gives up sets this word (sticky) and the launch's outputs are invalid.

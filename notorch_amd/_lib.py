@@ -122,6 +122,11 @@ SIGNATURES: dict[str, tuple] = {
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _c_int, _vp, _c_i64, _vp, _vp, _vp],
     ),
+    "nt_dmpnn_weight_grad_fk": (
+        _c_int,
+        [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _vp, _vp, _c_int, _vp, _c_i64, _vp, _vp,
+         _vp],
+    ),
     "nt_device_status": (_c_int, [_vp, _vp]),
     "nt_device_status_reset": (_c_int, [_vp]),
 }

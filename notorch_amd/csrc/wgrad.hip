@@ -437,6 +437,240 @@ __global__ void __launch_bounds__(512, 1) wgrad_wide_kernel(WwArgs a) {
   }
 }
 
+// wgrad_fk_kernel (h <= 320, gathered A): the wide kernel's work split on the fp32 layer kernel's
+// numerics (csrc/update_fk.hpp): G scaled by s_G = 2^(14 - e(max|G|)), A by s_A = 2^(14 - e(bound
+// of |S[src] - act(H[rev])|)) (device amax values the caller already has: the forward's amax chain
+// and the max|G| the backward's dA takes), each split into two fp16 parts, and three
+// v_mfma_f32_16x16x32_f16 products G1 A0 + G0 A1 + G0 A0 per tile (the dropped G1 A1 and the split
+// roundings are ~2^-22 relative: fp32 accuracy).  Against the bf16x6 wide kernel: half the MFMAs,
+// two thirds of the LDS bytes and of the split arithmetic, and a double-buffered LDS slab (112 KiB,
+// one barrier per step instead of two).  Same work split: one 512-thread workgroup per (edge chunk,
+// 128-column block of A), wave w owns i-tiles 5 (w % 4) .. +5 and j-tiles 4 (w / 4) .. +4.
+constexpr int kFJ = 128;                     // A columns per workgroup
+constexpr int kFGPart = 4 * kWI * 16;        // one fp16 part of the G slab (20 KiB)
+constexpr int kFAPart = 4 * kFJ * 16;        // one fp16 part of the A slab (10 KiB)
+constexpr int kFBuf = 2 * (kFGPart + kFAPart);
+constexpr int kFLds = 2 * kFBuf;             // 112 KiB: two slabs
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split2s(const float (&x)[8], float s, f16x8& p0, f16x8& p1) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float v = x[j] * s;
+    const _Float16 h0 = (_Float16)v;
+    p0[j] = h0;
+    p1[j] = (_Float16)(v - (float)h0);
+  }
+}
+
+// 2^(14 - e): the power-of-two scale that maps |x| <= bound below 2^14 (update_fk.hpp scale_exp, but
+// up to 2^120: tiny gradients are scaled up all the way, and the result is unscaled in two steps)
+__device__ __forceinline__ int wg_scale_exp(float bound) {
+  if (!(bound > 0.f) || !(bound <= 3.0e38f)) return 0;
+  int e;
+  frexpf(bound, &e);
+  const int s = 14 - e;
+  return s < -100 ? -100 : (s > 120 ? 120 : s);
+}
+__device__ __forceinline__ float wg_act_bound(float m, int act, float alpha) {
+  if (act == NT_ACT_RELU || act == NT_ACT_IDENTITY) return m;
+  const float b = fabsf(alpha) > 1.f ? fabsf(alpha) : 1.f;
+  return b * m + b;
+}
+
+struct WfArgs {
+  const float* G;
+  const float* H;
+  const float* S;
+  const int64_t* src;
+  const int64_t* rev;
+  const float* amax_G;   // [0] >= max|G|
+  const float* amax_HS;  // [0] >= max|H|, [1] >= max|S|
+  int64_t E, h;
+  int jblocks, ksplit, chunk_steps, xcds;
+  float alpha;
+  int act;
+  float* part;     // [ksplit][h][h]
+  float* part_db;  // [ksplit][h] or NULL
+};
+
+template <int ACT>
+__global__ void __launch_bounds__(512, 1) wgrad_fk_kernel(WfArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int nb = gridDim.x;
+  int w = blockIdx.x;
+  if (a.xcds > 1 && nb % a.xcds == 0) w = (w % a.xcds) * (nb / a.xcds) + w / a.xcds;
+  const int y = w / a.jblocks, jb = w - y * a.jblocks;
+  const int64_t h = a.h, j0 = (int64_t)jb * kFJ;
+  const int64_t e_beg = (int64_t)y * a.chunk_steps * kK;
+  const int64_t e_end0 = e_beg + (int64_t)a.chunk_steps * kK;
+  const int64_t e_end = e_end0 < a.E ? e_end0 : a.E;
+  const int nsteps = e_end > e_beg ? (int)((e_end - e_beg + kK - 1) / kK) : 0;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int ni16 = (int)((h + 15) / 16) * 16;
+  const bool want_db = a.part_db != nullptr && jb == 0;
+  const int eG = wg_scale_exp(a.amax_G[0]);
+  const int eA = wg_scale_exp(a.amax_HS[1] + wg_act_bound(a.amax_HS[0], a.act, a.alpha));
+  const float sG = ldexpf(1.f, eG), sA = ldexpf(1.f, eA);
+
+  int cg[3], gg[3];
+  bool okg[3];
+#pragma unroll
+  for (int m = 0; m < 3; ++m) {
+    const int q = t + 512 * m;
+    okg[m] = q < 4 * ni16;
+    const int qq = okg[m] ? q : 0;
+    gg[m] = qq / ni16;
+    cg[m] = qq - gg[m] * ni16;
+  }
+  const int c1 = t & (kFJ - 1), ga = t >> 7;  // 128 columns x 4 groups = 512: one edge group per wave
+  const int64_t jc1 = j0 + c1 < h ? j0 + c1 : 0;
+  const unsigned mj1 = j0 + c1 < h ? ~0u : 0u;
+  float dbacc[3] = {0.f, 0.f, 0.f};
+
+  auto load_idx = [&](int s) __attribute__((always_inline)) -> int {
+    int64_t e = e_beg + (int64_t)s * kK + 8 * ga + (lane & 7);
+    e = e < e_end ? e : e_end - 1;
+    return lane >= 16 ? 0 : (int)(lane < 8 ? a.src[e] : a.rev[e]);
+  };
+  float xg[3][8], xs[8], xh[8];
+  int64_t eb_cur = 0;
+  auto load = [&](int s, int idxv) __attribute__((always_inline)) {
+    const int64_t eb = e_beg + (int64_t)s * kK;
+    eb_cur = eb;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      const int64_t col = cg[m] < h ? cg[m] : 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        int64_t e = eb + 8 * gg[m] + r;
+        e = e < e_end ? e : e_end - 1;
+        xg[m][r] = a.G[e * h + col];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int64_t se = __builtin_amdgcn_readlane(idxv, r), re = __builtin_amdgcn_readlane(idxv, 8 + r);
+      xs[r] = a.S[se * h + jc1];
+      xh[r] = a.H[re * h + jc1];
+    }
+  };
+  auto store = [&](char* buf) __attribute__((always_inline)) {
+    char* gbase = buf;
+    char* abase = buf + 2 * kFGPart;
+#pragma unroll
+    for (int m = 0; m < 3; ++m) {
+      float gv[8];
+      const unsigned mc = (okg[m] && cg[m] < h) ? ~0u : 0u;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const unsigned ok = eb_cur + 8 * gg[m] + r < e_end ? ~0u : 0u;
+        gv[r] = __uint_as_float(__float_as_uint(xg[m][r]) & (ok & mc));
+      }
+      if (want_db) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) dbacc[m] += gv[r];
+      }
+      if (okg[m]) {
+        f16x8 p0, p1;
+        split2s(gv, sG, p0, p1);
+        const int off = (gg[m] * kWI + cg[m]) * 16;
+        *reinterpret_cast<f16x8*>(gbase + off) = p0;
+        *reinterpret_cast<f16x8*>(gbase + kFGPart + off) = p1;
+      }
+    }
+    float av[8];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const unsigned ok = eb_cur + 8 * ga + r < e_end ? ~0u : 0u;
+      const float v = xs[r] - act_t<ACT>(xh[r], a.act, a.alpha);
+      av[r] = __uint_as_float(__float_as_uint(v) & (ok & mj1));
+    }
+    f16x8 p0, p1;
+    split2s(av, sA, p0, p1);
+    const int off = (ga * kFJ + c1) * 16;
+    *reinterpret_cast<f16x8*>(abase + off) = p0;
+    *reinterpret_cast<f16x8*>(abase + kFAPart + off) = p1;
+  };
+
+  const int fr = lane & 15, g16 = lane >> 4;
+  const int wi = wave & 3, wj = wave >> 2;  // i-tiles 5 wi .. 5 wi + 4, j-tiles 4 wj .. 4 wj + 3
+  f32x4 acc[5][4];
+#pragma unroll
+  for (int x = 0; x < 5; ++x)
+#pragma unroll
+    for (int z = 0; z < 4; ++z) acc[x][z] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // waves whose i-tiles or j-tiles all lie past h skip the MFMAs
+  const bool active = 16 * 5 * wi < ni16 && j0 + 16 * 4 * wj < h;
+
+  int idx_next = 0;
+  if (nsteps > 0) {
+    load(0, load_idx(0));
+    if (nsteps > 1) idx_next = load_idx(1);
+    store(lds);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps;
+    if (more) {
+      load(s + 1, idx_next);
+      if (s + 2 < nsteps) idx_next = load_idx(s + 2);
+    }
+    if (active) {
+      const char* gb = lds + (s & 1) * kFBuf;
+      const char* ab = gb + 2 * kFGPart;
+      f16x8 fb[4][2];
+#pragma unroll
+      for (int z = 0; z < 4; ++z) {
+        const int off_b = (g16 * kFJ + 16 * (4 * wj + z) + fr) * 16;
+        fb[z][0] = *reinterpret_cast<const f16x8*>(ab + off_b);
+        fb[z][1] = *reinterpret_cast<const f16x8*>(ab + kFAPart + off_b);
+      }
+#pragma unroll
+      for (int x = 0; x < 5; ++x) {
+        const int off_a = (g16 * kWI + 16 * (5 * wi + x) + fr) * 16;
+        const f16x8 fa0 = *reinterpret_cast<const f16x8*>(gb + off_a);
+        const f16x8 fa1 = *reinterpret_cast<const f16x8*>(gb + kFGPart + off_a);
+#pragma unroll
+        for (int z = 0; z < 4; ++z) {
+          f32x4 cc = acc[x][z];
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa1, fb[z][0], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa0, fb[z][1], cc, 0, 0, 0);
+          cc = __builtin_amdgcn_mfma_f32_16x16x32_f16(fa0, fb[z][0], cc, 0, 0, 0);
+          acc[x][z] = cc;
+        }
+      }
+    }
+    if (more) store(lds + ((s + 1) & 1) * kFBuf);
+    __syncthreads();  // one barrier: the next slab is written, this one is read by every wave
+  }
+
+  // unscale by 2^-eG 2^-eA (two exact steps: their product may leave the fp32 range)
+  const float iG = ldexpf(1.f, -eG), iA = ldexpf(1.f, -eA);
+  float* P = a.part + (int64_t)y * h * h;
+#pragma unroll
+  for (int x = 0; x < 5; ++x)
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+      const int64_t col = j0 + 16 * (4 * wj + z) + fr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = 16 * (5 * wi + x) + 4 * g16 + q;
+        if (row < h && col < h) P[row * h + col] = (acc[x][z][q] * iG) * iA;
+      }
+    }
+  if (want_db) {  // fixed-order column sums over the 4 edge groups (deterministic)
+    float* red = reinterpret_cast<float*>(lds);  // the slabs are dead after the last barrier
+#pragma unroll
+    for (int m = 0; m < 3; ++m)
+      if (okg[m]) red[gg[m] * kWI + cg[m]] = dbacc[m];
+    __syncthreads();
+    if (t < h) a.part_db[(int64_t)y * h + t] = ((red[t] + red[kWI + t]) + red[2 * kWI + t]) + red[3 * kWI + t];
+  }
+}
+
 // out[i] = sum_y part[y][i] in ascending y (fixed order: deterministic)
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int64_t n,
                                                            int ksplit, float* __restrict__ out) {
@@ -480,10 +714,10 @@ struct WPlan {
   int ksplit, chunk_steps;
 };
 
-// one workgroup per CU: ksplit = CUs / jblocks chunks of the edge range
-WPlan make_wide_plan(int64_t E, int64_t h) {
+// one workgroup per CU: ksplit = CUs / jblocks chunks of the edge range (jcols: A columns per block)
+WPlan make_wide_plan(int64_t E, int64_t h, int jcols = kWJ) {
   WPlan p;
-  const int jblocks = (int)((h + kWJ - 1) / kWJ);
+  const int jblocks = (int)((h + jcols - 1) / jcols);
   const int64_t steps = (E + kK - 1) / kK;
   int64_t ks = (cu_count() > 0 ? cu_count() : 256) / jblocks;
   if (ks < 1) ks = 1;
@@ -503,8 +737,9 @@ int xcd_count();  // csrc/update_ps.hip: the current device's XCD count, queried
 extern "C" int64_t nt_dmpnn_weight_grad_workspace(int64_t E, int64_t h) {
   if (E < 0 || h <= 0) return -1;
   const nt::Plan p = nt::make_plan(E, h);
-  const nt::WPlan q = nt::make_wide_plan(E, h);
-  const int64_t ks = p.ksplit > q.ksplit ? p.ksplit : q.ksplit;  // either kernel fits
+  const nt::WPlan q = nt::make_wide_plan(E, h), f = nt::make_wide_plan(E, h, nt::kFJ);
+  int64_t ks = p.ksplit > q.ksplit ? p.ksplit : q.ksplit;  // every kernel fits
+  ks = ks > f.ksplit ? ks : f.ksplit;
   return ks * (h * h + h) * (int64_t)sizeof(float);
 }
 
@@ -598,6 +833,64 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
   NT_LAUNCH_CHECK();
   if (db_out) {
     wgrad_reduce_kernel<<<grid_for(h, 256, 64), 256, 0, stream>>>(a.part_db, h, p.ksplit, (float*)db_out);
+    NT_LAUNCH_CHECK();
+  }
+  return NT_OK;
+}
+
+extern "C" int nt_dmpnn_weight_grad_fk(const void* G, const void* H, const void* S, const int64_t* src,
+                                       const int64_t* rev, int64_t V, int64_t E, int64_t h, int act,
+                                       float act_alpha, const float* amax_G, const float* amax_HS, int dtype,
+                                       void* workspace, int64_t workspace_bytes, void* dW_out, void* db_out,
+                                       void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_weight_grad_fk: fp32 only");
+  NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
+  NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(h <= kWI, NT_EUNSUPPORTED, "nt_dmpnn_weight_grad_fk: h <= 320 (use nt_dmpnn_weight_grad)");
+  NT_REQUIRE(V < ((int64_t)1 << 31) && E < ((int64_t)1 << 31), NT_EUNSUPPORTED,
+             "nt_dmpnn_weight_grad_fk: V and E must be < 2^31");
+  NT_REQUIRE(dW_out, NT_EINVAL, "NULL dW_out");
+  hipStream_t stream = as_stream(stream_);
+  if (E == 0) {
+    NT_HIP(hipMemsetAsync(dW_out, 0, h * h * sizeof(float), stream));
+    if (db_out) NT_HIP(hipMemsetAsync(db_out, 0, h * sizeof(float), stream));
+    return NT_OK;
+  }
+  NT_REQUIRE(G && S && H && src && rev && amax_G && amax_HS, NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(workspace && workspace_bytes >= nt_dmpnn_weight_grad_workspace(E, h), NT_EINVAL,
+             "workspace too small (nt_dmpnn_weight_grad_workspace)");
+  const WPlan q = make_wide_plan(E, h, kFJ);
+  WfArgs b;
+  b.G = (const float*)G;
+  b.H = (const float*)H;
+  b.S = (const float*)S;
+  b.src = src;
+  b.rev = rev;
+  b.amax_G = amax_G;
+  b.amax_HS = amax_HS;
+  b.E = E;
+  b.h = h;
+  b.jblocks = (int)((h + kFJ - 1) / kFJ);
+  b.ksplit = q.ksplit;
+  b.chunk_steps = q.chunk_steps;
+  b.xcds = xcd_count();
+  b.alpha = act_alpha;
+  b.act = act;
+  b.part = (float*)workspace;
+  b.part_db = db_out ? b.part + (int64_t)q.ksplit * h * h : nullptr;
+  const int grid = b.jblocks * q.ksplit;
+  auto kern = act == NT_ACT_IDENTITY ? wgrad_fk_kernel<NT_ACT_IDENTITY>
+              : act == NT_ACT_RELU   ? wgrad_fk_kernel<NT_ACT_RELU>
+                                     : wgrad_fk_kernel<-1>;
+  NT_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kFLds));
+  kern<<<grid, 512, kFLds, stream>>>(b);
+  NT_LAUNCH_CHECK();
+  wgrad_reduce_kernel<<<grid_for(h * h, 256, 256 * 8), 256, 0, stream>>>(b.part, h * h, q.ksplit, (float*)dW_out);
+  NT_LAUNCH_CHECK();
+  if (db_out) {
+    wgrad_reduce_kernel<<<grid_for(h, 256, 64), 256, 0, stream>>>(b.part_db, h, q.ksplit, (float*)db_out);
     NT_LAUNCH_CHECK();
   }
   return NT_OK;

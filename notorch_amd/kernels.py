@@ -210,13 +210,13 @@ def dmpnn_init(
     return H0, S
 
 
-def _require_amax(amax: Tensor | None, dtype: torch.dtype) -> None:
+def _require_amax(amax: Tensor | None, dtype: torch.dtype, n: int = 2) -> None:
     if amax is None:
         return
     if dtype != torch.float32:
         raise ValueError("amax is fp32 only")
-    if amax.dtype != torch.float32 or amax.numel() < 2 or not amax.is_contiguous():
-        raise ValueError("amax must be a contiguous float32 device tensor of 2 elements")
+    if amax.dtype != torch.float32 or amax.numel() < n or not amax.is_contiguous():
+        raise ValueError(f"amax must be a contiguous float32 device tensor of {n} elements")
 
 
 def absmax(X: Tensor, out: Tensor | None = None) -> Tensor:
@@ -551,11 +551,13 @@ def dmpnn_row_table(perm: Tensor, dst_sorted: Tensor, src: Tensor, rev: Tensor, 
     return out
 
 
-def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None, *, kernel: str = "fk") -> Tensor:
+def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None, *, kernel: str = "fk",
+                 amax: Tensor | None = None) -> Tensor:
     """X @ W^T for the packed image Wp of W (fp32, h % 4 == 0): the layer GEMM alone.  With
     Wp = pack_weights(W.t()) it is the backward's dA = G @ W.  kernel = "fk": the fp16x3 layer kernel
-    in dense mode (max|X| by nt_absmax first, any h); "pk": the bf16x6 persistent kernel (h <= 304)."""
-    dev = _require_device(X, Wp, out)
+    in dense mode (amax: 2 device floats whose [1] >= max|X|, else nt_absmax first; any h); "pk": the
+    bf16x6 persistent kernel (h <= 304)."""
+    dev = _require_device(X, Wp, out, amax)
     _require_f32("X", X)
     M, h = X.shape
     if Wp.numel() != packed_weight_numel(h, X.dtype):
@@ -564,10 +566,12 @@ def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None, *, kernel: st
         raise ValueError("dense_matmul: X must be contiguous")
     if out is None:
         out = torch.empty_like(X)
-    amax = None
     if kernel == "fk":
-        amax = torch.zeros(2, dtype=torch.float32, device=dev)
-        absmax(X, amax[1:2])
+        if amax is None:
+            amax = torch.zeros(2, dtype=torch.float32, device=dev)
+            absmax(X, amax[1:2])
+        else:
+            _require_amax(amax, X.dtype)
     elif kernel != "pk":
         raise ValueError("kernel must be 'fk' or 'pk'")
     _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_F32, _ptr(amax), _ptr(out),
@@ -576,10 +580,13 @@ def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None, *, kernel: st
 
 
 def weight_grad(G: Tensor, H: Tensor | None, S: Tensor, src: Tensor | None, rev: Tensor | None, *,
-                act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0), bias: bool = True) -> tuple[Tensor, Tensor | None]:
+                act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0), bias: bool = True,
+                amax_G: Tensor | None = None, amax_HS: Tensor | None = None) -> tuple[Tensor, Tensor | None]:
     """(dW, db) = (G^T A, sum_e G[e]) with A[e] = S[src e] - act(H[rev e]) formed on the fly
-    (src = rev = None: A = S).  fp32, split-K bf16x6 MFMA, deterministic."""
-    dev = _require_device(G, H, S, src, rev)
+    (src = rev = None: A = S).  fp32, split-K, deterministic.  With amax_G (1 device float >= max|G|)
+    and amax_HS (2 floats >= max|H|, max|S|), h <= 320 and src / rev given: the two-part fp16 kernel
+    (nt_dmpnn_weight_grad_fk); else the bf16x6 kernel."""
+    dev = _require_device(G, H, S, src, rev, amax_G, amax_HS)
     _require_f32("G", G)
     _require_f32("S", S)
     E, h = G.shape
@@ -609,6 +616,13 @@ def weight_grad(G: Tensor, H: Tensor | None, S: Tensor, src: Tensor | None, rev:
     ws = torch.empty((max(nbytes, 4) + 3) // 4, dtype=torch.float32, device=dev)
     dW = torch.empty(h, h, dtype=torch.float32, device=dev)
     db = torch.empty(h, dtype=torch.float32, device=dev) if bias else None
+    if amax_G is not None and amax_HS is not None and src is not None and h <= 320:
+        _require_amax(amax_G, G.dtype, n=1)
+        _require_amax(amax_HS, G.dtype)
+        _run(dev, lib.nt_dmpnn_weight_grad_fk, _ptr(G), _ptr(H), _ptr(S), _ptr(src), _ptr(rev), S.shape[0], E,
+             h, act[0], act[1], _ptr(amax_G), _ptr(amax_HS), NT_F32, _ptr(ws), ws.numel() * 4, _ptr(dW), _ptr(db),
+             _stream(dev))
+        return dW, db
     _run(dev, lib.nt_dmpnn_weight_grad, _ptr(G), _ptr(H), _ptr(S), _ptr(src), _ptr(rev), S.shape[0], E, h,
          act[0], act[1], NT_F32, _ptr(ws), ws.numel() * 4, _ptr(dW), _ptr(db), _stream(dev))
     return dW, db

@@ -47,7 +47,8 @@ from notorch_amd._lib import NT_ACT_IDENTITY
 from notorch_amd.data.models.graph import DeviceLayout
 
 _IDENTITY = (NT_ACT_IDENTITY, 0.0)
-# fp32 weight gradient: "kernel" (nt_dmpnn_weight_grad) or "library" (message + split-K library GEMM)
+# fp32 weight gradient: "kernel" (nt_dmpnn_weight_grad_fk for h <= 320, else nt_dmpnn_weight_grad),
+# "kernel6" (nt_dmpnn_weight_grad, bf16x6) or "library" (message + split-K library GEMM)
 _WGRAD_DEFAULT = "kernel"
 
 # Optional per-launch timer for the dominant kernel (bench.py sets it): a list that receives
@@ -277,8 +278,9 @@ def block_forward(
     keep_states: bool = False,
     drop: Optional[tuple[float, int]] = None,
 ) -> tuple[Tensor, Tensor, list[tuple[Tensor, Tensor]]]:
-    """Run the kernel sequence; returns (node, H_d, states) with states = [(H_l, S_l)] for
-    l = 0..d-1 (each layer's input hidden state and its aggregation) if keep_states, else [].
+    """Run the kernel sequence; returns (node, H_d, states) with states = [(H_l, S_l, amax_l)] for
+    l = 0..d-1 (each layer's input hidden state, its aggregation and the fp32 split bounds (max|H_l|,
+    max|S_l|) on the device, or an empty tensor) if keep_states, else [].
     drop = (p, seed): training-mode dropout of every layer update (layer l draws from
     dropout_offset(l, E, h))."""
     V = Xv.shape[0]
@@ -298,6 +300,9 @@ def block_forward(
         H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce, amax=a0)
     return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop,
                            amax)
+
+
+_NO_AMAX = torch.empty(0)  # a state without a valid amax row (bf16, or a path that skips the chain)
 
 
 def _amax_buffer(d: int, X: Tensor) -> Optional[Tensor]:
@@ -384,8 +389,9 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
     timer = UPDATE_EVENTS
     _note_update("persistent" if persistent else "unfused", H.dtype, h)
     for l in range(d):
-        if keep_states:
-            states.append((H, S))
+        if keep_states:  # the amax row is valid where the persistent kernel keeps the chain
+            states.append((H, S, amax[l] if amax is not None and ((persistent and drop is None) or l == 0)
+                           else _NO_AMAX))
         if timer is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
@@ -444,7 +450,7 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
     for l in range(d):
         last = l == d - 1
         if keep_states:
-            states.append((H, S))
+            states.append((H, S, _NO_AMAX if amax is None else amax[l]))
         if timer is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
@@ -657,22 +663,39 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
     d = len(weights)
     dWs: list = [None] * d
     dbs: list = [None] * d
+    wgrad = os.environ.get("NT_WGRAD", _WGRAD_DEFAULT)
     for l in range(d - 1, -1, -1):
-        H_l, S_l = states[l]
+        H_l, S_l, am_l = states[l]
         W = weights[l].detach()
         # dropout: the update's gradient is keep * G / (1 - p); the residual path keeps G
         Gu = G if drop is None else K.dropout_residual(G, drop[0], drop[1], dropout_offset(l, E, h))
-        if Gu.dtype == torch.float32 and os.environ.get("NT_WGRAD", _WGRAD_DEFAULT) == "kernel":
-            # split-K bf16x6 MFMA with A = S[src] - act(H[rev]) formed while staging (never written)
-            dWs[l], dbs[l] = K.weight_grad(Gu.contiguous(), H_l.contiguous(), S_l.contiguous(), src, rev,
-                                           act=act)
+        Gu = Gu.contiguous()
+        fp32 = Gu.dtype == torch.float32
+        fk_dense = fp32 and K.fused_supported(V, E, h, Gu.dtype)
+        fk_wgrad = fp32 and wgrad == "kernel" and h <= 320
+        gmax = None
+        if fk_dense or fk_wgrad:  # max|G|: the split scale of both fp16-split kernels
+            gmax = torch.zeros(2, dtype=torch.float32, device=Gu.device)
+            K.absmax(Gu, gmax[1:2])
+        if fp32 and wgrad in ("kernel", "kernel6"):
+            # split-K MFMA with A = S[src] - act(H[rev]) formed while staging (never written): the
+            # two-part fp16 kernel (h <= 320) on the forward's bounds, else bf16x6
+            am = None
+            if fk_wgrad:
+                am = am_l if am_l.numel() == 2 else None
+                if am is None:  # a forward path that did not keep the chain
+                    am = torch.zeros(2, dtype=torch.float32, device=Gu.device)
+                    K.absmax(H_l.contiguous(), am[0:1])
+                    K.absmax(S_l.contiguous(), am[1:2])
+            dWs[l], dbs[l] = K.weight_grad(Gu, H_l.contiguous(), S_l.contiguous(), src, rev, act=act,
+                                           amax_G=None if am is None else gmax[1:2], amax_HS=am)
         else:
             A = K.dmpnn_message(H_l, S_l, src, rev, act=act)
             dWs[l] = _weight_grad(Gu, A)
             dbs[l] = Gu.sum(0)
             del A
-        if Gu.dtype == torch.float32 and K.fused_supported(V, E, h, Gu.dtype):
-            dA = K.dense_matmul(Gu.contiguous(), K.pack_weights(W.t().contiguous(), fk_only=True))
+        if fk_dense:
+            dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous(), fk_only=True), amax=gmax)
         else:
             dA = torch.mm(Gu, W)
         del Gu
@@ -719,8 +742,8 @@ class ChempropBlockFunction(torch.autograd.Function):
         need = ctx.needs_input_grad
         if kernel_bwd:
             flat = rest[nparams:]
-            states = [(flat[2 * i], flat[2 * i + 1]) for i in range(nlayers)]
-            H_last = flat[2 * nlayers] if reduce in ("max", "min") else None
+            states = [tuple(flat[3 * i:3 * i + 3]) for i in range(nlayers)]
+            H_last = flat[3 * nlayers] if reduce in ("max", "min") else None
             src = edge_index[0].contiguous()
             dst = edge_index[1].contiguous()
             dXv, dXe, dWs, dbs = block_backward(

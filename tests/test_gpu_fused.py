@@ -424,3 +424,32 @@ def test_weight_grad_no_edges():
     dW, db = K.weight_grad(Z, Z, torch.randn(3, 16, device=DEV), torch.empty(0, dtype=torch.long, device=DEV),
                            torch.empty(0, dtype=torch.long, device=DEV))
     assert torch.count_nonzero(dW) == 0 and torch.count_nonzero(db) == 0
+
+
+@pytest.mark.parametrize("h,E,act,gs,xs", [(300, 77_840, "relu", 1.0, 1.0), (300, 1, "relu", 1.0, 1.0),
+                                            (100, 1000, "identity", 1e-6, 1e3), (64, 4097, "gelu", 1e4, 1e-3),
+                                            (4, 3, "relu", 1.0, 1.0), (320, 5000, "tanh", 1.0, 1.0),
+                                            (300, 33, "leaky_relu", 3.0, 0.5), (36, 20_000, "silu", 1e-20, 1e10)])
+def test_weight_grad_fk(h, E, act, gs, xs):
+    """nt_dmpnn_weight_grad_fk (two-part fp16 split on the forward's bounds) against fp64 at the fp32
+    contract, over magnitudes that need the power-of-two scales (G from 1e-20 to 1e4, H / S from 1e-3
+    to 1e10) and with bounds above the true maxima (any bound >= max works); bit-identical repeat."""
+    K = _K()
+    mods = {"relu": nn.ReLU(), "identity": nn.Identity(), "gelu": nn.GELU(), "tanh": nn.Tanh(),
+            "leaky_relu": nn.LeakyReLU(0.1), "silu": nn.SiLU()}
+    mod = mods[act]
+    g = torch.Generator().manual_seed(E + h + 1)
+    V = max(E // 2, 1)
+    Gr = torch.randn(E, h, generator=g) * gs
+    H, S = torch.randn(E, h, generator=g) * xs, torch.randn(V, h, generator=g) * xs
+    src = torch.randint(0, V, (E,), generator=g)
+    rev = torch.randint(0, E, (E,), generator=g)
+    amax_G = torch.tensor([Gr.abs().max().item() * 1.7], device=DEV)
+    amax_HS = torch.tensor([H.abs().max().item(), S.abs().max().item() * 1.3], device=DEV)
+    args = (Gr.to(DEV), H.to(DEV), S.to(DEV), src.to(DEV), rev.to(DEV))
+    dW, db = K.weight_grad(*args, act=K.act_code(mod), amax_G=amax_G, amax_HS=amax_HS)
+    A = S.double()[src] - mod(H.double())[rev]
+    assert_parity(dW, Gr.double().t() @ A, FP32_NORM_TOL, f"dW h={h} E={E} {act}")
+    assert_parity(db, Gr.double().sum(0), FP32_NORM_TOL, f"db h={h} E={E}")
+    dW2, db2 = K.weight_grad(*args, act=K.act_code(mod), amax_G=amax_G, amax_HS=amax_HS)
+    assert torch.equal(dW, dW2) and torch.equal(db, db2)
