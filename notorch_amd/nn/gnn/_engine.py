@@ -291,7 +291,8 @@ def block_forward(
         return _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states,
                                drop)
     chunks = dst_chunks(lay)
-    if chunks is not None:  # hubs: the fused init would walk a hub's in-edges on one lane
+    if chunks is not None:
+        # hubs: the fused init would walk a hub's in-edges on one wave (polymer-16: 3.17 vs 3.00 ms)
         H, _ = K.dmpnn_init(Xv, Xe, src, amax=a0)
         S = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks)
         if a0 is not None:
