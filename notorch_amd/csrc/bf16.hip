@@ -270,7 +270,8 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     }
   };
   auto stage_c = [&]() {
-    const int64_t s = ce >= 0 ? src[ce] : -1, q = ce >= 0 ? rev[ce] : -1;
+    // dense mode (src = rev = NULL, nt_dmpnn_dense_matmul): row e of A is S[e]
+    const int64_t s = ce >= 0 ? (src ? src[ce] : (int64_t)ce) : -1, q = (ce >= 0 && rev) ? rev[ce] : -1;
     cs = (s >= 0 && s < V) ? (int)s : -1;
     cq = (q >= 0 && q < E) ? (int)q : -1;
   };

@@ -700,8 +700,15 @@ extern "C" int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const 
                                      const float* amax_in, void* out, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul: fp32 only");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul: fp32 or bf16");
   NT_REQUIRE(M >= 0 && M < (int64_t(1) << 31) && h > 0, NT_EINVAL, "bad sizes");
+  if (dtype == NT_BF16) {  // the bf16 layer kernel without gathers, residual or bias (h <= 512)
+    NT_REQUIRE(h <= 512, NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul: bf16 needs h <= 512");
+    if (M == 0) return NT_OK;
+    NT_REQUIRE(X && Wp && out && X != out, NT_EINVAL, "NULL pointer or out aliases X");
+    return launch_update_bf16(X, X, nullptr, nullptr, Wp, nullptr, M, M, h, 0, NT_ACT_IDENTITY, 0.f, out,
+                              as_stream(stream_));
+  }
   NT_REQUIRE(amax_in ? (h % 4 == 0 && h <= 8192) : ps_supported(h), NT_EUNSUPPORTED,
              "nt_dmpnn_dense_matmul needs h % 4 == 0 (and h <= 304 without amax_in)");
   if (M == 0) return NT_OK;

@@ -671,6 +671,203 @@ __global__ void __launch_bounds__(512, 1) wgrad_fk_kernel(WfArgs a) {
   }
 }
 
+// wgrad_bf16_kernel (bf16 storage, h <= 512, gathered A): dW = G^T A and db = colsum G of a bf16
+// layer (BASELINE config 3) with the message A = S[src] - act(H[rev]) formed in fp32 and rounded to
+// bf16 once, as the bf16 forward's message is (chemprop.py:40), never written.  The operands are
+// exact bf16 values, so one v_mfma_f32_16x16x32_bf16 per tile and fp32 partials (the library path
+// rounded every split-K partial to bf16).  One 512-thread workgroup per (edge chunk, 128-column
+// block of A) stages all of G's columns (<= 512; each thread loads column pairs as 4-B words) and
+// the block's A columns per 32-edge step into a double-buffered LDS slab (80 KiB, one barrier per
+// step); wave w owns i-tiles 8 (w % 4) .. +8 and j-tiles 4 (w / 4) .. +4 (32 accumulators).
+constexpr int kBI = 512;                // max G columns
+constexpr int kBGPart = 4 * kBI * 16;   // G slab (32 KiB)
+constexpr int kBAPart = 4 * kWJ * 16;   // A slab (8 KiB)
+constexpr int kBBuf = kBGPart + kBAPart;
+constexpr int kBLds = 2 * kBBuf;
+
+struct WbArgs {
+  const uint16_t* G;
+  const uint16_t* H;
+  const uint16_t* S;
+  const int64_t* src;
+  const int64_t* rev;
+  int64_t E, h;
+  int jblocks, ksplit, chunk_steps, xcds;
+  float alpha;
+  int act;
+  float* part;     // [ksplit][h][h]
+  float* part_db;  // [ksplit][h] or NULL
+};
+
+__device__ __forceinline__ float bfu(uint32_t u16) { return __uint_as_float(u16 << 16); }
+
+template <int ACT>
+__global__ void __launch_bounds__(512, 1) wgrad_bf16_kernel(WbArgs a) {
+  extern __shared__ __attribute__((aligned(16))) char lds[];
+  const int nb = gridDim.x;
+  int w = blockIdx.x;
+  if (a.xcds > 1 && nb % a.xcds == 0) w = (w % a.xcds) * (nb / a.xcds) + w / a.xcds;
+  const int y = w / a.jblocks, jb = w - y * a.jblocks;
+  const int64_t h = a.h, j0 = (int64_t)jb * kWJ;
+  const int64_t e_beg = (int64_t)y * a.chunk_steps * kK;
+  const int64_t e_end0 = e_beg + (int64_t)a.chunk_steps * kK;
+  const int64_t e_end = e_end0 < a.E ? e_end0 : a.E;
+  const int nsteps = e_end > e_beg ? (int)((e_end - e_beg + kK - 1) / kK) : 0;
+  const int t = threadIdx.x, lane = t & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(t >> 6);
+  const int ni16 = (int)((h + 15) / 16) * 16;
+  const int np = ni16 / 2;  // column pairs staged per edge group
+  const bool want_db = a.part_db != nullptr && jb == 0;
+
+  // G items: (column pair cp, group gg) for q = t + 512 m < 4 np
+  int cp[2], gg[2];
+  bool okg[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const int q = t + 512 * m;
+    okg[m] = q < 4 * np;
+    const int qq = okg[m] ? q : 0;
+    gg[m] = qq / np;
+    cp[m] = qq - gg[m] * np;
+  }
+  const int c1 = t & (kWJ - 1), ga = t >> 7;
+  const int64_t jc1 = j0 + c1 < h ? j0 + c1 : 0;
+  const bool okj = j0 + c1 < h;
+  float dbacc[2][2] = {{0.f, 0.f}, {0.f, 0.f}};
+
+  auto load_idx = [&](int s) __attribute__((always_inline)) -> int {
+    int64_t e = e_beg + (int64_t)s * kK + 8 * ga + (lane & 7);
+    e = e < e_end ? e : e_end - 1;
+    return lane >= 16 ? 0 : (int)(lane < 8 ? a.src[e] : a.rev[e]);
+  };
+  uint32_t xg[2][8], xs[8], xh[8];
+  int64_t eb_cur = 0;
+  const uint32_t* G32 = reinterpret_cast<const uint32_t*>(a.G);  // h even: column pairs are aligned words
+  auto load = [&](int s, int idxv) __attribute__((always_inline)) {
+    const int64_t eb = e_beg + (int64_t)s * kK;
+    eb_cur = eb;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      const int64_t col = 2 * cp[m] < h ? 2 * cp[m] : 0;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        int64_t e = eb + 8 * gg[m] + r;
+        e = e < e_end ? e : e_end - 1;
+        xg[m][r] = G32[(e * h + col) >> 1];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int64_t se = __builtin_amdgcn_readlane(idxv, r), re = __builtin_amdgcn_readlane(idxv, 8 + r);
+      xs[r] = a.S[se * h + jc1];
+      xh[r] = a.H[re * h + jc1];
+    }
+  };
+  auto store = [&](char* buf) __attribute__((always_inline)) {
+    char* gbase = buf;
+    char* abase = buf + kBGPart;
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      uint32_t lo[8], hi[8];
+      const bool in0 = okg[m] && 2 * cp[m] < h, in1 = okg[m] && 2 * cp[m] + 1 < h;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const bool ok = eb_cur + 8 * gg[m] + r < e_end;
+        lo[r] = (ok && in0) ? (xg[m][r] & 0xffffu) : 0u;
+        hi[r] = (ok && in1) ? (xg[m][r] >> 16) : 0u;
+      }
+      if (want_db) {
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+          dbacc[m][0] += bfu(lo[r]);
+          dbacc[m][1] += bfu(hi[r]);
+        }
+      }
+      if (okg[m]) {
+        uint4 v0, v1;
+        v0.x = lo[0] | (lo[1] << 16); v0.y = lo[2] | (lo[3] << 16); v0.z = lo[4] | (lo[5] << 16); v0.w = lo[6] | (lo[7] << 16);
+        v1.x = hi[0] | (hi[1] << 16); v1.y = hi[2] | (hi[3] << 16); v1.z = hi[4] | (hi[5] << 16); v1.w = hi[6] | (hi[7] << 16);
+        const int off = (gg[m] * kBI + 2 * cp[m]) * 16;
+        *reinterpret_cast<uint4*>(gbase + off) = v0;
+        *reinterpret_cast<uint4*>(gbase + off + 16) = v1;
+      }
+    }
+    bf16x8 av;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const bool ok = okj && eb_cur + 8 * ga + r < e_end;
+      const float v = bfu(xs[r] & 0xffffu) - act_t<ACT>(bfu(xh[r] & 0xffffu), a.act, a.alpha);
+      av[r] = (__bf16)(ok ? v : 0.f);
+    }
+    *reinterpret_cast<bf16x8*>(abase + (ga * kWJ + c1) * 16) = av;
+  };
+
+  const int fr = lane & 15, g16 = lane >> 4;
+  const int wi = wave & 3, wj = wave >> 2;  // i-tiles 8 wi .. 8 wi + 7, j-tiles 4 wj .. 4 wj + 3
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+#pragma unroll
+    for (int z = 0; z < 4; ++z) acc[x][z] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool active = 16 * 8 * wi < ni16 && j0 + 16 * 4 * wj < h;
+
+  int idx_next = 0;
+  if (nsteps > 0) {
+    load(0, load_idx(0));
+    if (nsteps > 1) idx_next = load_idx(1);
+    store(lds);
+  }
+  __syncthreads();
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps;
+    if (more) {
+      load(s + 1, idx_next);
+      if (s + 2 < nsteps) idx_next = load_idx(s + 2);
+    }
+    if (active) {
+      const char* gb = lds + (s & 1) * kBBuf;
+      const char* ab = gb + kBGPart;
+      bf16x8 fb[4];
+#pragma unroll
+      for (int z = 0; z < 4; ++z)
+        fb[z] = *reinterpret_cast<const bf16x8*>(ab + (g16 * kWJ + 16 * (4 * wj + z) + fr) * 16);
+#pragma unroll
+      for (int x = 0; x < 8; ++x) {
+        const bf16x8 fa = *reinterpret_cast<const bf16x8*>(gb + (g16 * kBI + 16 * (8 * wi + x) + fr) * 16);
+#pragma unroll
+        for (int z = 0; z < 4; ++z) acc[x][z] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[z], acc[x][z], 0, 0, 0);
+      }
+    }
+    if (more) store(lds + ((s + 1) & 1) * kBBuf);
+    __syncthreads();
+  }
+
+  float* P = a.part + (int64_t)y * h * h;
+#pragma unroll
+  for (int x = 0; x < 8; ++x)
+#pragma unroll
+    for (int z = 0; z < 4; ++z) {
+      const int64_t col = j0 + 16 * (4 * wj + z) + fr;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int64_t row = 16 * (8 * wi + x) + 4 * g16 + q;
+        if (row < h && col < h) P[row * h + col] = acc[x][z][q];
+      }
+    }
+  if (want_db) {  // fixed-order column sums over the 4 edge groups (deterministic)
+    float* red = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      if (okg[m]) {
+        red[gg[m] * kBI + 2 * cp[m]] = dbacc[m][0];
+        red[gg[m] * kBI + 2 * cp[m] + 1] = dbacc[m][1];
+      }
+    __syncthreads();
+    for (int c = t; c < h; c += 512)
+      a.part_db[(int64_t)y * h + c] = ((red[c] + red[kBI + c]) + red[2 * kBI + c]) + red[3 * kBI + c];
+  }
+}
+
 // out[i] = sum_y part[y][i] in ascending y (fixed order: deterministic)
 __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int64_t n,
                                                            int ksplit, float* __restrict__ out) {
@@ -749,9 +946,11 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
                                     void* dW_out, void* db_out, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_weight_grad: fp32 only");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "nt_dmpnn_weight_grad: fp32 or bf16");
   NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
   NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(dtype == NT_F32 || (h <= kBI && h % 2 == 0 && src && rev), NT_EUNSUPPORTED,
+             "nt_dmpnn_weight_grad: bf16 needs h <= 512, h even, src and rev");
   // row indices are narrowed to int for the lane broadcasts
   NT_REQUIRE(V < ((int64_t)1 << 31) && E < ((int64_t)1 << 31), NT_EUNSUPPORTED,
              "nt_dmpnn_weight_grad: V and E must be < 2^31");
@@ -783,6 +982,39 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
   a.act = act;
   a.part = (float*)workspace;
   a.part_db = db_out ? a.part + (int64_t)p.ksplit * h * h : nullptr;
+  if (dtype == NT_BF16) {
+    const WPlan q = make_wide_plan(E, h);
+    WbArgs b;
+    b.G = (const uint16_t*)G;
+    b.H = (const uint16_t*)H;
+    b.S = (const uint16_t*)S;
+    b.src = src;
+    b.rev = rev;
+    b.E = E;
+    b.h = h;
+    b.jblocks = (int)((h + kWJ - 1) / kWJ);
+    b.ksplit = q.ksplit;
+    b.chunk_steps = q.chunk_steps;
+    b.xcds = xcd_count();
+    b.alpha = act_alpha;
+    b.act = act;
+    b.part = (float*)workspace;
+    b.part_db = db_out ? b.part + (int64_t)q.ksplit * h * h : nullptr;
+    const int grid = b.jblocks * q.ksplit;
+    auto kern = act == NT_ACT_IDENTITY ? wgrad_bf16_kernel<NT_ACT_IDENTITY>
+                : act == NT_ACT_RELU   ? wgrad_bf16_kernel<NT_ACT_RELU>
+                                       : wgrad_bf16_kernel<-1>;
+    NT_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kBLds));
+    kern<<<grid, 512, kBLds, stream>>>(b);
+    NT_LAUNCH_CHECK();
+    wgrad_reduce_kernel<<<grid_for(h * h, 256, 256 * 8), 256, 0, stream>>>(b.part, h * h, q.ksplit, (float*)dW_out);
+    NT_LAUNCH_CHECK();
+    if (db_out) {
+      wgrad_reduce_kernel<<<grid_for(h, 256, 64), 256, 0, stream>>>(b.part_db, h, q.ksplit, (float*)db_out);
+      NT_LAUNCH_CHECK();
+    }
+    return NT_OK;
+  }
   if (src && h <= kWI) {  // the wide kernel: 128-column blocks of A against all of G
     const int jblocks = (int)((h + kWJ - 1) / kWJ);
     const WPlan q = make_wide_plan(E, h);

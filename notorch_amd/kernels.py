@@ -553,19 +553,24 @@ def dmpnn_row_table(perm: Tensor, dst_sorted: Tensor, src: Tensor, rev: Tensor, 
 
 def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None, *, kernel: str = "fk",
                  amax: Tensor | None = None) -> Tensor:
-    """X @ W^T for the packed image Wp of W (fp32, h % 4 == 0): the layer GEMM alone.  With
-    Wp = pack_weights(W.t()) it is the backward's dA = G @ W.  kernel = "fk": the fp16x3 layer kernel
-    in dense mode (amax: 2 device floats whose [1] >= max|X|, else nt_absmax first; any h); "pk": the
-    bf16x6 persistent kernel (h <= 304)."""
+    """X @ W^T for the packed image Wp of W: the layer GEMM alone.  With Wp = pack_weights(W.t()) it is
+    the backward's dA = G @ W.  fp32 (h % 4 == 0), kernel = "fk": the fp16x3 layer kernel in dense
+    mode (amax: 2 device floats whose [1] >= max|X|, else nt_absmax first; any h); "pk": the bf16x6
+    persistent kernel (h <= 304).  bf16 (h <= 512): the bf16 layer kernel without gathers (fp32
+    accumulate, one rounding)."""
     dev = _require_device(X, Wp, out, amax)
-    _require_f32("X", X)
+    code = _require_feat("X", X)
     M, h = X.shape
     if Wp.numel() != packed_weight_numel(h, X.dtype):
-        raise ValueError("Wp is not a packed fp32 weight image for this hidden size")
-    if not X.is_contiguous():
-        raise ValueError("dense_matmul: X must be contiguous")
+        raise ValueError(f"Wp is not a packed {X.dtype} weight image for this hidden size")
     if out is None:
         out = torch.empty_like(X)
+    if code == NT_BF16:
+        if h > 512:
+            raise ValueError("dense_matmul: bf16 needs h <= 512")
+        _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_BF16, None, _ptr(out),
+             _stream(dev))
+        return out
     if kernel == "fk":
         if amax is None:
             amax = torch.zeros(2, dtype=torch.float32, device=dev)
@@ -583,18 +588,21 @@ def weight_grad(G: Tensor, H: Tensor | None, S: Tensor, src: Tensor | None, rev:
                 act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0), bias: bool = True,
                 amax_G: Tensor | None = None, amax_HS: Tensor | None = None) -> tuple[Tensor, Tensor | None]:
     """(dW, db) = (G^T A, sum_e G[e]) with A[e] = S[src e] - act(H[rev e]) formed on the fly
-    (src = rev = None: A = S).  fp32, split-K, deterministic.  With amax_G (1 device float >= max|G|)
-    and amax_HS (2 floats >= max|H|, max|S|), h <= 320 and src / rev given: the two-part fp16 kernel
-    (nt_dmpnn_weight_grad_fk); else the bf16x6 kernel."""
+    (src = rev = None: A = S).  Split-K, deterministic.  fp32: with amax_G (1 device float >= max|G|)
+    and amax_HS (2 floats >= max|H|, max|S|), h <= 320 and src / rev given, the two-part fp16 kernel
+    (nt_dmpnn_weight_grad_fk); else the bf16x6 kernel.  bf16 (h <= 512, even, src / rev given): A
+    rounded to bf16 as the forward's message, one bf16 MFMA per tile; dW and db come back in fp32."""
     dev = _require_device(G, H, S, src, rev, amax_G, amax_HS)
-    _require_f32("G", G)
-    _require_f32("S", S)
+    code = _require_feat("G", G)
+    _require_feat("S", S, G.dtype)
+    if code == NT_BF16 and (src is None or G.shape[1] > 512 or G.shape[1] % 2):
+        raise ValueError("weight_grad: bf16 needs src / rev_index and an even h <= 512")
     E, h = G.shape
     if (src is None) != (rev is None):
         raise ValueError("weight_grad: pass both src and rev_index or neither")
     if src is not None:
         assert H is not None
-        _require_f32("H", H)
+        _require_feat("H", H, G.dtype)
         _require_i64("src", src)
         _require_i64("rev_index", rev)
         if H.shape != (E, h) or S.shape[1] != h or src.numel() != E or rev.numel() != E:
@@ -616,7 +624,7 @@ def weight_grad(G: Tensor, H: Tensor | None, S: Tensor, src: Tensor | None, rev:
     ws = torch.empty((max(nbytes, 4) + 3) // 4, dtype=torch.float32, device=dev)
     dW = torch.empty(h, h, dtype=torch.float32, device=dev)
     db = torch.empty(h, dtype=torch.float32, device=dev) if bias else None
-    if amax_G is not None and amax_HS is not None and src is not None and h <= 320:
+    if code == NT_F32 and amax_G is not None and amax_HS is not None and src is not None and h <= 320:
         _require_amax(amax_G, G.dtype, n=1)
         _require_amax(amax_HS, G.dtype)
         _run(dev, lib.nt_dmpnn_weight_grad_fk, _ptr(G), _ptr(H), _ptr(S), _ptr(src), _ptr(rev), S.shape[0], E,
@@ -624,7 +632,7 @@ def weight_grad(G: Tensor, H: Tensor | None, S: Tensor, src: Tensor | None, rev:
              _stream(dev))
         return dW, db
     _run(dev, lib.nt_dmpnn_weight_grad, _ptr(G), _ptr(H), _ptr(S), _ptr(src), _ptr(rev), S.shape[0], E, h,
-         act[0], act[1], NT_F32, _ptr(ws), ws.numel() * 4, _ptr(dW), _ptr(db), _stream(dev))
+         act[0], act[1], code, _ptr(ws), ws.numel() * 4, _ptr(dW), _ptr(db), _stream(dev))
     return dW, db
 
 

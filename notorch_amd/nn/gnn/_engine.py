@@ -674,6 +674,7 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
         fp32 = Gu.dtype == torch.float32
         fk_dense = fp32 and K.fused_supported(V, E, h, Gu.dtype)
         fk_wgrad = fp32 and wgrad == "kernel" and h <= 320
+        bf16_kernels = Gu.dtype == torch.bfloat16 and wgrad != "library" and h <= 512 and h % 8 == 0
         gmax = None
         if fk_dense or fk_wgrad:  # max|G|: the split scale of both fp16-split kernels
             gmax = torch.zeros(2, dtype=torch.float32, device=Gu.device)
@@ -690,6 +691,9 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
                     K.absmax(S_l.contiguous(), am[1:2])
             dWs[l], dbs[l] = K.weight_grad(Gu, H_l.contiguous(), S_l.contiguous(), src, rev, act=act,
                                            amax_G=None if am is None else gmax[1:2], amax_HS=am)
+        elif bf16_kernels:  # A rounded to bf16 in the kernel as the forward's message; fp32 partials
+            dW32, db32 = K.weight_grad(Gu, H_l.contiguous(), S_l.contiguous(), src, rev, act=act)
+            dWs[l], dbs[l] = dW32.to(Gu.dtype), db32.to(Gu.dtype)
         else:
             A = K.dmpnn_message(H_l, S_l, src, rev, act=act)
             dWs[l] = _weight_grad(Gu, A)
@@ -697,6 +701,8 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             del A
         if fk_dense:
             dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous(), fk_only=True), amax=gmax)
+        elif bf16_kernels:  # the bf16 layer kernel without gathers
+            dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous()))
         else:
             dA = torch.mm(Gu, W)
         del Gu

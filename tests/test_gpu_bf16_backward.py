@@ -159,3 +159,45 @@ def test_block_grads_bf16(kind, n, h, depth, act, reduce, monkeypatch):
         print(f"{name}: kernel max {e_max:.2e} l2 {e_l2:.2e} | torch bf16 max {r_max:.2e} l2 {r_l2:.2e}")
         assert e_max <= max(BF16_FLOOR, BF16_FACTOR * r_max), f"{name}: max {e_max:.3e} vs torch bf16 {r_max:.3e}"
         assert e_l2 <= max(BF16_FLOOR, BF16_FACTOR * r_l2), f"{name}: L2 {e_l2:.3e} vs torch bf16 {r_l2:.3e}"
+
+
+@pytest.mark.parametrize("h,E,act", [(512, 20_000, "relu"), (64, 4097, "identity"), (128, 33, "gelu"),
+                                     (96, 1, "relu"), (400, 3000, "tanh")])
+def test_weight_grad_bf16(h, E, act):
+    """nt_dmpnn_weight_grad on bf16 storage (config 3's dW = G^T A, db = colsum G): A formed in fp32
+    and rounded to bf16 once (bit-identical to nt_dmpnn_message), exact bf16 products, fp32
+    accumulation: within the fp32 contract of the fp64 product of the same bf16 operands; repeat
+    bit-identical."""
+    from helpers import FP32_NORM_TOL
+    from notorch_amd import kernels as K
+
+    mods = {"relu": nn.ReLU(), "identity": nn.Identity(), "gelu": nn.GELU(), "tanh": nn.Tanh()}
+    mod = mods[act]
+    g = torch.Generator().manual_seed(E + h)
+    V = max(E // 2, 1)
+    Gr = torch.randn(E, h, generator=g).to(BF16)
+    H, S = torch.randn(E, h, generator=g).to(BF16), torch.randn(V, h, generator=g).to(BF16)
+    src = torch.randint(0, V, (E,), generator=g)
+    rev = torch.randint(0, E, (E,), generator=g)
+    args = (Gr.to(DEV), H.to(DEV), S.to(DEV), src.to(DEV), rev.to(DEV))
+    dW, db = K.weight_grad(*args, act=K.act_code(mod))
+    A = K.dmpnn_message(args[1], args[2], args[3], args[4], act=K.act_code(mod)).cpu()  # bf16 message
+    assert dW.dtype == torch.float32
+    assert_parity(dW, Gr.double().t() @ A.double(), FP32_NORM_TOL, f"dW h={h} E={E} {act}")
+    assert_parity(db, Gr.double().sum(0), FP32_NORM_TOL, f"db h={h} E={E}")
+    dW2, db2 = K.weight_grad(*args, act=K.act_code(mod))
+    assert torch.equal(dW, dW2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("h,M", [(512, 20_000), (64, 100), (200, 7)])
+def test_dense_matmul_bf16(h, M):
+    """dA = G W on the bf16 layer kernel's dense mode: fp32 accumulation of exact bf16 products,
+    one rounding (within one bf16 ulp of the fp64 product, normalised)."""
+    from notorch_amd import kernels as K
+
+    g = torch.Generator().manual_seed(M + h)
+    X = torch.randn(M, h, generator=g).to(BF16)
+    W = (torch.randn(h, h, generator=g) / h ** 0.5).to(BF16)
+    out = K.dense_matmul(X.to(DEV), K.pack_weights(W.t().contiguous().to(DEV)))
+    assert out.dtype == BF16
+    assert_parity(out, X.double() @ W.double(), ULP, f"dense bf16 h={h} M={M}")
