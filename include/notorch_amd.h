@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define NT_ABI_VERSION 2
+#define NT_ABI_VERSION 3
 
 #if defined(NT_BUILD)
 #define NT_API __attribute__((visibility("default")))
@@ -337,21 +337,25 @@ NT_API int nt_dmpnn_message(const void* H, const void* S, const int64_t* src, co
  * G = dL/dH_{l+1}; H = H_l; dA = G W; dS = nt_segment_reduce(dA, src CSR, sum);
  * (rev_ptr, rev_perm) = nt_csr_build(rev_index, E, E); c(v) = max(in-degree, 1) for
  * reduce = NT_MEAN (dst_ptr required), 1 for NT_SUM.  max/min are not covered (NT_EUNSUPPORTED).
+ * amax_out (fp32, may be NULL; ignored for bf16): one zero-filled device float raised to max|G_out|,
+ * the split scale of the backward's fp16-split kernels (nt_dmpnn_weight_grad_fk, dense dA).
  */
 NT_API int nt_dmpnn_edge_backward(const void* G, const void* H, const void* dA, const void* dS,
                                   const int64_t* dst, const int32_t* rev_ptr, const int32_t* rev_perm,
                                   const int32_t* dst_ptr, int64_t V, int64_t E, int64_t h,
                                   int residual, int act, float act_alpha, int reduce, int dtype,
-                                  void* G_out, void* stream);
+                                  void* G_out, float* amax_out, void* stream);
 
 /*
  * Row gather with optional base and mean scaling (backward of a sum/mean scatter):
  *   out[i] = (base ? base[i] : 0) + X[idx[i]] / (seg_ptr ? max(seg_ptr[idx+1] - seg_ptr[idx], 1) : 1)
  * Used for dL/dH_d += dnode[dst] (chemprop.py:86) and the Sum/Mean readout backward
  * (agg.py:23-38, idx = batch_node_index, seg_ptr = molecule CSR for mean).
+ * amax_out: as nt_dmpnn_edge_backward (max|out|).
  */
 NT_API int nt_gather_rows(const void* base, const void* X, const int64_t* idx, const int32_t* seg_ptr,
-                          int64_t n, int64_t nseg, int64_t h, int dtype, void* out, void* stream);
+                          int64_t n, int64_t nseg, int64_t h, int dtype, void* out, float* amax_out,
+                          void* stream);
 
 /* Dropout of the layer update fused with its residual add: replaces `nn.Dropout(p)` inside
  * ChempropLayer.update (notorch/nn/gnn/chemprop.py:26, applied at :42) followed by
@@ -371,7 +375,7 @@ NT_API int nt_dropout_residual(const void* base, const void* Y, int64_t n, float
  *   nt_dmpnn_edge_backward_arg: nt_dmpnn_edge_backward with the dS term masked by arg (reduce of the
  *                               layer's aggregation = max | min): (arg[dst e][c] == e ? dS[dst e][c] : 0)
  *   nt_gather_rows_arg:         out[i] = (base ? base[i] : 0) + (arg[idx i] == i ? X[idx i] : 0)
- * fp32 only. */
+ * fp32 only; amax_out as nt_dmpnn_edge_backward. */
 NT_API int nt_segment_arg(const void* X, const int32_t* seg_ptr, const int32_t* perm, int64_t nseg,
                           int64_t h, int reduce, int act, float act_alpha, int dtype, int32_t* arg,
                           void* stream);
@@ -379,9 +383,9 @@ NT_API int nt_dmpnn_edge_backward_arg(const void* G, const void* H, const void* 
                                       const int32_t* arg, const int64_t* dst, const int32_t* rev_ptr,
                                       const int32_t* rev_perm, int64_t V, int64_t E, int64_t h,
                                       int residual, int act, float act_alpha, int dtype, void* G_out,
-                                      void* stream);
+                                      float* amax_out, void* stream);
 NT_API int nt_gather_rows_arg(const void* base, const void* X, const int64_t* idx, const int32_t* arg,
-                              int64_t n, int64_t h, int dtype, void* out, void* stream);
+                              int64_t n, int64_t h, int dtype, void* out, float* amax_out, void* stream);
 
 /* Dense layer GEMM, the backward's dA = G W of nn.Linear (chemprop.py:26,41), trained through
  * lightning_models/model.py:224-241 (the reference runs it as ATen addmm's autograd):

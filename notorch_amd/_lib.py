@@ -17,7 +17,7 @@ _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # environment variables, ablation / stamp builds); the default is the shipping library.
 DIAG = os.environ.get("NT_LIB", "") == "diag"
 LIB_PATH = os.path.join(_LIB_DIR, "libnotorch_amd_diag.so" if DIAG else "libnotorch_amd.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 NT_F32, NT_BF16 = 0, 1
 NT_SUM, NT_MEAN, NT_MAX, NT_MIN = 0, 1, 2, 3
@@ -104,18 +104,18 @@ SIGNATURES: dict[str, tuple] = {
     "nt_dmpnn_edge_backward": (
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32,
-         _c_int, _c_int, _vp, _vp],
+         _c_int, _c_int, _vp, _vp, _vp],
     ),
-    "nt_gather_rows": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp]),
+    "nt_gather_rows": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),
     "nt_dropout_residual": (_c_int, [_vp, _vp, _c_i64, ctypes.c_float, ctypes.c_uint64, ctypes.c_uint64,
                                      _c_int, _vp, _vp]),
     "nt_segment_arg": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp]),
     "nt_dmpnn_edge_backward_arg": (
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp,
-         _vp],
+         _vp, _vp],
     ),
-    "nt_gather_rows_arg": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_int, _vp, _vp]),
+    "nt_gather_rows_arg": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),
     "nt_dmpnn_dense_matmul": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, _vp, _vp]),
     "nt_dmpnn_weight_grad_workspace": (_c_i64, [_c_i64, _c_i64]),
     "nt_dmpnn_weight_grad": (

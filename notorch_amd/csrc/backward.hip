@@ -89,14 +89,21 @@ __global__ void __launch_bounds__(256) message_kernel(const T* __restrict__ H, c
   }
 }
 
+// max |x| over a value's components (the amax outputs: the backward's fp16-split scales)
+__device__ __forceinline__ float vamax(float x) { return fabsf(x); }
+__device__ __forceinline__ float vamax(float4 x) {
+  return fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w)));
+}
+
 // ------------------------------------------------------------------------------ edge backward
 template <typename T, int ACT, bool MEAN>
 __global__ void __launch_bounds__(256) edge_backward_kernel(
     const T* __restrict__ G, const T* __restrict__ H, const T* __restrict__ dA,
     const T* __restrict__ dS, const int64_t* __restrict__ dst, const int32_t* __restrict__ rev_ptr,
     const int32_t* __restrict__ rev_perm, const int32_t* __restrict__ dst_ptr, int64_t E,
-    int64_t hw, int residual, int act, float alpha, T* __restrict__ Gout) {
+    int64_t hw, int residual, int act, float alpha, T* __restrict__ Gout, float* __restrict__ amax) {
   const int64_t total = E * hw;
+  float m = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = t / hw, c = t - e * hw;
@@ -111,7 +118,9 @@ __global__ void __launch_bounds__(256) edge_backward_kernel(
     T g = vmul(vgrad<ACT>(H[t], act, alpha), dm);
     if (residual) g = g + G[t];
     Gout[t] = g;
+    m = fmaxf(m, vamax(g));
   }
+  if (amax) block_max_to(amax, m);
 }
 
 // ------------------------------------------------------------------------------ gather rows
@@ -120,8 +129,10 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const T* __restrict__ 
                                                           const T* __restrict__ X,
                                                           const int64_t* __restrict__ idx,
                                                           const int32_t* __restrict__ seg_ptr,
-                                                          int64_t n, int64_t hw, T* __restrict__ out) {
+                                                          int64_t n, int64_t hw, T* __restrict__ out,
+                                                          float* __restrict__ amax) {
   const int64_t total = n * hw;
+  float m = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = t / hw, c = t - i * hw;
@@ -131,8 +142,11 @@ __global__ void __launch_bounds__(256) gather_rows_kernel(const T* __restrict__ 
       const int cnt = seg_ptr[s + 1] - seg_ptr[s];
       x = vmul(x, vfill(x, 1.f / (float)(cnt > 1 ? cnt : 1)));
     }
-    out[t] = base ? base[t] + x : x;
+    const T y = base ? base[t] + x : x;
+    out[t] = y;
+    m = fmaxf(m, vamax(y));
   }
+  if (amax) block_max_to(amax, m);
 }
 
 // ------------------------------------------------------------------------------ max / min
@@ -176,8 +190,9 @@ __global__ void __launch_bounds__(256) edge_backward_arg_kernel(
     const T* __restrict__ G, const T* __restrict__ H, const T* __restrict__ dA,
     const T* __restrict__ dS, const TI* __restrict__ arg, const int64_t* __restrict__ dst,
     const int32_t* __restrict__ rev_ptr, const int32_t* __restrict__ rev_perm, int64_t E, int64_t hw,
-    int residual, int act, float alpha, T* __restrict__ Gout) {
+    int residual, int act, float alpha, T* __restrict__ Gout, float* __restrict__ amax) {
   const int64_t total = E * hw;
+  float m = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = t / hw, c = t - e * hw;
@@ -188,7 +203,9 @@ __global__ void __launch_bounds__(256) edge_backward_arg_kernel(
     T g = vmul(vgrad<ACT>(H[t], act, alpha), dm);
     if (residual) g = g + G[t];
     Gout[t] = g;
+    m = fmaxf(m, vamax(g));
   }
+  if (amax) block_max_to(amax, m);
 }
 
 // out[i] = (base ? base[i] : 0) + (arg[idx i] == i ? X[idx i] : 0): backward of a max/min scatter
@@ -198,15 +215,20 @@ __global__ void __launch_bounds__(256) gather_rows_arg_kernel(const T* __restric
                                                               const T* __restrict__ X,
                                                               const int64_t* __restrict__ idx,
                                                               const TI* __restrict__ arg, int64_t n,
-                                                              int64_t hw, T* __restrict__ out) {
+                                                              int64_t hw, T* __restrict__ out,
+                                                              float* __restrict__ amax) {
   const int64_t total = n * hw;
+  float m = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t i = t / hw, c = t - i * hw;
     const int64_t s = idx[i];
     const T x = arg_mask(X[s * hw + c], arg[s * hw + c], i);
-    out[t] = base ? base[t] + x : x;
+    const T y = base ? base[t] + x : x;
+    out[t] = y;
+    m = fmaxf(m, vamax(y));
   }
+  if (amax) block_max_to(amax, m);
 }
 
 // ---- bf16 storage (bf16 training): same math in fp32 registers, one rounding per stored element ----
@@ -356,7 +378,7 @@ extern "C" int nt_dmpnn_edge_backward(const void* G, const void* H, const void* 
                                       const int64_t* dst, const int32_t* rev_ptr,
                                       const int32_t* rev_perm, const int32_t* dst_ptr, int64_t V,
                                       int64_t E, int64_t h, int residual, int act, float act_alpha,
-                                      int reduce, int dtype, void* G_out, void* stream_) {
+                                      int reduce, int dtype, void* G_out, float* amax_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
@@ -393,7 +415,7 @@ extern "C" int nt_dmpnn_edge_backward(const void* G, const void* H, const void* 
   NT_BW_DISPATCH_ACT(act, (edge_backward_kernel<float4, A_, MEAN_><<<grid, 256, 0, stream>>>(     \
                               (const float4*)G, (const float4*)H, (const float4*)dA,              \
                               (const float4*)dS, dst, rev_ptr, rev_perm, dst_ptr, E, hw, residual, \
-                              act, act_alpha, (float4*)G_out)))
+                              act, act_alpha, (float4*)G_out, amax_out)))
     if (mean) NT_EB_LAUNCH(true); else NT_EB_LAUNCH(false);
 #undef NT_EB_LAUNCH
   } else {
@@ -402,7 +424,7 @@ extern "C" int nt_dmpnn_edge_backward(const void* G, const void* H, const void* 
   NT_BW_DISPATCH_ACT(act, (edge_backward_kernel<float, A_, MEAN_><<<grid, 256, 0, stream>>>(    \
                               (const float*)G, (const float*)H, (const float*)dA, (const float*)dS, \
                               dst, rev_ptr, rev_perm, dst_ptr, E, h, residual, act, act_alpha,   \
-                              (float*)G_out)))
+                              (float*)G_out, amax_out)))
     if (mean) NT_EB_LAUNCH(true); else NT_EB_LAUNCH(false);
 #undef NT_EB_LAUNCH
   }
@@ -412,7 +434,7 @@ extern "C" int nt_dmpnn_edge_backward(const void* G, const void* H, const void* 
 
 extern "C" int nt_gather_rows(const void* base, const void* X, const int64_t* idx,
                               const int32_t* seg_ptr, int64_t n, int64_t nseg, int64_t h, int dtype,
-                              void* out, void* stream_) {
+                              void* out, float* amax_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
@@ -439,18 +461,18 @@ extern "C" int nt_gather_rows(const void* base, const void* X, const int64_t* id
     const int grid = grid_for(n * hw, 256, 256 * 32);
     if (mean)
       gather_rows_kernel<float4, true><<<grid, 256, 0, stream>>>(
-          (const float4*)base, (const float4*)X, idx, seg_ptr, n, hw, (float4*)out);
+          (const float4*)base, (const float4*)X, idx, seg_ptr, n, hw, (float4*)out, amax_out);
     else
       gather_rows_kernel<float4, false><<<grid, 256, 0, stream>>>(
-          (const float4*)base, (const float4*)X, idx, seg_ptr, n, hw, (float4*)out);
+          (const float4*)base, (const float4*)X, idx, seg_ptr, n, hw, (float4*)out, amax_out);
   } else {
     const int grid = grid_for(n * h, 256, 256 * 32);
     if (mean)
       gather_rows_kernel<float, true><<<grid, 256, 0, stream>>>(
-          (const float*)base, (const float*)X, idx, seg_ptr, n, h, (float*)out);
+          (const float*)base, (const float*)X, idx, seg_ptr, n, h, (float*)out, amax_out);
     else
       gather_rows_kernel<float, false><<<grid, 256, 0, stream>>>(
-          (const float*)base, (const float*)X, idx, seg_ptr, n, h, (float*)out);
+          (const float*)base, (const float*)X, idx, seg_ptr, n, h, (float*)out, amax_out);
   }
   NT_LAUNCH_CHECK();
   return NT_OK;
@@ -482,7 +504,7 @@ extern "C" int nt_dmpnn_edge_backward_arg(const void* G, const void* H, const vo
                                           const int32_t* arg, const int64_t* dst,
                                           const int32_t* rev_ptr, const int32_t* rev_perm, int64_t V,
                                           int64_t E, int64_t h, int residual, int act, float act_alpha,
-                                          int dtype, void* G_out, void* stream_) {
+                                          int dtype, void* G_out, float* amax_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_edge_backward_arg: fp32 only");
@@ -499,20 +521,20 @@ extern "C" int nt_dmpnn_edge_backward_arg(const void* G, const void* H, const vo
     NT_BW_DISPATCH_ACT(act, (edge_backward_arg_kernel<float4, int4, A_><<<grid, 256, 0, stream>>>(
                                 (const float4*)G, (const float4*)H, (const float4*)dA, (const float4*)dS,
                                 (const int4*)arg, dst, rev_ptr, rev_perm, E, hw, residual, act,
-                                act_alpha, (float4*)G_out)));
+                                act_alpha, (float4*)G_out, amax_out)));
   } else {
     const int grid = grid_for(E * h, 256, 256 * 32);
     NT_BW_DISPATCH_ACT(act, (edge_backward_arg_kernel<float, int, A_><<<grid, 256, 0, stream>>>(
                                 (const float*)G, (const float*)H, (const float*)dA, (const float*)dS,
                                 arg, dst, rev_ptr, rev_perm, E, h, residual, act, act_alpha,
-                                (float*)G_out)));
+                                (float*)G_out, amax_out)));
   }
   NT_LAUNCH_CHECK();
   return NT_OK;
 }
 
 extern "C" int nt_gather_rows_arg(const void* base, const void* X, const int64_t* idx, const int32_t* arg,
-                                  int64_t n, int64_t h, int dtype, void* out, void* stream_) {
+                                  int64_t n, int64_t h, int dtype, void* out, float* amax_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_gather_rows_arg: fp32 only");
@@ -523,10 +545,10 @@ extern "C" int nt_gather_rows_arg(const void* base, const void* X, const int64_t
   if (h % 4 == 0 && aligned16(X) && aligned16(out) && aligned16(arg) && (!base || aligned16(base))) {
     const int64_t hw = h / 4;
     gather_rows_arg_kernel<float4, int4><<<grid_for(n * hw, 256, 256 * 32), 256, 0, stream>>>(
-        (const float4*)base, (const float4*)X, idx, (const int4*)arg, n, hw, (float4*)out);
+        (const float4*)base, (const float4*)X, idx, (const int4*)arg, n, hw, (float4*)out, amax_out);
   } else {
     gather_rows_arg_kernel<float, int><<<grid_for(n * h, 256, 256 * 32), 256, 0, stream>>>(
-        (const float*)base, (const float*)X, idx, arg, n, h, (float*)out);
+        (const float*)base, (const float*)X, idx, arg, n, h, (float*)out, amax_out);
   }
   NT_LAUNCH_CHECK();
   return NT_OK;

@@ -655,9 +655,10 @@ def segment_arg(X: Tensor, seg_ptr: Tensor, perm: Tensor | None, nseg: int, redu
 
 def dmpnn_edge_backward_arg(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor, arg: Tensor, dst: Tensor,
                             rev_ptr: Tensor, rev_perm: Tensor, *, residual: bool = True,
-                            act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0)) -> Tensor:
-    """dL/dH_l for a max / min aggregation (arg = segment_arg of act(H_l) over the dst CSR)."""
-    dev = _require_device(G, H, dA, dS, arg, dst, rev_ptr, rev_perm)
+                            act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0), amax: Tensor | None = None) -> Tensor:
+    """dL/dH_l for a max / min aggregation (arg = segment_arg of act(H_l) over the dst CSR); amax (1
+    zero-filled device float, optional) is raised to max|out|."""
+    dev = _require_device(G, H, dA, dS, arg, dst, rev_ptr, rev_perm, amax)
     for n_, t in (("H", H), ("dA", dA), ("dS", dS)):
         _require_f32(n_, t)
     E, h = H.shape
@@ -665,18 +666,20 @@ def dmpnn_edge_backward_arg(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor,
     out = torch.empty_like(H)
     _run(dev, _lib.load().nt_dmpnn_edge_backward_arg, _ptr(G), _ptr(H), _ptr(dA), _ptr(dS), _ptr(arg),
          _ptr(dst), _ptr(rev_ptr), _ptr(rev_perm), V, E, h, int(residual), act[0], act[1], NT_F32,
-         _ptr(out), _stream(dev))
+         _ptr(out), _ptr(amax), _stream(dev))
     return out
 
 
-def gather_rows_arg(X: Tensor, idx: Tensor, arg: Tensor, *, base: Tensor | None = None) -> Tensor:
-    """out[i] = base[i] + (arg[idx i] == i ? X[idx i] : 0) (max / min scatter backward)."""
-    dev = _require_device(X, idx, arg, base)
+def gather_rows_arg(X: Tensor, idx: Tensor, arg: Tensor, *, base: Tensor | None = None,
+                    amax: Tensor | None = None) -> Tensor:
+    """out[i] = base[i] + (arg[idx i] == i ? X[idx i] : 0) (max / min scatter backward); amax as
+    dmpnn_edge_backward_arg."""
+    dev = _require_device(X, idx, arg, base, amax)
     _require_f32("X", X)
     n, h = idx.numel(), X.shape[1]
     out = torch.empty(n, h, dtype=X.dtype, device=dev)
     _run(dev, _lib.load().nt_gather_rows_arg, _ptr(base), _ptr(X), _ptr(idx), _ptr(arg), n, h, NT_F32,
-         _ptr(out), _stream(dev))
+         _ptr(out), _ptr(amax), _stream(dev))
     return out
 
 
@@ -705,9 +708,10 @@ def dmpnn_message(H: Tensor, S: Tensor, src: Tensor, rev: Tensor, *,
 def dmpnn_edge_backward(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor, dst: Tensor,
                         rev_ptr: Tensor, rev_perm: Tensor, dst_ptr: Tensor | None, *,
                         residual: bool = True, act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
-                        reduce: str = "sum", out: Tensor | None = None) -> Tensor:
-    """dL/dH_l = (residual ? G : 0) + act'(H) * (dS[dst] / c - scatter(dA, rev))  (see header)."""
-    dev = _require_device(G, H, dA, dS, dst, rev_ptr, rev_perm, dst_ptr, out)
+                        reduce: str = "sum", out: Tensor | None = None, amax: Tensor | None = None) -> Tensor:
+    """dL/dH_l = (residual ? G : 0) + act'(H) * (dS[dst] / c - scatter(dA, rev))  (see header); fp32:
+    amax (1 zero-filled device float, optional) is raised to max|out|."""
+    dev = _require_device(G, H, dA, dS, dst, rev_ptr, rev_perm, dst_ptr, out, amax)
     code = _require_feat("H", H)
     for name, t in (("dA", dA), ("dS", dS)):
         _require_feat(name, t, H.dtype)
@@ -729,15 +733,15 @@ def dmpnn_edge_backward(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor, dst
     _run(dev, _lib.load().nt_dmpnn_edge_backward,
          _ptr(G if residual else None), _ptr(H), _ptr(dA), _ptr(dS), _ptr(dst), _ptr(rev_ptr),
          _ptr(rev_perm), _ptr(dst_ptr), V, E, h, int(residual), act[0], act[1], reduce_code(reduce),
-         code, _ptr(out), _stream(dev))
+         code, _ptr(out), _ptr(amax), _stream(dev))
     return out
 
 
 def gather_rows(X: Tensor, idx: Tensor, *, base: Tensor | None = None, seg_ptr: Tensor | None = None,
-                out: Tensor | None = None) -> Tensor:
+                out: Tensor | None = None, amax: Tensor | None = None) -> Tensor:
     """out[i] = (base[i] if base is given) + X[idx[i]], divided by max(segment size of idx[i], 1)
-    when ``seg_ptr`` is given (the backward of a mean scatter)."""
-    dev = _require_device(X, idx, base, seg_ptr, out)
+    when ``seg_ptr`` is given (the backward of a mean scatter); fp32: amax as dmpnn_edge_backward."""
+    dev = _require_device(X, idx, base, seg_ptr, out, amax)
     code = _require_feat("X", X)
     _require_i64("idx", idx)
     nseg, h = X.shape
@@ -753,7 +757,7 @@ def gather_rows(X: Tensor, idx: Tensor, *, base: Tensor | None = None, seg_ptr: 
     else:
         _require_feat("out", out, X.dtype)
     _run(dev, _lib.load().nt_gather_rows,
-         _ptr(base), _ptr(X), _ptr(idx), _ptr(seg_ptr), n, nseg, h, code, _ptr(out), _stream(dev))
+         _ptr(base), _ptr(X), _ptr(idx), _ptr(seg_ptr), n, nseg, h, code, _ptr(out), _ptr(amax), _stream(dev))
     return out
 
 

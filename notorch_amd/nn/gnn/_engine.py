@@ -655,12 +655,18 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
         G = torch.zeros(E, h, dtype=dnode.dtype, device=src.device)
     else:
         G = dH.contiguous()
+    # fp32: max|G| of the current G, raised by the kernel that writes G (the fp16-split kernels'
+    # scale); None = unknown (nt_absmax computes it)
+    fp32 = G.dtype == torch.float32
+    gmax_cur = None
     if dnode is not None:
+        gmax_cur = torch.zeros(2, dtype=torch.float32, device=src.device) if fp32 else None
+        g1 = None if gmax_cur is None else gmax_cur[1:2]
         if maxmin:  # chemprop.py:86 with scatter_max / scatter_min
             arg = K.segment_arg(H_last, lay.dst_ptr, lay.dst_perm, V, reduce)
-            G = K.gather_rows_arg(dnode.contiguous(), dst, arg, base=G)
+            G = K.gather_rows_arg(dnode.contiguous(), dst, arg, base=G, amax=g1)
         else:
-            G = K.gather_rows(dnode.contiguous(), dst, base=G, seg_ptr=mean_ptr)
+            G = K.gather_rows(dnode.contiguous(), dst, base=G, seg_ptr=mean_ptr, amax=g1)
     d = len(weights)
     dWs: list = [None] * d
     dbs: list = [None] * d
@@ -671,12 +677,11 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
         # dropout: the update's gradient is keep * G / (1 - p); the residual path keeps G
         Gu = G if drop is None else K.dropout_residual(G, drop[0], drop[1], dropout_offset(l, E, h))
         Gu = Gu.contiguous()
-        fp32 = Gu.dtype == torch.float32
         fk_dense = fp32 and K.fused_supported(V, E, h, Gu.dtype)
         fk_wgrad = fp32 and wgrad == "kernel" and h <= 320
         bf16_kernels = Gu.dtype == torch.bfloat16 and wgrad != "library" and h <= 512 and h % 8 == 0
-        gmax = None
-        if fk_dense or fk_wgrad:  # max|G|: the split scale of both fp16-split kernels
+        gmax = gmax_cur if drop is None else None  # dropout rescales G: its max is taken afresh
+        if (fk_dense or fk_wgrad) and gmax is None:  # max|G|: the split scale of both fp16-split kernels
             gmax = torch.zeros(2, dtype=torch.float32, device=Gu.device)
             K.absmax(Gu, gmax[1:2])
         if fp32 and wgrad in ("kernel", "kernel6"):
@@ -707,13 +712,15 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             dA = torch.mm(Gu, W)
         del Gu
         dS = K.segment_reduce(dA, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY)
+        gmax_cur = torch.zeros(2, dtype=torch.float32, device=G.device) if fp32 and l > 0 else None
+        g1 = None if gmax_cur is None else gmax_cur[1:2]
         if maxmin:  # chemprop.py:39 with scatter_max / scatter_min: the arg of act(H_l) per node
             arg = K.segment_arg(H_l, lay.dst_ptr, lay.dst_perm, V, reduce, act=act)
             G = K.dmpnn_edge_backward_arg(G, H_l, dA, dS, arg, dst, rev_ptr, rev_perm,
-                                          residual=residual, act=act)
+                                          residual=residual, act=act, amax=g1)
         else:
             G = K.dmpnn_edge_backward(G, H_l, dA, dS, dst, rev_ptr, rev_perm, lay.dst_ptr,
-                                      residual=residual, act=act, reduce=reduce)
+                                      residual=residual, act=act, reduce=reduce, amax=g1)
     dXv = K.segment_reduce(G, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY) if need_x[0] else None
     return dXv, G if need_x[1] else None, dWs, dbs
 

@@ -47,7 +47,7 @@ def test_abi_version_and_errors_without_gpu():
     from notorch_amd import _lib
 
     lib = _lib.load()
-    assert lib.nt_abi_version() == _lib.ABI_VERSION == 2
+    assert lib.nt_abi_version() == _lib.ABI_VERSION == 3
     assert lib.nt_dmpnn_packed_weight_bytes(300, 0) > 0
     assert lib.nt_dmpnn_packed_weight_bytes(0, 0) == 0
     # argument validation happens before any device call: EINVAL + message
@@ -68,11 +68,11 @@ def test_abi_version_and_errors_without_gpu():
     assert rc == 1
     # backward entry points validate before touching the device
     rc = lib.nt_dmpnn_edge_backward(None, None, None, None, None, None, None, None, 4, 8, 16, 1, 1,
-                                    0.0, 2, 0, None, None)
+                                    0.0, 2, 0, None, None, None)
     assert rc == 3 and b"sum | mean" in lib.nt_last_error()  # max/min backward: not a kernel
     rc = lib.nt_dmpnn_message(None, None, None, None, 4, 8, 16, 99, 0.0, 0, None, None)
     assert rc == 1
-    rc = lib.nt_gather_rows(None, None, None, None, -1, 4, 8, 0, None, None)
+    rc = lib.nt_gather_rows(None, None, None, None, -1, 4, 8, 0, None, None, None)
     assert rc == 1
 
 
