@@ -163,13 +163,15 @@ NT_API int nt_segment_reduce(const void* X, const int32_t* seg_ptr, const int32_
  * straddle a segment; segment s owns chunks [chunk_ptr[s], chunk_ptr[s+1]) (none when empty).
  * Pass 1 reduces every chunk into partial (nchunks x h fp32 workspace), pass 2 combines each
  * segment's partials in chunk order (mean divides by seg_ptr's count).  Same result as
- * nt_segment_reduce up to fp32 reassociation at chunk boundaries; deterministic.
+ * nt_segment_reduce up to fp32 reassociation at chunk boundaries; deterministic.  amax_out (fp32,
+ * may be NULL; ignored for bf16): one zero-filled device float raised to max|out| (the first layer's
+ * split scale on hub graphs).
  */
 NT_API int nt_segment_reduce_chunked(const void* X, const int32_t* perm, const int32_t* chunk_pos,
                                      int64_t nchunks, const int32_t* chunk_ptr,
                                      const int32_t* seg_ptr, int64_t nseg, int64_t h, int reduce,
                                      int act, float act_alpha, int dtype, float* partial, void* out,
-                                     void* stream);
+                                     float* amax_out, void* stream);
 
 /* Bytes of the packed weight image for one h x h layer (see nt_dmpnn_pack_weight). */
 NT_API size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype);

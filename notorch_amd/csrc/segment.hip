@@ -161,24 +161,34 @@ __global__ void __launch_bounds__(256) init_aggregate_scalar(
 __global__ void __launch_bounds__(256) init_only_vec4(const float4* __restrict__ Xv,
                                                       const float4* __restrict__ Xe,
                                                       const int64_t* __restrict__ src, int64_t E,
-                                                      int64_t hv, float4* __restrict__ H0) {
+                                                      int64_t hv, float4* __restrict__ H0,
+                                                      float* __restrict__ amax) {
   const int64_t total = E * hv;
+  float m = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = t / hv, c = t - e * hv;
-    H0[t] = Xv[src[e] * hv + c] + Xe[t];
+    const float4 y = Xv[src[e] * hv + c] + Xe[t];
+    H0[t] = y;
+    m = fmaxf(m, fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
   }
+  if (amax) block_max_to(amax, m);
 }
 __global__ void __launch_bounds__(256) init_only_scalar(const float* __restrict__ Xv,
                                                         const float* __restrict__ Xe,
                                                         const int64_t* __restrict__ src, int64_t E,
-                                                        int64_t h, float* __restrict__ H0) {
+                                                        int64_t h, float* __restrict__ H0,
+                                                        float* __restrict__ amax) {
   const int64_t total = E * h;
+  float m = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = t / h, c = t - e * h;
-    H0[t] = Xv[src[e] * h + c] + Xe[t];
+    const float y = Xv[src[e] * h + c] + Xe[t];
+    H0[t] = y;
+    m = fmaxf(m, fabsf(y));
   }
+  if (amax) block_max_to(amax, m);
 }
 
 // ---- dispatch helpers: (reduce, act) -> template instance ----
@@ -294,14 +304,13 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
     if (vec) {
       const int64_t hv = h / 4;
       init_only_vec4<<<grid_for(E * hv, 256, 256 * 32), 256, 0, stream>>>(
-          (const float4*)Xv, (const float4*)Xe, src, E, hv, (float4*)H0);
+          (const float4*)Xv, (const float4*)Xe, src, E, hv, (float4*)H0, amax_out);
     } else {
       init_only_scalar<<<grid_for(E * h, 256, 256 * 32), 256, 0, stream>>>(
-          (const float*)Xv, (const float*)Xe, src, E, h, (float*)H0);
+          (const float*)Xv, (const float*)Xe, src, E, h, (float*)H0, amax_out);
     }
   }
   NT_LAUNCH_CHECK();
-  if (amax_out) return fk_absmax((const float*)H0, E * h, amax_out, stream);
   return NT_OK;
 }
 
@@ -359,10 +368,11 @@ __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict
                                                          const int32_t* __restrict__ chunk_ptr,
                                                          const int32_t* __restrict__ seg_ptr,
                                                          int64_t nseg, int64_t h,
-                                                         T* __restrict__ out) {
+                                                         T* __restrict__ out, float* __restrict__ amax) {
   constexpr int N = Piece<T, VEC>::N;
   const int64_t hw = h / N;
   const int64_t total = nseg * hw;
+  float m = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t s = t / hw, c = (t - s * hw) * N;
@@ -385,13 +395,16 @@ __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict
       for (int i = 0; i < N; ++i) y[i] /= (float)(n > 1 ? n : 1);
     }
     Piece<T, VEC>::store(out + s * h + c, y);
+#pragma unroll
+    for (int i = 0; i < N; ++i) m = fmaxf(m, fabsf(y[i]));
   }
+  if (amax) block_max_to(amax, m);  // fp32 callers: max|out| (the fp32 layer kernel's split scale)
 }
 
 template <typename T, bool VEC>
 int launch_chunked(const void* X, const int32_t* perm, const int32_t* chunk_pos, int64_t nchunks,
                    const int32_t* chunk_ptr, const int32_t* seg_ptr, int64_t nseg, int64_t h,
-                   int reduce, int act, float alpha, float* P, void* out, hipStream_t stream) {
+                   int reduce, int act, float alpha, float* P, void* out, float* amax, hipStream_t stream) {
   constexpr int N = Piece<T, VEC>::N;
   if (nchunks > 0) {
     const int g1 = grid_for(nchunks * (h / N), 256, 256 * 32);
@@ -402,10 +415,10 @@ int launch_chunked(const void* X, const int32_t* perm, const int32_t* chunk_pos,
   }
   const int g2 = grid_for(nseg * (h / N), 256, 256 * 32);
   switch (reduce) {
-    case NT_SUM: seg_chunk_combine<T, VEC, NT_SUM><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out); break;
-    case NT_MEAN: seg_chunk_combine<T, VEC, NT_MEAN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out); break;
-    case NT_MAX: seg_chunk_combine<T, VEC, NT_MAX><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out); break;
-    default: seg_chunk_combine<T, VEC, NT_MIN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out); break;
+    case NT_SUM: seg_chunk_combine<T, VEC, NT_SUM><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out, amax); break;
+    case NT_MEAN: seg_chunk_combine<T, VEC, NT_MEAN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out, amax); break;
+    case NT_MAX: seg_chunk_combine<T, VEC, NT_MAX><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out, amax); break;
+    default: seg_chunk_combine<T, VEC, NT_MIN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out, amax); break;
   }
   NT_LAUNCH_CHECK();
   return NT_OK;
@@ -418,7 +431,7 @@ extern "C" int nt_segment_reduce_chunked(const void* X, const int32_t* perm, con
                                          int64_t nchunks, const int32_t* chunk_ptr,
                                          const int32_t* seg_ptr, int64_t nseg, int64_t h, int reduce,
                                          int act, float act_alpha, int dtype, float* partial,
-                                         void* out, void* stream_) {
+                                         void* out, float* amax_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
@@ -432,12 +445,12 @@ extern "C" int nt_segment_reduce_chunked(const void* X, const int32_t* perm, con
   if (dtype == NT_F32)
     return (h % 4 == 0 && al)
                ? launch_chunked<float, true>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
-                                             reduce, act, act_alpha, partial, out, stream)
+                                             reduce, act, act_alpha, partial, out, amax_out, stream)
                : launch_chunked<float, false>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
-                                              reduce, act, act_alpha, partial, out, stream);
+                                              reduce, act, act_alpha, partial, out, amax_out, stream);
   return (h % 8 == 0 && al)
              ? launch_chunked<bf16_raw, true>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
-                                              reduce, act, act_alpha, partial, out, stream)
+                                              reduce, act, act_alpha, partial, out, nullptr, stream)
              : launch_chunked<bf16_raw, false>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
-                                               reduce, act, act_alpha, partial, out, stream);
+                                               reduce, act, act_alpha, partial, out, nullptr, stream);
 }

@@ -294,9 +294,11 @@ def segment_reduce_chunked(
     reduce: str = "sum",
     act: tuple[int, float] = (_lib.NT_ACT_IDENTITY, 0.0),
     out: Tensor | None = None,
+    amax: Tensor | None = None,
 ) -> Tensor:
-    """segment_reduce load-balanced over chunks (plan = chunk_plan(seg_ptr)) for skewed segments."""
-    dev = _require_device(X, seg_ptr, perm)
+    """segment_reduce load-balanced over chunks (plan = chunk_plan(seg_ptr)) for skewed segments;
+    fp32: amax (1 zero-filled device float, optional) is raised to max|out|."""
+    dev = _require_device(X, seg_ptr, perm, amax)
     code = _require_feat("X", X)
     if seg_ptr.dtype != torch.int32 or seg_ptr.numel() != nseg + 1:
         raise ValueError("seg_ptr must be int32 of length nseg + 1")
@@ -309,7 +311,7 @@ def segment_reduce_chunked(
     partial = torch.empty(max(nchunks, 1), h, dtype=torch.float32, device=dev)
     _run(dev, _lib.load().nt_segment_reduce_chunked,
          _ptr(X), _ptr(perm), _ptr(chunk_pos), nchunks, _ptr(chunk_ptr), _ptr(seg_ptr), nseg, h,
-         reduce_code(reduce), act[0], act[1], code, _ptr(partial), _ptr(out), _stream(dev))
+         reduce_code(reduce), act[0], act[1], code, _ptr(partial), _ptr(out), _ptr(amax), _stream(dev))
     return out
 
 

@@ -229,10 +229,16 @@ def dst_chunks(lay: DeviceLayout):
     return ch or None
 
 
-def _aggregate(X, seg_ptr, perm, nseg, reduce, act, chunks, out=None):
+def _aggregate(X, seg_ptr, perm, nseg, reduce, act, chunks, out=None, amax=None):
+    """scatter(act(X), seg) by the chunked reduce (skewed segments) or the plain one; amax (fp32,
+    1 device float) is raised to max|out| (fused into the chunked reduce, a separate pass otherwise)."""
     if chunks is not None:
-        return K.segment_reduce_chunked(X, seg_ptr, perm, nseg, chunks, reduce=reduce, act=act, out=out)
-    return K.segment_reduce(X, seg_ptr, perm, nseg, reduce=reduce, act=act, out=out)
+        return K.segment_reduce_chunked(X, seg_ptr, perm, nseg, chunks, reduce=reduce, act=act, out=out,
+                                        amax=amax)
+    out = K.segment_reduce(X, seg_ptr, perm, nseg, reduce=reduce, act=act, out=out)
+    if amax is not None:
+        K.absmax(out, amax)
+    return out
 
 
 def _fused_enabled() -> bool:
@@ -294,9 +300,7 @@ def block_forward(
     if chunks is not None:
         # hubs: the fused init would walk a hub's in-edges on one wave (polymer-16: 3.17 vs 3.00 ms)
         H, _ = K.dmpnn_init(Xv, Xe, src, amax=a0)
-        S = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks)
-        if a0 is not None:
-            K.absmax(S, a0[1:2])
+        S = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks, amax=None if a0 is None else a0[1:2])
     else:
         H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce, amax=a0)
     return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop,
@@ -411,9 +415,7 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
             timer.append(ev)
         if l < d - 1:
             S = _aggregate(Hn, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks,
-                           out=None if keep_states else S)
-            if persistent:
-                K.absmax(S, amax[l + 1, 1:2])
+                           out=None if keep_states else S, amax=amax[l + 1, 1:2] if persistent else None)
         if not keep_states:
             spare = H  # H_l is dead once H_{l+1} exists: reuse its buffer for H_{l+2}
         H = Hn

@@ -132,3 +132,37 @@ def test_hub_block_deterministic_and_grads():
     assert_parity(xv.grad, Xv64.grad, 1e-4, "dXv")
     assert_parity(xe.grad, Xe64.grad, 1e-4, "dXe")
     assert_parity(lin0.weight.grad, W64[0].grad, 1e-4, "dW0")
+
+
+def test_amax_outputs_of_the_producers():
+    """The kernels that write an fp32 operand of the fp16-split kernels report its max |value|
+    exactly (ABI 3): the plain init (H0), the chunked reduce (S of hub graphs), the backward's row
+    gather and edge backward (G)."""
+    from notorch_amd import kernels as K
+    from notorch_amd.nn.gnn import _engine
+
+    G = _polymer(2, seed=4)
+    lay = G._nt_layout
+    E, V, h = G.num_edges, G.num_nodes, 64
+    g = torch.Generator().manual_seed(0)
+    Xv, Xe = torch.randn(V, h, generator=g).to(DEV), torch.randn(E, h, generator=g).to(DEV) * 3
+    src, dst = G.edge_index[0].to(DEV), G.edge_index[1].to(DEV)
+    dst_ptr, perm = lay.dst_ptr.to(DEV), lay.dst_perm.to(DEV)
+    am = torch.zeros(2, device=DEV)
+    H0, _ = K.dmpnn_init(Xv, Xe, src, amax=am)
+    assert am[0].item() == H0.abs().max().item()
+    chunks = K.chunk_plan(dst_ptr)
+    S = K.segment_reduce_chunked(H0, dst_ptr, perm, V, chunks, act=K.act_code(nn.ReLU()), amax=am[1:2])
+    assert am[1].item() == S.abs().max().item()
+    dnode = torch.randn(V, h, generator=g).to(DEV)
+    gm = torch.zeros(1, device=DEV)
+    Gr = K.gather_rows(dnode, dst, base=H0, amax=gm)
+    assert gm.item() == Gr.abs().max().item()
+    rev = G.rev_index.to(DEV)
+    rev_ptr, rev_perm = K.csr_build(rev, E, check_bounds=False)
+    dA = torch.randn(E, h, generator=g).to(DEV)
+    dS = torch.randn(V, h, generator=g).to(DEV)
+    gm2 = torch.zeros(1, device=DEV)
+    Gn = K.dmpnn_edge_backward(Gr, H0, dA, dS, dst, rev_ptr, rev_perm, dst_ptr, amax=gm2)
+    assert gm2.item() == Gn.abs().max().item()
+    assert _engine.hub_info(lay) is not None
