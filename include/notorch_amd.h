@@ -247,7 +247,7 @@ NT_API int nt_dmpnn_mark_hub_rows(void* row_table, int64_t E, const int32_t* dst
  *   out[v] = reduce_{p in [seg_ptr[v], seg_ptr[v+1])} act(X[perm[p]])   for v in hubs[0 .. nhub)
  * (rows of other nodes untouched).  amax_out (may be NULL): one device float raised to max|out[v]|
  * (the fused layer's max|S_out| slot).  fp32, h % 4 == 0, 16-byte aligned X / out; deterministic
- * (eight contiguous row ranges per hub, combined in order).
+ * (16 contiguous row ranges per hub, combined in order).
  */
 NT_API int nt_dmpnn_hub_aggregate(const void* X, const int32_t* perm, const int32_t* seg_ptr,
                                   const int32_t* hubs, int64_t nhub, int64_t h, int reduce, int act,

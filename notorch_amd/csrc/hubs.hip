@@ -14,7 +14,7 @@
 namespace nt {
 namespace {
 
-constexpr int kHubWaves = 8;  // waves per workgroup: each reduces a contiguous 1/8 of the in-edges
+constexpr int kHubWaves = 16;  // waves per workgroup: each reduces a contiguous 1/16 of the in-edges
 constexpr int kHubBatch = 8;  // rows in flight per lane
 
 template <int R>
@@ -36,10 +36,10 @@ __device__ __forceinline__ float4 hub_op4(float4 a, float4 x) {
   return make_float4(hub_op<R>(a.x, x.x), hub_op<R>(a.y, x.y), hub_op<R>(a.z, x.z), hub_op<R>(a.w, x.w));
 }
 
-// grid (nhub, nslab), 512 threads.  Slab j holds pieces [j P, (j + 1) P) of the hv 16-B pieces of a
-// row (P = ceil(hv / nslab) <= 64, one per lane).  Wave w reduces rows [b + w n / 8, b + (w + 1) n / 8)
+// grid (nhub, nslab), 1024 threads.  Slab j holds pieces [j P, (j + 1) P) of the hv 16-B pieces of a
+// row (P = ceil(hv / nslab) <= 64, one per lane).  Wave w reduces rows [b + w n / 16, b + (w + 1) n / 16)
 // of the hub's CSR range in ascending order with kHubBatch row loads in flight (indices clamped, the
-// loads unconditional); the eight partials combine in wave order through LDS (deterministic).
+// loads unconditional); the 16 partials combine in wave order through LDS (deterministic).
 template <int R, int ACT>
 __global__ void __launch_bounds__(kHubWaves * 64) hub_aggregate_kernel(
     const float4* __restrict__ X, const int32_t* __restrict__ perm, const int32_t* __restrict__ seg_ptr,
