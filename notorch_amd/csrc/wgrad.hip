@@ -886,6 +886,40 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
   }
 }
 
+// dW and db partials reduced in one launch: index i < n1 sums part[y][i] into out1[i], the rest sums
+// part_db[y][i - n1] into out2 (each in ascending y, as wgrad_reduce_kernel: deterministic)
+__global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restrict__ part, int64_t n1,
+                                                            const float* __restrict__ part_db, int64_t n2,
+                                                            int ksplit, float* __restrict__ out1,
+                                                            float* __restrict__ out2) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n1 + n2; i += (int64_t)gridDim.x * blockDim.x) {
+    const bool first = i < n1;
+    const float* src = first ? part + i : part_db + (i - n1);
+    const int64_t stride = first ? n1 : n2;
+    float s = 0.f;
+    int y = 0;
+    for (; y + 8 <= ksplit; y += 8) {
+      float v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(int64_t)(y + u) * stride];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) s += v[u];
+    }
+    for (; y < ksplit; ++y) s += src[(int64_t)y * stride];
+    if (first) out1[i] = s;
+    else out2[i - n1] = s;
+  }
+}
+
+int reduce_partials(const float* part, const float* part_db, int64_t h, int ksplit, float* dW, float* db,
+                    hipStream_t stream) {
+  const int64_t n2 = db ? h : 0;
+  wgrad_reduce2_kernel<<<grid_for(h * h + n2, 256, 256 * 8), 256, 0, stream>>>(part, h * h, part_db, n2, ksplit,
+                                                                               dW, db);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
 struct Plan {
   int tiles, ksplit, chunk_steps;
 };
@@ -1007,13 +1041,7 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
     NT_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kBLds));
     kern<<<grid, 512, kBLds, stream>>>(b);
     NT_LAUNCH_CHECK();
-    wgrad_reduce_kernel<<<grid_for(h * h, 256, 256 * 8), 256, 0, stream>>>(b.part, h * h, q.ksplit, (float*)dW_out);
-    NT_LAUNCH_CHECK();
-    if (db_out) {
-      wgrad_reduce_kernel<<<grid_for(h, 256, 64), 256, 0, stream>>>(b.part_db, h, q.ksplit, (float*)db_out);
-      NT_LAUNCH_CHECK();
-    }
-    return NT_OK;
+    return reduce_partials(b.part, b.part_db, h, q.ksplit, (float*)dW_out, (float*)db_out, stream);
   }
   if (src && h <= kWI) {  // the wide kernel: 128-column blocks of A against all of G
     const int jblocks = (int)((h + kWJ - 1) / kWJ);
@@ -1042,13 +1070,7 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
     else
       wgrad_wide_kernel<-1><<<grid, 512, kWLds, stream>>>(b);
     NT_LAUNCH_CHECK();
-    wgrad_reduce_kernel<<<grid_for(h * h, 256, 256 * 8), 256, 0, stream>>>(b.part, h * h, q.ksplit, (float*)dW_out);
-    NT_LAUNCH_CHECK();
-    if (db_out) {
-      wgrad_reduce_kernel<<<grid_for(h, 256, 64), 256, 0, stream>>>(b.part_db, h, q.ksplit, (float*)db_out);
-      NT_LAUNCH_CHECK();
-    }
-    return NT_OK;
+    return reduce_partials(b.part, b.part_db, h, q.ksplit, (float*)dW_out, (float*)db_out, stream);
   }
   const int grid = p.tiles * p.ksplit;
   const size_t lds = kBufs * 2 * kSlabB;
@@ -1061,13 +1083,7 @@ extern "C" int nt_dmpnn_weight_grad(const void* G, const void* H, const void* S,
   else
     wgrad_kernel<-1, true><<<grid, 256, lds, stream>>>(a);
   NT_LAUNCH_CHECK();
-  wgrad_reduce_kernel<<<grid_for(h * h, 256, 256 * 8), 256, 0, stream>>>(a.part, h * h, p.ksplit, (float*)dW_out);
-  NT_LAUNCH_CHECK();
-  if (db_out) {
-    wgrad_reduce_kernel<<<grid_for(h, 256, 64), 256, 0, stream>>>(a.part_db, h, p.ksplit, (float*)db_out);
-    NT_LAUNCH_CHECK();
-  }
-  return NT_OK;
+  return reduce_partials(a.part, a.part_db, h, p.ksplit, (float*)dW_out, (float*)db_out, stream);
 }
 
 extern "C" int nt_dmpnn_weight_grad_fk(const void* G, const void* H, const void* S, const int64_t* src,
@@ -1119,11 +1135,5 @@ extern "C" int nt_dmpnn_weight_grad_fk(const void* G, const void* H, const void*
   NT_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, kFLds));
   kern<<<grid, 512, kFLds, stream>>>(b);
   NT_LAUNCH_CHECK();
-  wgrad_reduce_kernel<<<grid_for(h * h, 256, 256 * 8), 256, 0, stream>>>(b.part, h * h, q.ksplit, (float*)dW_out);
-  NT_LAUNCH_CHECK();
-  if (db_out) {
-    wgrad_reduce_kernel<<<grid_for(h, 256, 64), 256, 0, stream>>>(b.part_db, h, q.ksplit, (float*)db_out);
-    NT_LAUNCH_CHECK();
-  }
-  return NT_OK;
+  return reduce_partials(b.part, b.part_db, h, q.ksplit, (float*)dW_out, (float*)db_out, stream);
 }
