@@ -868,26 +868,8 @@ __global__ void __launch_bounds__(512, 1) wgrad_bf16_kernel(WbArgs a) {
   }
 }
 
-// out[i] = sum_y part[y][i] in ascending y (fixed order: deterministic)
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ part, int64_t n,
-                                                           int ksplit, float* __restrict__ out) {
-  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-    float s = 0.f;
-    int y = 0;
-    for (; y + 8 <= ksplit; y += 8) {  // 8 loads in flight, summed in ascending y
-      float v[8];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = part[(int64_t)(y + u) * n + i];
-#pragma unroll
-      for (int u = 0; u < 8; ++u) s += v[u];
-    }
-    for (; y < ksplit; ++y) s += part[(int64_t)y * n + i];
-    out[i] = s;
-  }
-}
-
 // dW and db partials reduced in one launch: index i < n1 sums part[y][i] into out1[i], the rest sums
-// part_db[y][i - n1] into out2 (each in ascending y, as wgrad_reduce_kernel: deterministic)
+// part_db[y][i - n1] into out2, each in ascending y (fixed order: deterministic)
 __global__ void __launch_bounds__(256) wgrad_reduce2_kernel(const float* __restrict__ part, int64_t n1,
                                                             const float* __restrict__ part_db, int64_t n2,
                                                             int ksplit, float* __restrict__ out1,
