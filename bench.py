@@ -501,20 +501,22 @@ def pipeline_leg(res, dev, workers, n_batches=24, warm=4):
 
 def training_leg(args, timeout_s=300):
     """Config-2 training step (ChempropBlock + Sum, forward + backward, kernel backward) with each
-    weight-grad path, each in a fresh child process (tools/train_bench.py --json: 10 warm-ups, median
-    of 30 event-timed steps)."""
+    weight-grad path, each in a fresh child process (tools/train_bench.py --json: 10 warm-ups and at
+    least 1 s more, median of 50 event-timed steps)."""
     import subprocess
 
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "train_bench.py")
     out = {"step": "config 2 batch (4096 qm9-shaped molecules, seed 1000), ChempropBlock depth=3 h=300 + Sum, "
                    "forward + backward of sum(readout^2) w.r.t. weights and input features, fp32; "
-                   "one fresh process per weight-grad path; median of 30 after 10 warm-ups",
+                   "one fresh process per weight-grad path; median of 50 after 10 warm-ups and >= 1 s of "
+                   "warm-up steps",
            "unit": "edge-messages/s"}
     for wgrad in ("kernel", "library"):
         env = dict(os.environ, NT_WGRAD=wgrad)
         try:
-            r = subprocess.run([sys.executable, script, "--json", "--modes", "kernel", "--steps", "30",
-                                "--warmup", "10"], env=env, capture_output=True, text=True, timeout=timeout_s)
+            r = subprocess.run([sys.executable, script, "--json", "--modes", "kernel", "--steps", "50",
+                                "--warmup", "10", "--warmup-s", "1"], env=env, capture_output=True, text=True,
+                               timeout=timeout_s)
         except subprocess.TimeoutExpired:
             out[wgrad] = {"error": f"timed out after {timeout_s} s"}
             continue

@@ -4,12 +4,13 @@ Modes: `kernel` (the kernel backward, the weight grad per NT_WGRAD) and `torch` 
 recompute-in-torch backward, NT_BWD=torch).  bench.py's `training` key runs this once per weight-grad
 path (NT_WGRAD=kernel / library), each in a fresh process, with --json.
 Usage: python tools/train_bench.py [--kind qm9] [--mols 4096] [--h 300] [--depth 3] [--dtype f32|bf16]
-                                  [--steps 30] [--warmup 10] [--modes kernel,torch] [--json]"""
+                                  [--steps 30] [--warmup 10] [--warmup-s 0] [--modes kernel,torch] [--json]"""
 import argparse
 import json
 import os
 import statistics
 import sys
+import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch  # noqa: E402
@@ -28,6 +29,9 @@ def main():
     p.add_argument("--depth", type=int, default=3)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--warmup-s", type=float, default=0.0,
+                   help="after the counted warm-ups, keep warming up until this many seconds have passed "
+                        "(lets the clocks settle in a fresh process)")
     p.add_argument("--modes", default="kernel,torch")
     p.add_argument("--json", action="store_true", help="print one JSON object instead of the table")
     a = p.parse_args()
@@ -65,6 +69,10 @@ def main():
             for _ in range(a.warmup):
                 fn()
             torch.cuda.synchronize()
+            t_end = time.perf_counter() + a.warmup_s
+            while time.perf_counter() < t_end:
+                fn()
+                torch.cuda.synchronize()
             ts = []
             for _ in range(a.steps):
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
