@@ -466,7 +466,9 @@ __device__ __forceinline__ void fk_barrier() {
 
 // ABL (diagnostic builds only, 0 in the shipping library): timing ablations, results invalid --
 // 1 gathers read row 0, 2 no MFMA, 4 no split, 8 no epilogue, 16 no per-step barrier, 32 no residual,
-// 64 no H_out stores, 128 no S_out stores.
+// 64 no H_out stores, 128 no S_out stores; 256 (results valid): per-phase s_memtime cycle sums into
+// g_pk_stamps (0 residual scale + MFMAs, 1 W issue, 2 split + gather issue, 3 barrier, 4 epilogue,
+// 6 whole loop, 7 waves).
 template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL, int GD = 2, int ABL = 0>
 __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   // fused variants (MAXL > 1) read their rows from the row table, plain ones from src / rev
@@ -580,6 +582,15 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   // ahead, gathers three steps ahead, both before the epilogue's stores (vmcnt counts loads and
   // stores in issue order, so the next two steps' waits do not cover the stores).
   int g = 0, i = 0, k = 0;  // global step, tile-local index, step within the tile
+  [[maybe_unused]] unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tp = 0, tb = 0;
+  if constexpr ((ABL & 256) != 0) tb = tp = __builtin_amdgcn_s_memtime();
+  auto stamp = [&](int slot) __attribute__((always_inline)) {
+    if constexpr ((ABL & 256) != 0) {
+      const unsigned long long t = __builtin_amdgcn_s_memtime();
+      tacc[slot] += t - tp;
+      tp = t;
+    }
+  };
   while (g < G) {
 #pragma unroll
     for (int P = 0; P < 2; ++P) {
@@ -593,6 +604,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
           if (P == 0) fk_mfma<RT, CT, 0>(st, c, (n_cur + 15) >> 4);
           else fk_mfma<RT, CT, 1>(st, c, (n_cur + 15) >> 4);
         }
+        stamp(0);
         // (3) W fragments of step g + 2 into the registers step g used
         {
           int c2, s2;
@@ -600,6 +612,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
           if (P == 0) fk_load_w<RT, CT, 0>(st, c2, s2);
           else fk_load_w<RT, CT, 1>(st, c2, s2);
         }
+        stamp(1);
         // (4) split step g + 1's staged piece into the other buffer, then gather step g + 3 into the
         // freed slot (tile i or i + 1)
         {
@@ -617,12 +630,15 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
           if (P == 0) fk_gather<RT, CT, ACT, 1>(st, a, so, qo, s3);
           else fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s3);
         }
+        stamp(2);
         if constexpr ((ABL & 16) == 0) fk_barrier();
+        stamp(3);
         // (5) epilogue at the chunk's last k-step; it starts the next (tile, chunk)'s residual loads
         if ((ABL & 8) == 0 && s == a.KS - 1) {
           const bool last_c = c + 1 == a.nchunks;
           const int i_next = last_c ? (i + 1 < ntl ? i + 1 : i) : i, c_next = last_c ? 0 : c + 1;
           fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
+          stamp(4);
         }
         // (6) advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
         ++g;
@@ -648,6 +664,13 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
     if (st.lane == 0) {
       atomic_max_abs(a.amax_out, mh);
       if (a.SO) atomic_max_abs(a.amax_out + 1, ms);
+    }
+  }
+  if constexpr ((ABL & 256) != 0) {
+    if (st.lane == 0) {
+      for (int q = 0; q < 5; ++q) atomicAdd(&g_pk_stamps[q], tacc[q]);
+      atomicAdd(&g_pk_stamps[6], __builtin_amdgcn_s_memtime() - tb);
+      atomicAdd(&g_pk_stamps[7], 1ull);
     }
   }
 }

@@ -749,6 +749,16 @@ int launch_fk_wide(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
   }
   // fused (fk_tile_rows: act = relu): scan rounds 3 cover in-degree <= 4 (molecules), 8 in-degree <= 9
   // (the non-hub nodes of hub graphs, cut at HUB_CUT_DEGREE), 16 every plan
+#ifdef NT_DIAG
+  {  // per-phase stamps of the config-2 instance (tools/stamps_fk.py)
+    const char* e = getenv("NT_FK_ABL");
+    if (e && atoi(e) == 256 && maxl <= 3 && a.aact == NT_ACT_RELU) {
+      fk::update_fk_kernel<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 3, 2, 256><<<grid, fk::kThreads, 0, stream>>>(a);
+      NT_LAUNCH_CHECK();
+      return NT_OK;
+    }
+  }
+#endif
   if (a.aact == NT_ACT_RELU)
     return maxl <= 3   ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 3>(a, grid, stream)
            : maxl <= 8 ? launch_fk_t<8, CT, NT_ACT_RELU, NT_ACT_RELU, true, 8>(a, grid, stream)
