@@ -708,8 +708,8 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             del A
         if fk_dense:
             dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous(), fk_only=True), amax=gmax)
-        elif bf16_kernels:  # the bf16 layer kernel without gathers
-            dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous()))
+        elif bf16_kernels and os.environ.get("NT_BF16_DA", "kernel") == "kernel":  # the bf16 layer kernel
+            dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous()))  # without gathers
         else:
             dA = torch.mm(Gu, W)
         del Gu
