@@ -8,10 +8,16 @@ FLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result 
            -fvisibility=hidden -DNT_BUILD
 # DIAG=1: the diagnostic library (A/B kernel variants, ablation and stamp builds selected by NT_*
 # environment variables) next to the shipping one; notorch_amd._lib loads it when NT_LIB=diag.
+# VARIANT=<name> EXTRA=-D...: an A/B build of the shipping sources into lib/libnotorch_amd_<name>.so
+# (loaded with NT_LIB=variant:<name>; experiments only, git- and gpurun-ignored build dirs)
+FLAGS   += $(EXTRA)
 ifeq ($(DIAG),1)
 OUT     := notorch_amd/lib/libnotorch_amd_diag.so
 BDIR    := build_diag
 FLAGS   += -DNT_DIAG
+else ifneq ($(VARIANT),)
+OUT     := notorch_amd/lib/libnotorch_amd_$(VARIANT).so
+BDIR    := build_$(VARIANT)
 else
 OUT     := notorch_amd/lib/libnotorch_amd.so
 BDIR    := build

@@ -268,8 +268,10 @@ def committed_traffic(workload, kernel_substr):
 
 # --------------------------------------------------------------------------- CPU baseline
 def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
-    """Oracle restatement (ATen CPU) timed on the host at P = 1 and at P = the box's CPU share
-    (OMP_NUM_THREADS, which the GPU box sets to its per-GPU share), median of runs per budget."""
+    """Oracle restatement (ATen CPU) timed on the host at P = 1, at P = the box's CPU share
+    (OMP_NUM_THREADS, which the GPU box sets to its per-GPU share) and at P = the physical cores this
+    process may run on (lscpu cores, capped at the affinity mask), median of runs per budget; the
+    reported value is the fastest P."""
     from oracle import dmpnn_ref
 
     if job.B > sample_mols:  # bounded sample: the first sample_mols molecules of the job
@@ -290,8 +292,11 @@ def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
     except AttributeError:
         visible = os.cpu_count() or 1
     share = min(int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or 16, visible)
-    thread_counts = sorted({1, share})  # more threads than the per-GPU share only oversubscribe
     host = host_cpu_info()
+    # P = 1, the box's per-GPU CPU share, and P = the physical cores this process may use (the
+    # BASELINE.md plan: set_num_threads(P) with P = the physical cores); value = the fastest P
+    phys = min(host.get("physical_cores", visible) or visible, visible)
+    thread_counts = sorted({1, share, phys})
 
     def one():
         with torch.inference_mode():
@@ -320,8 +325,9 @@ def cpu_baseline(job, embedding, budget_s, sample_mols=4096):
         "by_threads": {str(p): {"value": E * job.depth / m, "ms": m * 1e3, "runs": n} for p, (m, n) in res.items()},
         "host": dict(host, cpus_visible=visible),
         "sample": f"oracle/dmpnn_ref.py (ATen CPU restatement of chemprop.py+agg.py) on {sample} "
-        f"(V={G.num_nodes}, E={E}), fp32, torch.set_num_threads(P) for P in {sorted(res)} (P = 1 and "
-        f"the box's per-GPU CPU share OMP_NUM_THREADS={share}); host {host.get('model', '?')}, "
+        f"(V={G.num_nodes}, E={E}), fp32, torch.set_num_threads(P) for P in {sorted(res)} (P = 1, "
+        f"the box's per-GPU CPU share OMP_NUM_THREADS={share} and the physical cores usable here, {phys}); "
+        f"host {host.get('model', '?')}, "
         f"{host.get('physical_cores', '?')} physical cores ({visible} CPUs visible to this process); "
         f"median of runs within {budget_s:.0f} s each after 1 warm-up; value and cores = the fastest P",
     }
@@ -500,36 +506,41 @@ def pipeline_leg(res, dev, workers, n_batches=24, warm=4):
 
 
 def training_leg(args, timeout_s=300):
-    """Config-2 training step (ChempropBlock + Sum, forward + backward, kernel backward) with each
-    weight-grad path, each in a fresh child process (tools/train_bench.py --json: 10 warm-ups and at
-    least 1 s more, median of 50 event-timed steps)."""
+    """Training steps as the reference trains (tools/train_bench.py --json, each in a fresh child
+    process: zero_grad + forward + backward + Adam(lr=1e-4).step(), 10 warm-ups and at least 1 s
+    more, median of 50 event-timed steps).  Headline: config 2 on the default (kernel) weight-grad
+    path; `library` is the same step with NT_WGRAD=library, a comparison only; `config3_bf16` is
+    config 3 (zinc-4096, bf16, h=512, depth=5) on the default path."""
     import subprocess
 
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "train_bench.py")
     out = {"step": "config 2 batch (4096 qm9-shaped molecules, seed 1000), ChempropBlock depth=3 h=300 + Sum, "
-                   "forward + backward of sum(readout^2) w.r.t. weights and input features, fp32; "
-                   "one fresh process per weight-grad path; median of 50 after 10 warm-ups and >= 1 s of "
-                   "warm-up steps",
+                   "zero_grad + forward + backward of sum(readout^2) w.r.t. weights and input features + "
+                   "Adam(lr=1e-4).step() (model.py:153,273), fp32; fresh process per leg; median of 50 after "
+                   "10 warm-ups and >= 1 s of warm-up steps",
            "unit": "edge-messages/s"}
-    for wgrad in ("kernel", "library"):
-        env = dict(os.environ, NT_WGRAD=wgrad)
+
+    def run(env_extra, extra_args):
+        env = dict(os.environ, **env_extra)
         try:
             r = subprocess.run([sys.executable, script, "--json", "--modes", "kernel", "--steps", "50",
-                                "--warmup", "10", "--warmup-s", "1"], env=env, capture_output=True, text=True,
-                               timeout=timeout_s)
+                                "--warmup", "10", "--warmup-s", "1", *extra_args], env=env,
+                               capture_output=True, text=True, timeout=timeout_s)
         except subprocess.TimeoutExpired:
-            out[wgrad] = {"error": f"timed out after {timeout_s} s"}
-            continue
+            return {"error": f"timed out after {timeout_s} s"}
         if r.returncode != 0:
-            out[wgrad] = {"error": f"exit {r.returncode}: {r.stderr.strip().splitlines()[-1:]}"}
-            continue
+            return {"error": f"exit {r.returncode}: {r.stderr.strip().splitlines()[-1:]}"}
         d = json.loads(r.stdout.strip().splitlines()[-1])
-        out[wgrad] = {"train_ms": d["ms"]["train[kernel]"], "forward_ms": d["ms"]["fwd"],
-                      "value": d["edge_messages_per_s"]["train[kernel]"]}
-    ok = [k for k in ("kernel", "library") if "train_ms" in out.get(k, {})]
-    if ok:
-        best = min(ok, key=lambda k: out[k]["train_ms"])
-        out.update(weight_grad=best, train_ms=out[best]["train_ms"], value=out[best]["value"])
+        return {"train_ms": d["ms"]["train[kernel]"], "forward_ms": d["ms"]["fwd"],
+                "value": d["edge_messages_per_s"]["train[kernel]"]}
+
+    out["kernel"] = run({}, [])
+    out["library"] = run({"NT_WGRAD": "library"}, [])
+    if "train_ms" in out["kernel"]:
+        out.update(weight_grad="kernel", train_ms=out["kernel"]["train_ms"], value=out["kernel"]["value"])
+    out["config3_bf16"] = dict(run({}, ["--kind", "zinc", "--h", "512", "--depth", "5", "--dtype", "bf16"]),
+                               step="config 3 batch (4096 zinc-shaped molecules), depth=5 h=512, bf16 storage, "
+                                    "same step (Adam included)")
     return out
 
 

@@ -15,8 +15,14 @@ import threading
 _LIB_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib")
 # NT_LIB=diag loads the diagnostic build (make DIAG=1: A/B kernel variants selectable by NT_*
 # environment variables, ablation / stamp builds); the default is the shipping library.
-DIAG = os.environ.get("NT_LIB", "") == "diag"
-LIB_PATH = os.path.join(_LIB_DIR, "libnotorch_amd_diag.so" if DIAG else "libnotorch_amd.so")
+# NT_LIB=variant:<name> loads lib/libnotorch_amd_<name>.so, an A/B build of the shipping sources
+# (make VARIANT=<name> EXTRA=-D...; tools only).
+_NT_LIB = os.environ.get("NT_LIB", "")
+DIAG = _NT_LIB == "diag"
+if _NT_LIB.startswith("variant:"):
+    LIB_PATH = os.path.join(_LIB_DIR, f"libnotorch_amd_{_NT_LIB.split(':', 1)[1]}.so")
+else:
+    LIB_PATH = os.path.join(_LIB_DIR, "libnotorch_amd_diag.so" if DIAG else "libnotorch_amd.so")
 ABI_VERSION = 3
 
 NT_F32, NT_BF16 = 0, 1

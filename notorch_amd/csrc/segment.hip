@@ -82,10 +82,12 @@ __global__ void __launch_bounds__(256) init_aggregate_vec4(
 }
 
 // One wave per node (the node id is wave-uniform, so the index chain seg_ptr -> perm -> src runs on
-// scalar loads once per wave instead of once per 16-B piece): lanes take the node's row pieces
-// (p = lane + 64 k), the in-edges go 4 at a time with all their row loads in flight.  Same order of
-// operations as init_aggregate_vec4, so the same bits.
-template <int R, int ACT>
+// scalar loads once per wave instead of once per 16-B piece): lane l takes the row pieces
+// p = l + 64 q (q < PPL, so one pass covers up to 64 PPL pieces, rows of h <= 256 PPL), and the
+// in-edges go 4 at a time with all their row loads in flight (4 x 2 x PPL 16-B loads per lane).
+// Lanes past the row read piece 0 and are masked at the stores.  Same order of operations per piece
+// as init_aggregate_vec4, so the same bits.  Rows wider than one pass loop over passes.
+template <int R, int ACT, int PPL>
 __global__ void __launch_bounds__(256) init_aggregate_wave(
     const float4* __restrict__ Xv, const float4* __restrict__ Xe, const int64_t* __restrict__ src,
     const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm, int64_t V, int64_t hv,
@@ -93,43 +95,70 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
   const int lane = threadIdx.x & 63;
   float mh = 0.f, ms = 0.f;  // max |H0|, max |S| of this lane (amax != NULL)
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  auto amax4 = [](float m, float4 v) __attribute__((always_inline)) {
+    return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+  };
   for (int64_t v = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
        v < V; v += nwaves) {
     const int32_t b = seg_ptr[v], en = seg_ptr[v + 1];
-    for (int64_t c = lane; c < hv; c += 64) {
-      Reducer4<R> r;
-      r.init();
+    for (int64_t c0 = 0; c0 < hv; c0 += 64 * PPL) {
+      int64_t cc[PPL];
+      bool ok[PPL];
+      Reducer4<R> r[PPL];
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) {
+        const int64_t c = c0 + lane + 64 * q;
+        ok[q] = c < hv;
+        cc[q] = ok[q] ? c : 0;
+        r[q].init();
+      }
       int32_t j = b;
       for (; j + 4 <= en; j += 4) {
         int64_t ed[4], sv[4];
-        float4 a[4], x[4];
+        float4 a[4][PPL], x[4][PPL];
 #pragma unroll
         for (int u = 0; u < 4; ++u) ed[u] = perm[j + u];
 #pragma unroll
         for (int u = 0; u < 4; ++u) sv[u] = src[ed[u]];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          a[u] = Xv[sv[u] * hv + c];
-          x[u] = Xe[ed[u] * hv + c];
-        }
+        for (int u = 0; u < 4; ++u)
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const float4 h0 = a[u] + x[u];
-          H0[ed[u] * hv + c] = h0;
-          mh = fmaxf(mh, fmaxf(fmaxf(fabsf(h0.x), fabsf(h0.y)), fmaxf(fabsf(h0.z), fabsf(h0.w))));
-          r.push(act4_t<ACT>(h0, act, alpha));
-        }
+          for (int q = 0; q < PPL; ++q) {
+            a[u][q] = Xv[sv[u] * hv + cc[q]];
+            x[u][q] = Xe[ed[u] * hv + cc[q]];
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < PPL; ++q) {
+            const float4 h0 = a[u][q] + x[u][q];
+            if (ok[q]) {
+              H0[ed[u] * hv + cc[q]] = h0;
+              mh = amax4(mh, h0);
+            }
+            r[q].push(act4_t<ACT>(h0, act, alpha));
+          }
       }
       for (; j < en; ++j) {
-        const int64_t ed = perm[j];
-        const float4 h0 = Xv[src[ed] * hv + c] + Xe[ed * hv + c];
-        H0[ed * hv + c] = h0;
-        mh = fmaxf(mh, fmaxf(fmaxf(fabsf(h0.x), fabsf(h0.y)), fmaxf(fabsf(h0.z), fabsf(h0.w))));
-        r.push(act4_t<ACT>(h0, act, alpha));
+        const int64_t ed = perm[j], sv = src[ed];
+#pragma unroll
+        for (int q = 0; q < PPL; ++q) {
+          const float4 h0 = Xv[sv * hv + cc[q]] + Xe[ed * hv + cc[q]];
+          if (ok[q]) {
+            H0[ed * hv + cc[q]] = h0;
+            mh = amax4(mh, h0);
+          }
+          r[q].push(act4_t<ACT>(h0, act, alpha));
+        }
       }
-      const float4 sv = r.result();
-      S[v * hv + c] = sv;
-      ms = fmaxf(ms, fmaxf(fmaxf(fabsf(sv.x), fabsf(sv.y)), fmaxf(fabsf(sv.z), fabsf(sv.w))));
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) {
+        if (ok[q]) {
+          const float4 s4 = r[q].result();
+          S[v * hv + cc[q]] = s4;
+          ms = amax4(ms, s4);
+        }
+      }
     }
   }
   if (amax) block_max_to(amax, mh, ms, true);  // one atomic max per block
@@ -269,12 +298,19 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
     NT_REQUIRE(E == 0 || (Xv && Xe && src && H0), NT_EINVAL, "NULL pointer");
     if (vec) {
       const int64_t hv = h / 4;
-      if (hv >= 32) {  // rows of >= 32 pieces: a wave per node
+      if (hv >= 32) {  // rows of >= 32 pieces: a wave per node, every piece of the row in one pass
         const int grid = grid_for(V * 64, 256, 256 * 8);  // grid-stride: 32 waves per CU
-        NT_DISPATCH_RA(reduce, act,
-                       (init_aggregate_wave<R_, A_><<<grid, 256, 0, stream>>>(
-                           (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
-                           act_alpha, (float4*)H0, (float4*)S, amax_out)));
+        if (hv <= 64) {
+          NT_DISPATCH_RA(reduce, act,
+                         (init_aggregate_wave<R_, A_, 1><<<grid, 256, 0, stream>>>(
+                             (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
+                             act_alpha, (float4*)H0, (float4*)S, amax_out)));
+        } else {
+          NT_DISPATCH_RA(reduce, act,
+                         (init_aggregate_wave<R_, A_, 2><<<grid, 256, 0, stream>>>(
+                             (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
+                             act_alpha, (float4*)H0, (float4*)S, amax_out)));
+        }
         NT_LAUNCH_CHECK();
         return NT_OK;
       } else {

@@ -58,6 +58,8 @@ int fk_row_table(const int32_t* perm, const int32_t* dsts, const int64_t* src, c
 int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_t img_stride, void* img,
             hipStream_t stream);
 int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);
+// a library-owned (max|H|, max|S|) slot filled on `stream` (H or S may be NULL: that entry stays 0)
+int amax_scratch(const float* H, int64_t nh, const float* S, int64_t ns, float** out, hipStream_t stream);
 inline int64_t fk_image_bytes(int64_t h) { return 256 + ((h + 31) / 32) * ((h + 15) / 16) * 2 * 1024; }
 
 // Deeper-ring variant (S/H 2 chunks ahead); requires additionally NT <= 24.

@@ -29,6 +29,7 @@
 #include "common.hpp"
 #include "update.hpp"
 
+#ifdef NT_DIAG  // A/B variant: superseded by update_fk_kernel in the shipping library
 namespace nt {
 
 // Diagnostic build (NT_AS_DIAG=1): per-wave phase cycles summed over waves: gather (incl. barrier),
@@ -328,6 +329,7 @@ int launch_update_as(const UpdateArgs& a) {
 }
 
 }  // namespace nt
+#endif  // NT_DIAG
 
 // Debug-only (not part of include/notorch_amd.h): read (and optionally reset) the stamp sums of the
 #ifdef NT_DIAG

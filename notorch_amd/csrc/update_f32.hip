@@ -40,14 +40,16 @@ constexpr int kWaves = 4;
 // kernel selection for A/B runs (read per call):
 //   NT_UPDATE_KERNEL = as (default: A-stationary bf16x6) | x6 (LDS-ring bf16x6)
 //                      | stream | tile (exact fp32 MFMA)
+#ifdef NT_DIAG
 static char update_kernel_choice() {
 #ifdef NT_DIAG
   const char* v = getenv("NT_UPDATE_KERNEL");
   return (v && v[0]) ? v[0] : 'a';
 #else
-  return 'a';  // shipping build: as16 (h <= 304), x6 (h <= 512), fp32 MFMA tile kernel
+  return 'a';
 #endif
 }
+#endif
 
 struct UpdateGeom {
   int KB;   // 16-deep k blocks (Kpad = 16*KB >= h)
@@ -510,15 +512,29 @@ static int dispatch_cpw(const float* H, const float* S, const int64_t* src, cons
 
 }  // namespace nt
 
-// Packed image per layer (fp32 weights): [fp32 fragment image (16x16x4 MFMA)][bf16x6 image (32x32x16
-// MFMA)][bf16x6 image (16x16x32 MFMA)][fk image (two-part fp16, 16x16x32 MFMA, scale header)], each
-// part 256-B aligned; the update kernel variant picks the part it consumes.  Hidden sizes above 512
-// carry only the fk image.
+// Packed image per layer (fp32 weights).  Shipping library: h % 4 == 0 (or h > 512) carries only the
+// fk image (two-part fp16, 16x16x32 MFMA, scale header: every fp32 update, fused or not, and the
+// backward's dense dA run on update_fk_kernel); other h <= 512 carry only the fp32 fragment image of
+// the exact fp32 tile kernel (16x16x4 MFMA; the one kernel for h % 4 != 0).  Diagnostic library (A/B
+// variants): [fp32 fragment image][bf16x6 image (32x32x16)][bf16x6 image (16x16x32)][fk image], each
+// part 256-B aligned; the variant picks the part it consumes.
+static bool has_fk_image(int64_t h) {
+#ifdef NT_DIAG
+  (void)h;
+  return true;
+#else
+  return h % 4 == 0 || h > 512;
+#endif
+}
 static size_t f32_image_bytes(int64_t h) {
   if (h > 512) return 0;
+#ifndef NT_DIAG
+  if (h % 4 == 0) return 0;
+#endif
   const nt::UpdateGeom g = nt::geom_for(h);
   return ((size_t)g.KB * g.NT * 64 * sizeof(float4) + 255) & ~size_t(255);
 }
+#ifdef NT_DIAG
 static size_t x6_part_bytes(int64_t h) {
   return nt::x6_supported(h) ? ((nt::x6_image_bytes(h) + 255) & ~size_t(255)) : 0;
 }
@@ -526,13 +542,17 @@ static size_t x6_part_bytes(int64_t h) {
 static size_t as_part_bytes(int64_t h) {
   return nt::as_supported(h) ? ((nt::as_image_bytes(h) + 255) & ~size_t(255)) : 0;
 }
+#else
+static size_t x6_part_bytes(int64_t) { return 0; }
+static size_t as_part_bytes(int64_t) { return 0; }
+#endif
 
 static size_t fk_offset(int64_t h) { return f32_image_bytes(h) + x6_part_bytes(h) + as_part_bytes(h); }
 
 extern "C" size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype) {
   if (h <= 0) return 0;
   if (dtype == NT_BF16) return (nt::bf16_image_bytes(h) + 255) & ~size_t(255);
-  return fk_offset(h) + (((size_t)nt::fk_image_bytes(h) + 255) & ~size_t(255));
+  return fk_offset(h) + (has_fk_image(h) ? (((size_t)nt::fk_image_bytes(h) + 255) & ~size_t(255)) : 0);
 }
 
 extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, int dtype, void* Wp,
@@ -550,7 +570,7 @@ extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, i
   const size_t per_layer = nt_dmpnn_packed_weight_bytes(h, dtype);
   NT_REQUIRE(per_layer % 16 == 0, NT_EINVAL, "internal: packed layer size");
   hipStream_t stream = as_stream(stream_);
-  if (h <= 512) {
+  if (f32_image_bytes(h) > 0) {
     const UpdateGeom g = geom_for(h);
     // fp32 image of every layer (layer stride = per_layer bytes)
     for (int64_t l = 0; l < nlayers; ++l) {
@@ -561,6 +581,7 @@ extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, i
       NT_LAUNCH_CHECK();
     }
   }
+#ifdef NT_DIAG
   if (x6_supported(h)) {
     int rc = pack_weight_x6((const float*)W, nlayers, h, (int64_t)per_layer,
                             (char*)Wp + f32_image_bytes(h), stream);
@@ -571,6 +592,8 @@ extern "C" int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, i
                             (char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), stream);
     if (rc != NT_OK) return rc;
   }
+#endif
+  if (!has_fk_image(h)) return NT_OK;
   return fk_pack((const float*)W, nlayers, h, h * h, (int64_t)per_layer, (char*)Wp + fk_offset(h), stream);
 }
 
@@ -580,6 +603,7 @@ extern "C" int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h
   NT_REQUIRE(nlayers >= 0 && h > 0 && h <= 8192, NT_EINVAL, "bad sizes (1 <= h <= 8192)");
   if (nlayers == 0) return NT_OK;
   NT_REQUIRE(W && Wp && aligned16(Wp), NT_EINVAL, "NULL or misaligned pointer");
+  NT_REQUIRE(has_fk_image(h), NT_EUNSUPPORTED, "the fk image needs h % 4 == 0 (or h > 512)");
   const size_t per_layer = nt_dmpnn_packed_weight_bytes(h, NT_F32);
   return fk_pack((const float*)W, nlayers, h, h * h, (int64_t)per_layer, (char*)Wp + fk_offset(h),
                  as_stream(stream_));
@@ -629,9 +653,10 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
     return launch_update_bf16(H, S, src, rev, Wp, b, V, E, h, residual, act, act_alpha, H_out,
                               as_stream(stream_));
   const UpdateGeom g = geom_for(h);
+  hipStream_t stream = as_stream(stream_);
+#ifdef NT_DIAG
   const bool vec = (h % 4 == 0) && aligned16(H) && aligned16(S) && aligned16(H_out) &&
                    (b == nullptr || aligned16(b));
-  hipStream_t stream = as_stream(stream_);
   const char choice = update_kernel_choice();
   if (vec && choice == 'a' && as_supported(h)) {
     UpdateArgs a{(const float*)H, (const float*)S, src, rev,
@@ -645,6 +670,22 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                  stream};
     return launch_update_x6(a);
   }
+#else
+  // h % 4 == 0: update_fk_kernel in its plain mode (no aggregation); the split scales come from a
+  // max|H|, max|S| pass into a library-owned scratch slot (the C ABI call carries no amax)
+  if (h % 4 == 0) {
+    NT_REQUIRE(aligned16(H) && aligned16(S) && aligned16(H_out) && (b == nullptr || aligned16(b)), NT_EINVAL,
+               "fp32 with h % 4 == 0 needs 16-byte aligned feature pointers");
+    float* amax = nullptr;
+    int rc = amax_scratch((const float*)H, E * h, (const float*)S, V * h, &amax, stream);
+    if (rc != NT_OK) return rc;
+    UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
+                 0, 0, residual, act, act_alpha, (float*)H_out, stream};
+    return launch_update_fk(a, (const char*)Wp + fk_offset(h), amax, nullptr, nullptr, 0, 0, 0, nullptr,
+                            NT_SUM, NT_ACT_IDENTITY, 0.f, nullptr);
+  }
+  const bool vec = false;  // h % 4 != 0: the exact fp32 tile kernel's scalar rows
+#endif
   // 64-edge tiles while two workgroups still fit one CU's LDS (h <= 304), else 32-edge tiles.
   if (lds_bytes<64>(g) <= 80 * 1024)
     return dispatch_cpw<64>((const float*)H, (const float*)S, src, rev, (const float4*)Wp,
@@ -709,21 +750,37 @@ extern "C" int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const 
     return launch_update_bf16(X, X, nullptr, nullptr, Wp, nullptr, M, M, h, 0, NT_ACT_IDENTITY, 0.f, out,
                               as_stream(stream_));
   }
+#ifdef NT_DIAG
   NT_REQUIRE(amax_in ? (h % 4 == 0 && h <= 8192) : ps_supported(h), NT_EUNSUPPORTED,
              "nt_dmpnn_dense_matmul needs h % 4 == 0 (and h <= 304 without amax_in)");
+#else
+  NT_REQUIRE(h % 4 == 0 && h <= 8192, NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul needs h % 4 == 0 (fp32)");
+#endif
   if (M == 0) return NT_OK;
   NT_REQUIRE(X && Wp && out, NT_EINVAL, "NULL pointer");
   NT_REQUIRE(X != out, NT_EINVAL, "out aliases X");
   NT_REQUIRE(aligned16(X) && aligned16(out) && aligned16(Wp), NT_EINVAL, "pointers must be 16-byte aligned");
+#ifndef NT_DIAG
+  if (!amax_in) {  // max|X| into a library-owned scratch slot
+    float* slot = nullptr;
+    int rc = amax_scratch(nullptr, 0, (const float*)X, M * h, &slot, as_stream(stream_));
+    if (rc != NT_OK) return rc;
+    amax_in = slot;
+  }
+#endif
   if (amax_in) {
     UpdateArgs a{nullptr, (const float*)X, nullptr, nullptr, Wp, nullptr, M, M, h,
                  0, 0, 0, NT_ACT_IDENTITY, 0.f, (float*)out, as_stream(stream_)};
     return launch_update_fk(a, (const char*)Wp + fk_offset(h), amax_in, nullptr, nullptr, 0, 0, 0, nullptr,
                             NT_SUM, NT_ACT_IDENTITY, 0.f, nullptr);
   }
+#ifdef NT_DIAG
   const UpdateGeom g = geom_for(h);
   UpdateArgs a{(const float*)X, (const float*)X, nullptr, nullptr,
                (const char*)Wp + f32_image_bytes(h) + x6_part_bytes(h), nullptr, M, M, h,
                g.KB, g.NT, 0, NT_ACT_IDENTITY, 0.f, (float*)out, as_stream(stream_)};
   return launch_update_pk(a, nullptr, 0, nullptr, nullptr, NT_SUM, NT_ACT_IDENTITY, 0.f, nullptr);
+#else
+  return NT_OK;  // not reached: amax_in is set above
+#endif
 }

@@ -38,6 +38,12 @@
 
 #include "common.hpp"
 
+// FK_MFMA_MODE (A/B builds): 0 = per-(row tile, column tile) guarded MFMAs; 1 = branch-free steps
+// (column-tile count switched once per step, every row tile computed)
+#ifndef FK_MFMA_MODE
+#define FK_MFMA_MODE 0
+#endif
+
 namespace nt {
 namespace fk {
 
@@ -83,14 +89,17 @@ struct Args {
   int stagger;  // diagnostic: start delay of workgroup b = stagger * ((b / nxcd) % 4) x 8k cycles (0)
 };
 
-// power-of-two scale that maps a magnitude bound to < 2^14 (exponent clamped to [-100, 24]);
-// a zero or non-finite bound leaves the operand unscaled
+// power-of-two scale that maps a magnitude bound to < 2^14 (exponent at most 24; every finite
+// bound < 2^128 gets s >= -114, so no finite operand overflows fp16 after scaling).  A zero bound
+// leaves the operand unscaled; so does a non-finite one (an inf / NaN in H or S): the rows holding it
+// come out inf / NaN as in fp32, and finite entries above 65504 of that tensor overflow too (the
+// contract covers finite inputs).
 __host__ __device__ inline int scale_exp(float bound) {
-  if (!(bound > 0.f) || !(bound <= 3.0e38f)) return 0;
+  if (!(bound > 0.f) || !(bound <= 3.4028235e38f)) return 0;
   int e;
-  frexpf(bound, &e);  // bound < 2^e
+  frexpf(bound, &e);  // bound < 2^e, e <= 128
   int s = 14 - e;
-  return s < -100 ? -100 : (s > 24 ? 24 : s);
+  return s > 24 ? 24 : s;
 }
 
 // upper bound of |act(x)| for |x| <= m (every act code: relu / identity / gelu / silu <= m + 1,
@@ -311,6 +320,58 @@ __device__ __forceinline__ void fk_mfma(State<RT, CT, GD>& st, int c, int nrt) {
   }
 }
 
+// Branch-free MFMA step: NCT (compile time) active column tiles for this wave, and every row tile
+// of the tile computed (rows past the tile hold zeros in the A buffer, so their accumulators keep
+// whatever they held and are never stored).  One scalar branch per step (the NCT switch) instead of
+// one per (row tile, column tile).
+template <int RT, int CT, int P, int GD, int NCT>
+__device__ __forceinline__ void fk_mfma_nb(State<RT, CT, GD>& st) {
+  using St = State<RT, CT, GD>;
+  const char* bb = st.abuf + P * St::kBufB + st.lane * 16;
+  f16x8 a0 = *reinterpret_cast<const f16x8*>(bb);
+  f16x8 a1 = *reinterpret_cast<const f16x8*>(bb + St::kPartB);
+#pragma unroll
+  for (int rt = 0; rt < RT; ++rt) {
+    f16x8 n0 = a0, n1 = a1;
+    if (rt + 1 < RT) {
+      n0 = *reinterpret_cast<const f16x8*>(bb + (rt + 1) * 1024);
+      n1 = *reinterpret_cast<const f16x8*>(bb + St::kPartB + (rt + 1) * 1024);
+    }
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) {
+      const f16x8 w0 = as_f16x8(st.wb[P][j][0]), w1 = as_f16x8(st.wb[P][j][1]);
+      f32x4 t = st.acc[rt][j];
+      t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, a0, t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a1, t, 0, 0, 0);
+      t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a0, t, 0, 0, 0);
+      st.acc[rt][j] = t;
+    }
+    a0 = n0;
+    a1 = n1;
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
+template <int RT, int CT, int P, int GD>
+__device__ __forceinline__ void fk_mfma_sw(State<RT, CT, GD>& st, int c, int nrt) {
+#if FK_MFMA_MODE == 1
+  // active column tiles of this wave in chunk c (wave-uniform)
+  const int first = c * st.CTC + st.wave;
+  const int nct = first >= st.NT ? 0 : min(CT, (st.NT - first + 7) / 8);
+  if constexpr (CT >= 4) {
+    if (nct == 4) { fk_mfma_nb<RT, CT, P, GD, 4>(st); return; }
+  }
+  if constexpr (CT >= 3) {
+    if (nct == 3) { fk_mfma_nb<RT, CT, P, GD, 3>(st); return; }
+  }
+  if (nct == 2) { fk_mfma_nb<RT, CT, P, GD, 2>(st); return; }
+  if (nct == 1) { fk_mfma_nb<RT, CT, P, GD, 1>(st); return; }
+  (void)nrt;
+#else
+  fk_mfma<RT, CT, P, GD>(st, c, nrt);
+#endif
+}
+
 // Residual rows H[e] of (tile i, chunk c), column tile j, loaded straight into the accumulators:
 // issued by the epilogue of the previous (tile, chunk) as soon as it has stored column tile j, so
 // they land during the rest of that epilogue; fk_resid_scale multiplies them by s_A s_W before the
@@ -521,7 +582,6 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   const bool resid = (ABL & 32) == 0 && a.residual && a.H != nullptr;
   const bool info_writer = st.g16 == 0 && (RT == 8 || st.wave < 4);
   const int SPT = a.nchunks * a.KS;  // steps per tile
-  const int G = ntl * SPT;
 
   // ---- tile info: cur (tile i) and nxt (i + 1) row offsets, raw row of tile i + 2 in flight
   int2 cur, nxt;
@@ -576,12 +636,16 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   }
   fk_barrier();
 
-  // ---- main loop: one 32-deep k-step per iteration, two iterations per trip (register parity P: A
-  // buffer and W fragments of steps g and g + 2, gather slot of steps g + 1 and g + 3).  Every
-  // vector-memory op is unconditional and issued into registers the step has just freed: W two steps
-  // ahead, gathers three steps ahead, both before the epilogue's stores (vmcnt counts loads and
-  // stores in issue order, so the next two steps' waits do not cover the stores).
-  int g = 0, i = 0, k = 0;  // global step, tile-local index, step within the tile
+  // ---- main loop: per (tile, column chunk) unit, the residual scale, then the unit's KS k-steps as
+  // an inner loop of two steps per trip (register parity P: A buffer and W fragments of steps k and
+  // k + 2, gather slot of steps k + 1 and k + 3; KS is even, so every unit starts at parity 0), then
+  // the epilogue.  The epilogue loads the next unit's residual rows into the accumulators; they are
+  // consumed (the residual scale) before the inner loop starts, so inside the inner loop no
+  // accumulator is a pending load and the compiler's vmcnt waits count only the W fragments and
+  // gathers each step really needs: W two steps ahead and gathers three steps ahead stay in flight
+  // across the MFMAs.  Every vector-memory op is unconditional.
+  int i = 0, c = 0;  // tile-local index, column chunk
+  const int U = ntl * a.nchunks;
   [[maybe_unused]] unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tp = 0, tb = 0;
   if constexpr ((ABL & 256) != 0) tb = tp = __builtin_amdgcn_s_memtime();
   auto stamp = [&](int slot) __attribute__((always_inline)) {
@@ -591,21 +655,24 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
       tp = t;
     }
   };
-  while (g < G) {
+  for (int u = 0; u < U; ++u) {
+    // (1) residual rows (loaded by the previous epilogue) into the accumulators' scale; without a
+    // residual the accumulators are zero and the scale leaves them so.  Unconditional, so that no
+    // path into the inner loop carries an accumulator load still pending.
+    fk_resid_scale(st);
+    const int nrt = (n_cur + 15) >> 4;
+    const int kb = c * a.KS;
+    for (int s0 = 0; s0 < a.KS; s0 += 2) {
 #pragma unroll
-    for (int P = 0; P < 2; ++P) {
-      if (P == 0 || g < G) {
-        int c, s;
-        kcs(k, c, s);
-        // (1) residual rows (loaded by the previous epilogue) into the accumulators' scale
-        if (resid && s == 0) fk_resid_scale(st);
-        // (2) MFMAs of step g
+      for (int P = 0; P < 2; ++P) {
+        const int k = kb + s0 + P;
+        // (2) MFMAs of step k
         if constexpr ((ABL & 2) == 0) {
-          if (P == 0) fk_mfma<RT, CT, 0>(st, c, (n_cur + 15) >> 4);
-          else fk_mfma<RT, CT, 1>(st, c, (n_cur + 15) >> 4);
+          if (P == 0) fk_mfma_sw<RT, CT, 0>(st, c, nrt);
+          else fk_mfma_sw<RT, CT, 1>(st, c, nrt);
         }
         stamp(0);
-        // (3) W fragments of step g + 2 into the registers step g used
+        // (3) W fragments of step k + 2 into the registers step k used
         {
           int c2, s2;
           kcs(k + 2 < SPT ? k + 2 : k + 2 - SPT, c2, s2);
@@ -613,7 +680,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
           else fk_load_w<RT, CT, 1>(st, c2, s2);
         }
         stamp(1);
-        // (4) split step g + 1's staged piece into the other buffer, then gather step g + 3 into the
+        // (4) split step k + 1's staged piece into the other buffer, then gather step k + 3 into the
         // freed slot (tile i or i + 1)
         {
           const int k1 = k + 1 < SPT ? k + 1 : k + 1 - SPT;
@@ -633,30 +700,29 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
         stamp(2);
         if constexpr ((ABL & 16) == 0) fk_barrier();
         stamp(3);
-        // (5) epilogue at the chunk's last k-step; it starts the next (tile, chunk)'s residual loads
-        if ((ABL & 8) == 0 && s == a.KS - 1) {
-          const bool last_c = c + 1 == a.nchunks;
-          const int i_next = last_c ? (i + 1 < ntl ? i + 1 : i) : i, c_next = last_c ? 0 : c + 1;
-          fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
-          stamp(4);
-        }
-        // (6) advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
-        ++g;
-        if (++k == SPT) {
-          k = 0;
-          ++i;
-          cur = nxt;
-          n_cur = n_nxt;
-          const bool v2 = st.grow < h2.n;
-          nxt = row_offsets(a, raw2, v2);
-          if (info_writer) st.emap[((i + 1) % kEmaps) * ROWS + st.grow] = row_entry(raw2, v2);
-          if (h2.n > ROWS && i + 1 < ntl && tid == 0) atomicOr(&g_pk_timeout, 2u);
-          n_nxt = h2.n < ROWS ? h2.n : ROWS;
-          h2 = h3;
-          raw2 = row_raw<RT, TABLE>(a, h2, st.grow);
-          h3 = tile_head<RT, TABLE>(a, tile(i + 3));
-        }
       }
+    }
+    // (5) epilogue of the unit; it starts the next (tile, chunk)'s residual loads
+    const bool last_c = c + 1 == a.nchunks;
+    const int i_next = last_c ? (i + 1 < ntl ? i + 1 : i) : i, c_next = last_c ? 0 : c + 1;
+    if constexpr ((ABL & 8) == 0) {
+      fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
+      stamp(4);
+    }
+    // (6) advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
+    c = c_next;
+    if (last_c) {
+      ++i;
+      cur = nxt;
+      n_cur = n_nxt;
+      const bool v2 = st.grow < h2.n;
+      nxt = row_offsets(a, raw2, v2);
+      if (info_writer) st.emap[((i + 1) % kEmaps) * ROWS + st.grow] = row_entry(raw2, v2);
+      if (h2.n > ROWS && i + 1 < ntl && tid == 0) atomicOr(&g_pk_timeout, 2u);
+      n_nxt = h2.n < ROWS ? h2.n : ROWS;
+      h2 = h3;
+      raw2 = row_raw<RT, TABLE>(a, h2, st.grow);
+      h3 = tile_head<RT, TABLE>(a, tile(i + 3));
     }
   }
   if (a.amax_out) {

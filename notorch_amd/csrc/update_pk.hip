@@ -22,6 +22,8 @@
 // Supports h % 4 == 0, h <= 304, E * h / 4 < 2^31, V * h / 4 < 2^31.
 #include <stdlib.h>
 
+#include <atomic>
+
 #include <type_traits>
 
 #include "common.hpp"
@@ -46,6 +48,15 @@ __device__ unsigned long long g_pk_stamps[10];
 #include "update_fk2.hpp"  // A/B: LDS-staged output variant (NT_FK=2)
 #endif
 
+namespace nt {
+int cu_count();   // update_ps.hip
+int xcd_count();  // update_ps.hip
+}  // namespace nt
+
+#ifdef NT_DIAG
+// ------------------------------------------------------------------------------ pk (A/B only)
+// The persistent bf16x6 K-slice-ring kernel: superseded by update_fk_kernel, kept in the diagnostic
+// library for A/B runs.
 namespace nt {
 
 namespace {
@@ -671,9 +682,6 @@ int dispatch_pk(const Args& a, int ks, int grid, hipStream_t stream,
 
 }  // namespace
 
-int cu_count();   // update_ps.hip
-int xcd_count();  // update_ps.hip
-
 int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntiles,
                      const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
                      float* S_out) {
@@ -726,7 +734,10 @@ int launch_update_pk(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
     return dispatch_pk<NT_ACT_IDENTITY, NT_ACT_IDENTITY, true>(a, KS, grid, u.stream, Seq{});
   return dispatch_pk<-1, -1, false>(a, KS, grid, u.stream, Seq{});
 }
+}  // namespace nt
+#endif  // NT_DIAG
 
+namespace nt {
 // ------------------------------------------------------------------------------ fk launcher
 namespace {
 template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL>
@@ -892,9 +903,10 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   a.E = u.E;
   a.h = (int)u.h;
   a.hv = (int)(u.h / 4);
-  // at least three k-steps per tile (update_fk_kernel gathers three steps ahead, within the next
-  // tile at most); a k-step past the image reads zeros (buffer range) and masked-off pieces
-  a.KS = fk::ks_for(u.h) < 3 ? 3 : fk::ks_for(u.h);
+  // an even number of k-steps, at least four, per tile (update_fk_kernel runs two steps per inner
+  // trip and gathers three steps ahead, within the next tile at most); a k-step past the image reads
+  // zeros (buffer range) and masked-off pieces
+  a.KS = fk::ks_for(u.h) < 4 ? 4 : (fk::ks_for(u.h) + 1) / 2 * 2;
   a.NT = fk::nt_for(u.h);
   a.residual = u.residual;
   a.act = u.act;
@@ -960,6 +972,29 @@ int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream) {
   fk::absmax_kernel<<<grid_for(n / 4 + 1, 256, 256 * 8), 256, 0, stream>>>(X, n, out);
   NT_LAUNCH_CHECK();
   return NT_OK;
+}
+
+// Split-scale scratch for the C ABI entry points that carry no amax (nt_dmpnn_update,
+// nt_dmpnn_dense_matmul without amax_in): a ring of (max|H|, max|S|) slots in device memory owned by
+// the library.  Each call takes the next slot (host-side counter), zeroes it on its stream and runs
+// the max passes into it, so calls on different streams get different slots; a slot is reused only
+// after kAmaxRing later calls, long after its layer kernel has read it.
+constexpr int kAmaxRing = 4096;
+__device__ float g_amax_ring[kAmaxRing][2];
+
+int amax_scratch(const float* H, int64_t nh, const float* S, int64_t ns, float** out, hipStream_t stream) {
+  static std::atomic<unsigned> next{0};
+  float* base = nullptr;
+  if (hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_amax_ring)) != hipSuccess) {
+    set_error("amax scratch: hipGetSymbolAddress failed");
+    return NT_EHIP;
+  }
+  float* slot = base + 2 * (next.fetch_add(1, std::memory_order_relaxed) % kAmaxRing);
+  NT_HIP(hipMemsetAsync(slot, 0, 2 * sizeof(float), stream));
+  int rc = H ? fk_absmax(H, nh, slot, stream) : NT_OK;
+  if (rc == NT_OK && S) rc = fk_absmax(S, ns, slot + 1, stream);
+  *out = slot;
+  return rc;
 }
 
 }  // namespace nt

@@ -671,8 +671,9 @@ extern "C" int nt_dmpnn_tile_plan(const int32_t* dst_ptr, int64_t V, int64_t E, 
   return nt_dmpnn_tile_plan_hubs(dst_ptr, V, E, stride, INT32_MAX, tile_ptr, ntiles, dst_sorted, stream_);
 }
 
+#ifdef NT_DIAG
 namespace nt {
-// Called by nt_dmpnn_update_fused (update_f32.hip) with the as16 weight image.
+// A/B only: the persistent producer/consumer ps kernel (NT_FUSED_KERNEL=ps) or the pk kernel.
 int launch_update_ps(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntiles,
                      const int32_t* perm, const int32_t* dsts, int reduce, int aact, float aalpha,
                      float* S_out) {
@@ -729,6 +730,7 @@ int launch_update_ps(const UpdateArgs& u, const int32_t* tile_ptr, int64_t ntile
 #endif
 }
 }  // namespace nt
+#endif  // NT_DIAG
 
 #ifdef NT_DIAG
 // Debug-only (not part of include/notorch_amd.h): read (and optionally reset) the stamp sums of the

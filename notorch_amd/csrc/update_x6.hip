@@ -27,6 +27,7 @@
 #include "common.hpp"
 #include "update.hpp"
 
+#ifdef NT_DIAG  // A/B variant: superseded by update_fk_kernel in the shipping library
 namespace nt {
 
 // Diagnostic-build stamp accumulators (cycles summed over waves): issue, A read+split, MFMA
@@ -547,6 +548,7 @@ int launch_update_x6(const UpdateArgs& a) {
 }
 
 }  // namespace nt
+#endif  // NT_DIAG
 
 // Debug-only (not part of include/notorch_amd.h): read (and optionally reset) the stamp sums of the
 #ifdef NT_DIAG

@@ -467,11 +467,11 @@ __device__ __forceinline__ void split2s(const float (&x)[8], float s, f16x8& p0,
 // 2^(14 - e): the power-of-two scale that maps |x| <= bound below 2^14 (update_fk.hpp scale_exp, but
 // up to 2^120: tiny gradients are scaled up all the way, and the result is unscaled in two steps)
 __device__ __forceinline__ int wg_scale_exp(float bound) {
-  if (!(bound > 0.f) || !(bound <= 3.0e38f)) return 0;
+  if (!(bound > 0.f) || !(bound <= 3.4028235e38f)) return 0;
   int e;
-  frexpf(bound, &e);
+  frexpf(bound, &e);  // e <= 128 for every finite bound, so s >= -114 keeps it below 2^14
   const int s = 14 - e;
-  return s < -100 ? -100 : (s > 120 ? 120 : s);
+  return s > 120 ? 120 : s;
 }
 __device__ __forceinline__ float wg_act_bound(float m, int act, float alpha) {
   if (act == NT_ACT_RELU || act == NT_ACT_IDENTITY) return m;

@@ -104,13 +104,21 @@ def launch_local_ranks(argv: list[str], nprocs: int, master_port: int | None = N
             if live:
                 time.sleep(poll_s)
     finally:
-        for p in procs:
-            if p.poll() is None:
-                try:
-                    p.wait(timeout=30)
-                except subprocess.TimeoutExpired:
-                    p.kill()
-                    p.wait()
+        # normal exit: nothing is left running.  On an exception / KeyboardInterrupt in the parent,
+        # signal every rank still running first, then wait on one shared deadline, then kill.
+        running = [p for p in procs if p.poll() is None]
+        for p in running:
+            try:
+                p.send_signal(signal.SIGTERM)
+            except ProcessLookupError:
+                pass
+        deadline = time.monotonic() + 30.0
+        for p in running:
+            try:
+                p.wait(timeout=max(0.0, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
     return rc
 
 

@@ -1,10 +1,15 @@
-"""Training-step timing of ChempropBlock + Sum readout (forward + backward) at config 2.
+"""Training-step timing of ChempropBlock + Sum readout at config 2 (or config 3 with --kind zinc
+--h 512 --depth 5 --dtype bf16), as the reference trains: zero_grad, forward, backward and an
+Adam(lr=1e-4) step (notorch/lightning_models/model.py:153 optim_factory, :224-241 training_step,
+:273 configure_optimizers; Lightning calls optimizer.step() every batch).  The step after the
+optimizer sees new weights, so the forward re-packs them (one pack per layer weight).
 
 Modes: `kernel` (the kernel backward, the weight grad per NT_WGRAD) and `torch` (the
-recompute-in-torch backward, NT_BWD=torch).  bench.py's `training` key runs this once per weight-grad
-path (NT_WGRAD=kernel / library), each in a fresh process, with --json.
+recompute-in-torch backward, NT_BWD=torch).  bench.py's `training` key runs this in fresh processes
+with --json (the default weight-grad path as the headline, NT_WGRAD=library as a comparison).
 Usage: python tools/train_bench.py [--kind qm9] [--mols 4096] [--h 300] [--depth 3] [--dtype f32|bf16]
-                                  [--steps 30] [--warmup 10] [--warmup-s 0] [--modes kernel,torch] [--json]"""
+                                  [--steps 30] [--warmup 10] [--warmup-s 0] [--modes kernel,torch]
+                                  [--optim adam|none] [--json]"""
 import argparse
 import json
 import os
@@ -33,6 +38,9 @@ def main():
                    help="after the counted warm-ups, keep warming up until this many seconds have passed "
                         "(lets the clocks settle in a fresh process)")
     p.add_argument("--modes", default="kernel,torch")
+    p.add_argument("--optim", default="adam", choices=["adam", "none"],
+                   help="adam: Adam(lr=1e-4).step() in every training step (the reference's default "
+                        "optim_factory); none: forward + backward only")
     p.add_argument("--json", action="store_true", help="print one JSON object instead of the table")
     a = p.parse_args()
     from notorch_amd import _lib
@@ -51,12 +59,15 @@ def main():
     Xv_d = Gd.node_feats.requires_grad_(True)
     Xe_d = Gd.edge_feats.requires_grad_(True)
     E = G.num_edges
+    opt = torch.optim.Adam(blk.parameters(), lr=1e-4) if a.optim == "adam" else None
 
     def step():
         blk.zero_grad(set_to_none=True)
         Xv_d.grad = Xe_d.grad = None
         out = blk(Gd.update(node_feats=Xv_d, edge_feats=Xe_d))
         ro(out).float().pow(2).sum().backward()
+        if opt is not None:
+            opt.step()
 
     def fwd():
         with torch.no_grad():
@@ -85,11 +96,12 @@ def main():
     if a.json:
         print(json.dumps({
             "V": G.num_nodes, "E": E, "h": a.h, "depth": a.depth, "dtype": a.dtype,
-            "weight_grad": os.environ.get("NT_WGRAD", "default"), "warmup": a.warmup, "steps": a.steps,
+            "weight_grad": os.environ.get("NT_WGRAD", "default"), "optim": a.optim,
+            "warmup": a.warmup, "steps": a.steps,
             "ms": res, "edge_messages_per_s": {k: E * a.depth / (v * 1e-3) for k, v in res.items()},
         }), flush=True)
         return
-    print(f"{a.kind} V={G.num_nodes} E={E} h={a.h} depth={a.depth} {a.dtype}")
+    print(f"{a.kind} V={G.num_nodes} E={E} h={a.h} depth={a.depth} {a.dtype} optim={a.optim}")
     for k, v in res.items():
         print(f"{k:14s} {v:8.3f} ms/step  {E * a.depth / (v * 1e-3):.3e} edge-msg/s")
 
