@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define NT_ABI_VERSION 3
+#define NT_ABI_VERSION 4
 
 #if defined(NT_BUILD)
 #define NT_API __attribute__((visibility("default")))
@@ -317,6 +317,22 @@ NT_API int nt_softmax_pool(const void* X, const float* scores, const int32_t* se
                            const int32_t* perm, int64_t nseg, int64_t h, int dtype, void* out,
                            void* stream);
 
+/*
+ * Backward of nt_node_scores + nt_softmax_pool (the Gated / SDPAttention readouts trained through
+ * lightning_models/model.py:224-241; reference: ATen autograd of agg.py:50-86).  For dout (nseg x h):
+ *   dalpha[v] = <dout[g], X[v]>,  c_g = <dout[g], out[g]>,  ds[v] = alpha[v] (dalpha[v] - c_g)
+ *   dX[v]     = alpha[v] dout[g] + ds[v] key[v]   (key = a: Gated; Q[g] / sqrt_key: SDPA)
+ *   P[g]      = sum_{v in g} ds[v] X[v]           (ascending v, fp32; Gated: da = sum_g P[g],
+ *                                                  db = sum_v ds[v]; SDPA: dQ = P / sqrt_key)
+ * alpha is recomputed exactly as nt_softmax_pool computes it.  X, out, dout, a / Q, dX: dtype;
+ * scores, ds (n), P (nseg x h), stats (3 nseg workspace): fp32.  node_seg = batch_node_index.
+ */
+NT_API int nt_softmax_pool_backward(const void* X, const float* scores, const int32_t* seg_ptr,
+                                    const int32_t* perm, const int64_t* node_seg, int64_t nseg, int64_t n,
+                                    int64_t h, const void* out, const void* dout, const void* a,
+                                    const void* Q, float sqrt_key, int dtype, float* stats, void* dX,
+                                    float* ds, float* P, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Backward (training through ChempropBlock, lightning_models/model.py:224-241).  The reference's
  * backward is ATen autograd of chemprop.py:28-43,81-88 (index_backward = index_add, scatter_add
@@ -377,7 +393,8 @@ NT_API int nt_dropout_residual(const void* base, const void* Y, int64_t n, float
  *   nt_dmpnn_edge_backward_arg: nt_dmpnn_edge_backward with the dS term masked by arg (reduce of the
  *                               layer's aggregation = max | min): (arg[dst e][c] == e ? dS[dst e][c] : 0)
  *   nt_gather_rows_arg:         out[i] = (base ? base[i] : 0) + (arg[idx i] == i ? X[idx i] : 0)
- * fp32 only; amax_out as nt_dmpnn_edge_backward. */
+ * fp32 or bf16 storage (bf16: values widened exactly, compared / masked in fp32, one rounding at the
+ * store; amax_out must be NULL); amax_out (fp32) as nt_dmpnn_edge_backward. */
 NT_API int nt_segment_arg(const void* X, const int32_t* seg_ptr, const int32_t* perm, int64_t nseg,
                           int64_t h, int reduce, int act, float act_alpha, int dtype, int32_t* arg,
                           void* stream);

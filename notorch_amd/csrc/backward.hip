@@ -324,6 +324,71 @@ __global__ void __launch_bounds__(256) gather_rows_bf16(const bf16_raw* __restri
   }
 }
 
+// ---- bf16 max / min backward: the fp32 arg kernels' math on bf16 storage (one element per lane; the
+// values are widened exactly, compared and masked in fp32, rounded once at the store) ----
+__device__ __forceinline__ float bf_ld(const bf16_raw* p) { return __uint_as_float((unsigned)*p << 16); }
+__device__ __forceinline__ bf16_raw bf_st(float x) { return __builtin_bit_cast(bf16_raw, (__bf16)x); }
+
+template <int ACT, bool MAXR>
+__global__ void __launch_bounds__(256) segment_arg_bf16(const bf16_raw* __restrict__ X,
+                                                        const int32_t* __restrict__ seg_ptr,
+                                                        const int32_t* __restrict__ perm, int64_t nseg,
+                                                        int64_t h, int act, float alpha,
+                                                        int32_t* __restrict__ arg) {
+  const int64_t total = nseg * h;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t v = t / h, c = t - v * h;
+    const int32_t b = seg_ptr[v], en = seg_ptr[v + 1];
+    int32_t best_r = -1;
+    float best = 0.f;
+    for (int32_t j = b; j < en; ++j) {
+      const int32_t r = perm ? perm[j] : j;
+      // the forward aggregates act(H) of the stored (bf16) H; act evaluated in fp32 as there
+      const float x = act_t<ACT>(bf_ld(X + (int64_t)r * h + c), act, alpha);
+      if (best_r < 0 || (MAXR ? x > best : x < best)) {
+        best = x;
+        best_r = r;
+      }
+    }
+    arg[t] = best_r;
+  }
+}
+
+template <int ACT>
+__global__ void __launch_bounds__(256) edge_backward_arg_bf16(
+    const bf16_raw* __restrict__ G, const bf16_raw* __restrict__ H, const bf16_raw* __restrict__ dA,
+    const bf16_raw* __restrict__ dS, const int32_t* __restrict__ arg, const int64_t* __restrict__ dst,
+    const int32_t* __restrict__ rev_ptr, const int32_t* __restrict__ rev_perm, int64_t E, int64_t h,
+    int residual, int act, float alpha, bf16_raw* __restrict__ Gout) {
+  const int64_t total = E * h;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = t / h, c = t - e * h;
+    const int64_t v = dst[e];
+    float dm = arg[v * h + c] == e ? bf_ld(dS + v * h + c) : 0.f;
+    for (int32_t j = rev_ptr[e]; j < rev_ptr[e + 1]; ++j) dm -= bf_ld(dA + (int64_t)rev_perm[j] * h + c);
+    float g = act_grad_t<ACT>(bf_ld(H + t), act, alpha) * dm;
+    if (residual) g += bf_ld(G + t);
+    Gout[t] = bf_st(g);
+  }
+}
+
+__global__ void __launch_bounds__(256) gather_rows_arg_bf16(const bf16_raw* __restrict__ base,
+                                                            const bf16_raw* __restrict__ X,
+                                                            const int64_t* __restrict__ idx,
+                                                            const int32_t* __restrict__ arg, int64_t n,
+                                                            int64_t h, bf16_raw* __restrict__ out) {
+  const int64_t total = n * h;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t i = t / h, c = t - i * h;
+    const int64_t s = idx[i];
+    const float x = arg[s * h + c] == i ? bf_ld(X + s * h + c) : 0.f;
+    out[t] = bf_st(base ? bf_ld(base + t) + x : x);
+  }
+}
+
 static bool valid_act(int a) { return a >= NT_ACT_IDENTITY && a <= NT_ACT_SIGMOID; }
 
 #define NT_BW_DISPATCH_ACT(ACT, LAUNCH)                                          \
@@ -483,7 +548,7 @@ extern "C" int nt_segment_arg(const void* X, const int32_t* seg_ptr, const int32
                               void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_segment_arg: fp32 only");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(reduce == NT_MAX || reduce == NT_MIN, NT_EINVAL, "nt_segment_arg: reduce must be max or min");
   NT_REQUIRE(valid_act(act), NT_EINVAL, "bad act code");
   NT_REQUIRE(nseg >= 0 && h > 0, NT_EINVAL, "bad sizes");
@@ -491,6 +556,15 @@ extern "C" int nt_segment_arg(const void* X, const int32_t* seg_ptr, const int32
   NT_REQUIRE(X && seg_ptr && arg, NT_EINVAL, "NULL pointer");
   hipStream_t stream = as_stream(stream_);
   const int grid = grid_for(nseg * h, 256, 256 * 32);
+  if (dtype == NT_BF16) {
+#define NT_SA(MAXR_)                                                                          \
+  NT_BW_DISPATCH_ACT(act, (segment_arg_bf16<A_, MAXR_><<<grid, 256, 0, stream>>>(             \
+                              (const bf16_raw*)X, seg_ptr, perm, nseg, h, act, act_alpha, arg)))
+    if (reduce == NT_MAX) NT_SA(true); else NT_SA(false);
+#undef NT_SA
+    NT_LAUNCH_CHECK();
+    return NT_OK;
+  }
 #define NT_SA(MAXR_)                                                                          \
   NT_BW_DISPATCH_ACT(act, (segment_arg_kernel<A_, MAXR_><<<grid, 256, 0, stream>>>(           \
                               (const float*)X, seg_ptr, perm, nseg, h, act, act_alpha, arg)))
@@ -507,13 +581,23 @@ extern "C" int nt_dmpnn_edge_backward_arg(const void* G, const void* H, const vo
                                           int dtype, void* G_out, float* amax_out, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_edge_backward_arg: fp32 only");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(valid_act(act), NT_EINVAL, "bad act code");
   NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
   if (E == 0) return NT_OK;
   NT_REQUIRE(H && dA && dS && arg && dst && rev_ptr && rev_perm && G_out, NT_EINVAL, "NULL pointer");
   NT_REQUIRE(!residual || G, NT_EINVAL, "residual needs G");
   hipStream_t stream = as_stream(stream_);
+  if (dtype == NT_BF16) {
+    NT_REQUIRE(amax_out == nullptr, NT_EINVAL, "amax_out is fp32 only");
+    const int grid = grid_for(E * h, 256, 256 * 32);
+    NT_BW_DISPATCH_ACT(act, (edge_backward_arg_bf16<A_><<<grid, 256, 0, stream>>>(
+                                (const bf16_raw*)G, (const bf16_raw*)H, (const bf16_raw*)dA,
+                                (const bf16_raw*)dS, arg, dst, rev_ptr, rev_perm, E, h, residual, act,
+                                act_alpha, (bf16_raw*)G_out)));
+    NT_LAUNCH_CHECK();
+    return NT_OK;
+  }
   if (h % 4 == 0 && aligned16(H) && aligned16(dA) && aligned16(dS) && aligned16(G_out) &&
       aligned16(arg) && (!residual || aligned16(G))) {
     const int64_t hw = h / 4;
@@ -537,11 +621,18 @@ extern "C" int nt_gather_rows_arg(const void* base, const void* X, const int64_t
                                   int64_t n, int64_t h, int dtype, void* out, float* amax_out, void* stream_) {
   using namespace nt;
   clear_error();
-  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_gather_rows_arg: fp32 only");
+  NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(n >= 0 && h > 0, NT_EINVAL, "bad sizes");
   if (n == 0) return NT_OK;
   NT_REQUIRE(X && idx && arg && out, NT_EINVAL, "NULL pointer");
   hipStream_t stream = as_stream(stream_);
+  if (dtype == NT_BF16) {
+    NT_REQUIRE(amax_out == nullptr, NT_EINVAL, "amax_out is fp32 only");
+    gather_rows_arg_bf16<<<grid_for(n * h, 256, 256 * 32), 256, 0, stream>>>(
+        (const bf16_raw*)base, (const bf16_raw*)X, idx, arg, n, h, (bf16_raw*)out);
+    NT_LAUNCH_CHECK();
+    return NT_OK;
+  }
   if (h % 4 == 0 && aligned16(X) && aligned16(out) && aligned16(arg) && (!base || aligned16(base))) {
     const int64_t hw = h / 4;
     gather_rows_arg_kernel<float4, int4><<<grid_for(n * hw, 256, 256 * 32), 256, 0, stream>>>(

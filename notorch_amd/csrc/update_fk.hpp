@@ -43,6 +43,10 @@
 #ifndef FK_MFMA_MODE
 #define FK_MFMA_MODE 0
 #endif
+// FK_PRIO (A/B builds): 1 = s_setprio 1 for waves 4-7 for the whole loop
+#ifndef FK_PRIO
+#define FK_PRIO 0
+#endif
 
 namespace nt {
 namespace fk {
@@ -645,6 +649,11 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   // gathers each step really needs: W two steps ahead and gathers three steps ahead stay in flight
   // across the MFMAs.  Every vector-memory op is unconditional.
   int i = 0, c = 0;  // tile-local index, column chunk
+#if FK_PRIO
+  // static priority for the second-dispatched half (waves 4-7: each SIMD's younger wave), which
+  // otherwise loses every issue arbitration against its partner (MI355X_MICROARCH, two waves per SIMD)
+  if (st.wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
   const int U = ntl * a.nchunks;
   [[maybe_unused]] unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tp = 0, tb = 0;
   if constexpr ((ABL & 256) != 0) tb = tp = __builtin_amdgcn_s_memtime();

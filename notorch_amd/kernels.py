@@ -641,9 +641,10 @@ def weight_grad(G: Tensor, H: Tensor | None, S: Tensor, src: Tensor | None, rev:
 def segment_arg(X: Tensor, seg_ptr: Tensor, perm: Tensor | None, nseg: int, reduce: str, *,
                 act: tuple[int, float] = (_lib.NT_ACT_IDENTITY, 0.0)) -> Tensor:
     """int32 (nseg x h): the first row (ascending CSR order) of each segment holding the max / min
-    of act(X) per column, -1 for empty segments (torch_scatter scatter_max / scatter_min's arg)."""
+    of act(X) per column, -1 for empty segments (torch_scatter scatter_max / scatter_min's arg).
+    fp32 or bf16 X."""
     dev = _require_device(X, seg_ptr, perm)
-    _require_f32("X", X)
+    code = _require_feat("X", X)
     if reduce not in ("max", "min"):
         raise ValueError("segment_arg: reduce must be 'max' or 'min'")
     h = X.shape[1]
@@ -651,7 +652,7 @@ def segment_arg(X: Tensor, seg_ptr: Tensor, perm: Tensor | None, nseg: int, redu
     if X.shape[0] == 0:  # no rows: every segment is empty
         return arg.fill_(-1)
     _run(dev, _lib.load().nt_segment_arg, _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce),
-         act[0], act[1], NT_F32, _ptr(arg), _stream(dev))
+         act[0], act[1], code, _ptr(arg), _stream(dev))
     return arg
 
 
@@ -659,15 +660,18 @@ def dmpnn_edge_backward_arg(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor,
                             rev_ptr: Tensor, rev_perm: Tensor, *, residual: bool = True,
                             act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0), amax: Tensor | None = None) -> Tensor:
     """dL/dH_l for a max / min aggregation (arg = segment_arg of act(H_l) over the dst CSR); amax (1
-    zero-filled device float, optional) is raised to max|out|."""
+    zero-filled device float, optional, fp32 only) is raised to max|out|.  fp32 or bf16 storage."""
     dev = _require_device(G, H, dA, dS, arg, dst, rev_ptr, rev_perm, amax)
-    for n_, t in (("H", H), ("dA", dA), ("dS", dS)):
-        _require_f32(n_, t)
+    code = _require_feat("H", H)
+    for n_, t in (("dA", dA), ("dS", dS)) + ((("G", G),) if G is not None else ()):
+        _require_feat(n_, t, H.dtype)
+    if amax is not None and code != NT_F32:
+        raise ValueError("amax is fp32 only")
     E, h = H.shape
     V = dS.shape[0]
     out = torch.empty_like(H)
     _run(dev, _lib.load().nt_dmpnn_edge_backward_arg, _ptr(G), _ptr(H), _ptr(dA), _ptr(dS), _ptr(arg),
-         _ptr(dst), _ptr(rev_ptr), _ptr(rev_perm), V, E, h, int(residual), act[0], act[1], NT_F32,
+         _ptr(dst), _ptr(rev_ptr), _ptr(rev_perm), V, E, h, int(residual), act[0], act[1], code,
          _ptr(out), _ptr(amax), _stream(dev))
     return out
 
@@ -675,12 +679,16 @@ def dmpnn_edge_backward_arg(G: Tensor | None, H: Tensor, dA: Tensor, dS: Tensor,
 def gather_rows_arg(X: Tensor, idx: Tensor, arg: Tensor, *, base: Tensor | None = None,
                     amax: Tensor | None = None) -> Tensor:
     """out[i] = base[i] + (arg[idx i] == i ? X[idx i] : 0) (max / min scatter backward); amax as
-    dmpnn_edge_backward_arg."""
+    dmpnn_edge_backward_arg.  fp32 or bf16."""
     dev = _require_device(X, idx, arg, base, amax)
-    _require_f32("X", X)
+    code = _require_feat("X", X)
+    if base is not None:
+        _require_feat("base", base, X.dtype)
+    if amax is not None and code != NT_F32:
+        raise ValueError("amax is fp32 only")
     n, h = idx.numel(), X.shape[1]
     out = torch.empty(n, h, dtype=X.dtype, device=dev)
-    _run(dev, _lib.load().nt_gather_rows_arg, _ptr(base), _ptr(X), _ptr(idx), _ptr(arg), n, h, NT_F32,
+    _run(dev, _lib.load().nt_gather_rows_arg, _ptr(base), _ptr(X), _ptr(idx), _ptr(arg), n, h, code,
          _ptr(out), _ptr(amax), _stream(dev))
     return out
 
@@ -876,6 +884,33 @@ def softmax_pool(X: Tensor, scores: Tensor, seg_ptr: Tensor, perm: Tensor | None
     _run(dev, _lib.load().nt_softmax_pool,
          _ptr(X), _ptr(scores), _ptr(seg_ptr), _ptr(perm), nseg, h, code, _ptr(out), _stream(dev))
     return out
+
+
+def softmax_pool_backward(X: Tensor, scores: Tensor, seg_ptr: Tensor, perm: Tensor | None, node_seg: Tensor,
+                          nseg: int, out: Tensor, dout: Tensor, *, a: Tensor | None = None,
+                          Q: Tensor | None = None, sqrt_key: float = 1.0) -> tuple[Tensor, Tensor, Tensor]:
+    """Backward of node_scores + softmax_pool for dout (nseg x h): (dX, ds, P) with ds the fp32 score
+    gradient and P[g] = sum_{v in g} ds[v] X[v] (fp32): Gated da = P.sum(0), db = ds.sum(); SDPA
+    dQ = P / sqrt_key (nt_softmax_pool_backward)."""
+    dev = _require_device(X, scores, seg_ptr, perm, node_seg, out, dout, a, Q)
+    code = _require_feat("X", X)
+    _require_feat("out", out, X.dtype)
+    _require_feat("dout", dout, X.dtype)
+    if (a is None) == (Q is None):
+        raise ValueError("pass exactly one of a (Gated) and Q (SDPAttention)")
+    _require_feat("a" if a is not None else "Q", a if a is not None else Q, X.dtype)
+    _require_i64("batch_node_index", node_seg)
+    if scores.dtype != torch.float32 or scores.numel() != X.shape[0]:
+        raise ValueError("scores must be fp32 with one entry per row of X")
+    n, h = X.shape
+    dX = torch.empty_like(X)
+    ds = torch.empty(n, dtype=torch.float32, device=dev)
+    P = torch.empty(nseg, h, dtype=torch.float32, device=dev)
+    stats = torch.empty(max(3 * nseg, 1), dtype=torch.float32, device=dev)
+    _run(dev, _lib.load().nt_softmax_pool_backward,
+         _ptr(X), _ptr(scores), _ptr(seg_ptr), _ptr(perm), _ptr(node_seg), nseg, n, h, _ptr(out), _ptr(dout),
+         _ptr(a), _ptr(Q), float(sqrt_key), code, _ptr(stats), _ptr(dX), _ptr(ds), _ptr(P), _stream(dev))
+    return dX, ds, P
 
 
 # ------------------------------------------------------------------------------------ dropout

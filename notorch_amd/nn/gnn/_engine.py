@@ -645,9 +645,9 @@ def _weight_grad(G: Tensor, A: Tensor) -> Tensor:
 
 def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, residual, V, need_x,
                    drop=None, H_last=None):
-    """Kernel backward of block_forward (see csrc/backward.hip).  reduce in {sum, mean}; fp32 also
-    max / min, whose aggregations send each gradient element to its arg (torch_scatter's scatter_max
-    / scatter_min): H_last = the forward's H_d, for the final node scatter's arg.
+    """Kernel backward of block_forward (see csrc/backward.hip), fp32 or bf16 storage, every reduce:
+    max / min aggregations send each gradient element to its arg (torch_scatter's scatter_max /
+    scatter_min): H_last = the forward's H_d, for the final node scatter's arg.
     Returns (dXv, dXe, [dW_l], [db_l])."""
     maxmin = reduce in ("max", "min")
     E, h = states[0][0].shape if states else dH.shape
@@ -728,16 +728,16 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
 
 
 class ChempropBlockFunction(torch.autograd.Function):
-    """Kernel forward; kernel backward for reduce in {sum, mean} (gather/scatter/element-wise HIP
-    kernels + two library GEMMs per layer), recompute-in-torch-device-ops backward for max/min."""
+    """Kernel forward; kernel backward (block_backward: gather / scatter / element-wise HIP kernels and
+    the MFMA dA / dW kernels) for every reduce in fp32 and bf16 storage; NT_BWD=torch selects the
+    recompute-in-torch-device-ops backward (an A/B reference only)."""
 
     @staticmethod
     def forward(ctx, Xv, Xe, edge_index, rev, lay, act_mod, act, reduce, residual, nlayers, drop, *params):
         weights = list(params[:nlayers])
         biases = list(params[nlayers:])
         src = edge_index[0].contiguous()
-        kernel_bwd = ((reduce in ("sum", "mean") and Xv.dtype in (torch.float32, torch.bfloat16)
-                       or reduce in ("max", "min") and Xv.dtype == torch.float32)
+        kernel_bwd = (reduce in ("sum", "mean", "max", "min") and Xv.dtype in (torch.float32, torch.bfloat16)
                       and os.environ.get("NT_BWD", "kernel") != "torch")
         node, H, states = block_forward(Xv, Xe, src, rev, lay, weights, biases, act, reduce, residual,
                                         keep_states=kernel_bwd, drop=drop)
@@ -834,7 +834,7 @@ class ReadoutFunction(torch.autograd.Function):
             # dX[v] = dout[batch v] (/ count for mean): one gather kernel
             dX = K.gather_rows(dout.contiguous(), bni, seg_ptr=mol_ptr if reduce == "mean" else None)
             return dX, None, None, None, None, None, None
-        if reduce in ("max", "min") and dout.dtype == torch.float32:
+        if reduce in ("max", "min") and dout.dtype in (torch.float32, torch.bfloat16):
             # agg.py:45 scatter_max: dX[v] = dout[batch v] where v is the molecule's arg
             mol_perm = ctx.mol_perm
             arg = K.segment_arg(X.contiguous(), mol_ptr, mol_perm, B, reduce)

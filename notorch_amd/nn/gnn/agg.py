@@ -10,7 +10,8 @@ by a per-molecule softmax of a node score (``nt_node_scores`` then ``nt_softmax_
 uses alpha as the (V, 1) node weight agg.py:59-61 evidently means: the reference's extra
 ``.unsqueeze(1)`` turns alpha into (V, 1, 1), which broadcasts against (V, d) into a (V, V, d) tensor
 and returns (b, V, d) — O(b V d) memory and not a readout.  This is the one documented divergence.
-Training through them runs the same math in device ops under autograd (recompute backward).
+Training through them runs the kernel backward (``nt_softmax_pool_backward``): the gradients of X,
+of Gated's ``a`` and of SDPAttention's query Q.
 """
 from __future__ import annotations
 
@@ -83,10 +84,42 @@ def _softmax_pool_torch(X: Tensor, scores: Tensor, bni: Tensor, B: int) -> Tenso
     return out.scatter_add(0, idx.view(-1, 1).expand_as(X), alpha * X)
 
 
+class SoftmaxPoolFunction(torch.autograd.Function):
+    """nt_node_scores + nt_softmax_pool with the kernel backward (nt_softmax_pool_backward).
+    key: Gated's a.weight (1 x d) with bias (1,) or None; SDPAttention's Q (b x d) with bias None."""
+
+    @staticmethod
+    def forward(ctx, X, key, bias, sdpa, sqrt_key, mol_ptr, mol_perm, bni, B):
+        if sdpa:
+            scores = K.node_scores(X, Q=key.contiguous(), node_seg=bni.contiguous(), sqrt_key=sqrt_key)
+        else:
+            scores = K.node_scores(X, a=key.detach().reshape(-1).contiguous(),
+                                   a_bias=None if bias is None else bias.detach())
+        out = K.softmax_pool(X, scores, mol_ptr, mol_perm, B)
+        ctx.save_for_backward(X, key, scores, out, bni)
+        ctx.cfg = (sdpa, sqrt_key, mol_ptr, mol_perm, B, bias is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        X, key, scores, out, bni = ctx.saved_tensors
+        sdpa, sqrt_key, mol_ptr, mol_perm, B, has_bias = ctx.cfg
+        k = key.detach().contiguous() if sdpa else key.detach().reshape(-1).contiguous()
+        dX, ds, P = K.softmax_pool_backward(
+            X, scores, mol_ptr, mol_perm, bni.contiguous(), B, out, dout.contiguous().to(X.dtype),
+            a=None if sdpa else k, Q=k if sdpa else None, sqrt_key=sqrt_key)
+        if sdpa:
+            dkey, dbias = (P / sqrt_key).to(key.dtype), None
+        else:
+            dkey = P.sum(0).reshape(key.shape).to(key.dtype)
+            dbias = ds.sum().reshape(1).to(key.dtype) if has_bias else None
+        return dX, dkey, dbias, None, None, None, None, None, None
+
+
 class _AttentionReadout(Aggregation):
-    def _pool(self, G, scores_fn, torch_scores_fn, extra=()) -> Tensor:
-        """``extra``: tensors the scores depend on besides X and the module's parameters (the
-        SDPAttention query Q, passed by keyword): their requires_grad selects the autograd path too."""
+    def _pool(self, G, key, bias, sdpa, sqrt_key=1.0) -> Tensor:
+        """Scores and softmax pool on the kernels; under autograd the kernel backward
+        (SoftmaxPoolFunction) for X, the module's parameters and the SDPAttention query."""
         X = G.node_feats
         if X.device.type != "cuda":
             raise RuntimeError(
@@ -94,13 +127,23 @@ class _AttentionReadout(Aggregation):
             )
         X = X.contiguous()
         B = len(G)
-        needs_grad = torch.is_grad_enabled() and (
-            X.requires_grad or any(p.requires_grad for p in self.parameters())
-            or any(t.requires_grad for t in extra))
-        if needs_grad:
-            return _softmax_pool_torch(X, torch_scores_fn(X), G.batch_node_index, B)
         mol_ptr, mol_perm = _engine.mol_layout(G)
-        return K.softmax_pool(X, scores_fn(X), mol_ptr, mol_perm, B)
+        bni = G.batch_node_index
+        if sdpa and (key.dim() != 2 or key.shape[1] != X.shape[1]):
+            raise RuntimeError(f"Q must be b x {X.shape[1]}, got {tuple(key.shape)}")
+        needs_grad = torch.is_grad_enabled() and (
+            X.requires_grad or key.requires_grad or (bias is not None and bias.requires_grad))
+        if needs_grad:
+            return SoftmaxPoolFunction.apply(X, key, bias, sdpa, sqrt_key, mol_ptr, mol_perm, bni, B)
+        with torch.no_grad():
+            return SoftmaxPoolFunction.forward(_NoCtx(), X, key, bias, sdpa, sqrt_key, mol_ptr, mol_perm, bni, B)
+
+
+class _NoCtx:
+    """Context stand-in for the no-grad forward (nothing is saved)."""
+
+    def save_for_backward(self, *a):
+        pass
 
 
 class Gated(_AttentionReadout):
@@ -111,13 +154,7 @@ class Gated(_AttentionReadout):
         self.a = nn.Linear(input_dim, 1)
 
     def forward(self, G, **kwargs) -> Tensor:
-        w, b = self.a.weight, self.a.bias
-        return self._pool(
-            G,
-            lambda X: K.node_scores(X, a=w.detach().reshape(-1).contiguous(),
-                                    a_bias=None if b is None else b.detach()),
-            lambda X: self.a(X).squeeze(-1).float(),
-        )
+        return self._pool(G, self.a.weight, self.a.bias, sdpa=False)
 
 
 class SDPAttention(_AttentionReadout):
@@ -128,11 +165,4 @@ class SDPAttention(_AttentionReadout):
         self.sqrt_key_dim = sqrt(key_dim)
 
     def forward(self, G, *, Q: Tensor, **kwargs) -> Tensor:
-        bni = G.batch_node_index
-        return self._pool(
-            G,
-            lambda X: K.node_scores(X, Q=Q.contiguous(), node_seg=bni.contiguous(),
-                                    sqrt_key=self.sqrt_key_dim),
-            lambda X: (torch.einsum("vd,vd->v", Q[bni], X) / self.sqrt_key_dim).float(),
-            extra=(Q,),
-        )
+        return self._pool(G, Q, None, sdpa=True, sqrt_key=self.sqrt_key_dim)

@@ -28,6 +28,7 @@ def test_header_declares_the_boundary():
         "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg", "nt_absmax", "nt_dmpnn_fused_tile_rows",
         "nt_dmpnn_tile_stride", "nt_dmpnn_row_table", "nt_dmpnn_pack_weight_fk", "nt_dmpnn_tile_plan_hubs",
         "nt_dmpnn_mark_hub_rows", "nt_dmpnn_hub_aggregate", "nt_dmpnn_weight_grad_fk",
+        "nt_softmax_pool_backward",
     }
 
 
@@ -47,7 +48,7 @@ def test_abi_version_and_errors_without_gpu():
     from notorch_amd import _lib
 
     lib = _lib.load()
-    assert lib.nt_abi_version() == _lib.ABI_VERSION == 3
+    assert lib.nt_abi_version() == _lib.ABI_VERSION == 4
     assert lib.nt_dmpnn_packed_weight_bytes(300, 0) > 0
     assert lib.nt_dmpnn_packed_weight_bytes(0, 0) == 0
     # argument validation happens before any device call: EINVAL + message
@@ -69,7 +70,8 @@ def test_abi_version_and_errors_without_gpu():
     # backward entry points validate before touching the device
     rc = lib.nt_dmpnn_edge_backward(None, None, None, None, None, None, None, None, 4, 8, 16, 1, 1,
                                     0.0, 2, 0, None, None, None)
-    assert rc == 3 and b"sum | mean" in lib.nt_last_error()  # max/min backward: not a kernel
+    # max / min aggregations take nt_dmpnn_edge_backward_arg; this entry point covers sum / mean
+    assert rc == 3 and b"sum | mean" in lib.nt_last_error()
     rc = lib.nt_dmpnn_message(None, None, None, None, 4, 8, 16, 99, 0.0, 0, None, None)
     assert rc == 1
     rc = lib.nt_gather_rows(None, None, None, None, -1, 4, 8, 0, None, None, None)
@@ -93,6 +95,6 @@ def test_weight_grad_host_checks():
     assert lib.nt_dmpnn_weight_grad_workspace(77_840, 300) > 0
     assert lib.nt_dmpnn_weight_grad_workspace(-1, 300) == -1
     rc = lib.nt_dmpnn_weight_grad(None, None, None, None, None, 4, 8, 16, 1, 0.0, 1, None, 0, None, None, None)
-    assert rc == 3  # bf16: not this kernel
+    assert rc == 3  # bf16 weight grad needs src / rev (the message is formed in the kernel): NULL here
     rc = lib.nt_dmpnn_weight_grad(None, None, None, None, None, 4, 8, 16, 1, 0.0, 0, None, 0, None, None, None)
     assert rc == 1 and b"dW_out" in lib.nt_last_error()

@@ -196,9 +196,9 @@ def test_host_tile_stride_matches_library():
 
 
 def test_collate_ships_balanced_plans():
-    """The collate's plans: the 64-row plan of the shipping kernels (update_fk2 / bf16) and the 128-row
-    plan of the diagnostic update_fk_kernel, node-aligned, cut to whole rounds of 256 tiles (config 2:
-    about 5 and 3 tiles per CU)."""
+    """The collate's plans: the 64-row plan (bf16 layer kernel, and update_fk_kernel's 64-row variants)
+    and the 128-row plan of the shipping fp32 update_fk_kernel, node-aligned, cut to whole rounds of
+    256 tiles (config 2: about 5 and 3 tiles per CU)."""
     import numpy as np
 
     from notorch_amd.data.synth import make_batch

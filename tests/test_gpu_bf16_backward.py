@@ -108,7 +108,7 @@ def _truth(G, Xv, Xe, blk, act_fn, reduce):
 
 
 def _device(G, Xv, Xe, blk, reduce, mode, monkeypatch):
-    from notorch_amd.nn import Mean, Sum
+    from notorch_amd.nn import Max, Mean, Min, Sum
 
     monkeypatch.setenv("NT_BWD", mode)
     for p in blk.parameters():
@@ -116,7 +116,7 @@ def _device(G, Xv, Xe, blk, reduce, mode, monkeypatch):
     Xv_d = Xv.to(DEV).requires_grad_(True)
     Xe_d = Xe.to(DEV).requires_grad_(True)
     out = blk(G.update(node_feats=Xv_d, edge_feats=Xe_d).to(DEV))
-    ro = {"sum": Sum, "mean": Mean}[reduce]()(out)
+    ro = {"sum": Sum, "mean": Mean, "max": Max, "min": Min}[reduce]()(out)
     e = out.edge_feats.float()
     loss = ro.float().pow(2).sum() + (e * torch.linspace(-1, 1, e.shape[1], device=DEV)).sum()
     loss.backward()
@@ -130,6 +130,8 @@ def _device(G, Xv, Xe, blk, reduce, mode, monkeypatch):
     ("qm9", 64, 64, 3, "SiLU", "mean"),
     ("qm9", 32, 36, 2, "ReLU", "sum"),       # h % 8 != 0: unfused update, scalar element kernels
     ("zinc", 256, 512, 5, "ReLU", "sum"),    # config-3 shape at a smaller batch (fused bf16 update)
+    ("qm9", 64, 64, 3, "ReLU", "max"),       # max / min: the arg kernels on bf16 storage
+    ("qm9", 32, 36, 2, "SiLU", "min"),
 ])
 def test_block_grads_bf16(kind, n, h, depth, act, reduce, monkeypatch):
     from notorch_amd.nn import ChempropBlock
@@ -148,7 +150,7 @@ def test_block_grads_bf16(kind, n, h, depth, act, reduce, monkeypatch):
     real = _engine.block_backward
     monkeypatch.setattr(_engine, "block_backward", lambda *a, **k: calls.append(1) or real(*a, **k))
     got = _device(G, Xv, Xe, blk, reduce, "kernel", monkeypatch)
-    assert calls, "bf16 sum/mean backward must take the kernel path"
+    assert calls, "bf16 backward must take the kernel path (every reduce)"
     ref = _device(G, Xv, Xe, blk, reduce, "torch", monkeypatch)
     names = ["dXv", "dXe"] + [f"dW[{l}]" for l in range(depth)] + [f"db[{l}]" for l in range(depth)]
     for name, a, r, t in zip(names, got, ref, truth):

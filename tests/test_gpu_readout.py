@@ -105,3 +105,67 @@ def test_sdpa_query_gradient_with_frozen_encoder():
     assert out.grad_fn is not None
     out.pow(2).sum().backward()
     assert_parity(Qd.grad, Qr.grad, 1e-5, "dQ")
+
+
+@pytest.mark.parametrize("kind,n,h", [("qm9", 256, 300), ("polymer", 2, 64), ("qm9", 16, 13)])
+def test_attention_kernel_backward(kind, n, h, monkeypatch):
+    """Gated (dX, da, db) and SDPAttention (dX, dQ) through nt_softmax_pool_backward against fp64
+    oracle autograd (agg.py:50-86), fp32 contract; the device-op recompute is never called."""
+    from notorch_amd.nn import Gated, SDPAttention
+    from notorch_amd.nn.gnn import agg
+
+    def _no_torch(*a, **k):
+        raise AssertionError("the attention readouts must train on the kernel backward")
+
+    monkeypatch.setattr(agg, "_softmax_pool_torch", _no_torch)
+    G = _graph(kind, n, seed=7)
+    torch.manual_seed(8)
+    X = torch.randn(G.num_nodes, h, dtype=torch.float64)
+    w = torch.linspace(-1, 1, h, dtype=torch.float64)
+    # Gated
+    ro = Gated(h).double()
+    Xr = X.clone().requires_grad_(True)
+    out = dmpnn_ref.readout_gated(Xr, G.batch_node_index, len(G), ro.a.weight, ro.a.bias)
+    (out.pow(2).sum() + (out * w).sum()).backward()
+    ref = (Xr.grad, ro.a.weight.grad.clone(), ro.a.bias.grad.clone())
+    ro.zero_grad()
+    ro = ro.float().to(DEV)
+    Xd = X.float().to(DEV).requires_grad_(True)
+    o = ro(G.update(node_feats=Xd).to(DEV))
+    (o.pow(2).sum() + (o * w.float().to(DEV)).sum()).backward()
+    assert_parity(Xd.grad, ref[0], 1e-5, "Gated dX")
+    assert_parity(ro.a.weight.grad, ref[1], 1e-5, "Gated da")
+    assert_parity(ro.a.bias.grad, ref[2], 1e-5, "Gated db")
+    # SDPAttention: X and Q both trained
+    Q = torch.randn(len(G), h, dtype=torch.float64)
+    Xr, Qr = X.clone().requires_grad_(True), Q.clone().requires_grad_(True)
+    out = dmpnn_ref.readout_sdpa(Xr, G.batch_node_index, len(G), Qr, h ** 0.5)
+    (out.pow(2).sum() + (out * w).sum()).backward()
+    Xd = X.float().to(DEV).requires_grad_(True)
+    Qd = Q.float().to(DEV).requires_grad_(True)
+    o = SDPAttention(h)(G.update(node_feats=Xd).to(DEV), Q=Qd)
+    (o.pow(2).sum() + (o * w.float().to(DEV)).sum()).backward()
+    assert_parity(Xd.grad, Xr.grad, 1e-5, "SDPA dX")
+    assert_parity(Qd.grad, Qr.grad, 1e-5, "SDPA dQ")
+
+
+def test_attention_kernel_backward_bf16():
+    """bf16 storage: the kernel gradients stay within 2e-2 (normalised) of fp64 autograd on the
+    bf16-rounded inputs."""
+    from notorch_amd.nn import Gated
+
+    G = _graph("qm9", 64, seed=9)
+    h = 64
+    torch.manual_seed(10)
+    X = torch.randn(G.num_nodes, h).to(torch.bfloat16)
+    ro = Gated(h).to(torch.bfloat16)
+    ro64 = Gated(h).double()
+    ro64.load_state_dict({k: v.double() for k, v in ro.state_dict().items()})
+    Xr = X.double().requires_grad_(True)
+    dmpnn_ref.readout_gated(Xr, G.batch_node_index, len(G), ro64.a.weight, ro64.a.bias).pow(2).sum().backward()
+    ro = ro.to(DEV)
+    Xd = X.to(DEV).requires_grad_(True)
+    ro(G.update(node_feats=Xd).to(DEV)).float().pow(2).sum().backward()
+    assert Xd.grad.dtype == torch.bfloat16
+    assert_parity(Xd.grad.float(), Xr.grad, 2e-2, "Gated bf16 dX")
+    assert_parity(ro.a.weight.grad.float(), ro64.a.weight.grad, 2e-2, "Gated bf16 da")
