@@ -300,7 +300,10 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
       const int64_t hv = h / 4;
       if (hv >= 32) {  // rows of >= 32 pieces: a wave per node, every piece of the row in one pass
         const int grid = grid_for(V * 64, 256, 256 * 8);  // grid-stride: 32 waves per CU
-        if (hv <= 64) {
+#ifndef NT_INIT_PPL1
+#define NT_INIT_PPL1 0  // A/B: 1 = one 64-piece pass at a time (the round-3 kernel)
+#endif
+        if (hv <= 64 || NT_INIT_PPL1) {
           NT_DISPATCH_RA(reduce, act,
                          (init_aggregate_wave<R_, A_, 1><<<grid, 256, 0, stream>>>(
                              (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,

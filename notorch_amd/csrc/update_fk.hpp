@@ -39,13 +39,21 @@
 #include "common.hpp"
 
 // FK_MFMA_MODE (A/B builds): 0 = per-(row tile, column tile) guarded MFMAs; 1 = branch-free steps
-// (column-tile count switched once per step, every row tile computed)
+// (column-tile count switched once per step, every row tile computed); 2 = every wave computes all
+// CT column tiles and all row tiles (no branch at all)
 #ifndef FK_MFMA_MODE
 #define FK_MFMA_MODE 0
+#endif
+// FK_EPI2 (A/B builds): 1 = the sum-only aggregation scan with bound-control DPP and fma selects
+#ifndef FK_EPI2
+#define FK_EPI2 0
 #endif
 // FK_PRIO (A/B builds): 1 = s_setprio 1 for waves 4-7 for the whole loop
 #ifndef FK_PRIO
 #define FK_PRIO 0
+#endif
+#ifndef FK_RTABL
+#define FK_RTABL 0
 #endif
 
 namespace nt {
@@ -54,6 +62,21 @@ namespace fk {
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+
+// bf16 storage (PREC = 1): the two bf16 halves of a 32-bit word, widened exactly
+__device__ __forceinline__ float bf_lo(unsigned u) { return __uint_as_float(u << 16); }
+__device__ __forceinline__ float bf_hi(unsigned u) { return __uint_as_float(u & 0xffff0000u); }
+// four consecutive bf16 (8 B, the low two words of v) widened to fp32
+__device__ __forceinline__ float4 bf4_widen(uint4 v) {
+  return float4{bf_lo(v.x), bf_hi(v.x), bf_lo(v.y), bf_hi(v.y)};
+}
+// fp32 -> four bf16 (round to nearest even), packed in 8 B
+__device__ __forceinline__ uint2 bf4_pack(float a, float b, float c, float d) {
+  const bf16x4 v = bf16x4{(__bf16)a, (__bf16)b, (__bf16)c, (__bf16)d};
+  return __builtin_bit_cast(uint2, v);
+}
 
 constexpr int kThreads = 512;
 constexpr int kWaves = 8;
@@ -91,6 +114,8 @@ struct Args {
   float* SO;  // NULL: no aggregation
   int nxcd;
   int stagger;  // diagnostic: start delay of workgroup b = stagger * ((b / nxcd) % 4) x 8k cycles (0)
+  int rtabl;    // FK_RTABL builds only (timing ablations, results invalid): 1 gathers read row 0, 2 W reads
+                // block 0, 4 no H_out / S_out stores, 8 residual reads row 0, 32 no aggregation scan
 };
 
 // power-of-two scale that maps a magnitude bound to < 2^14 (exponent at most 24; every finite
@@ -144,6 +169,10 @@ __device__ __forceinline__ float dpp_shr1(float old, float x) {
                                                                __builtin_bit_cast(int, x), 0x111, 0xf,
                                                                0xf, false));
 }
+// DPP with bound control: y[lane] = x[lane - 1] within each row of 16 lanes, lane 0 of a row reads 0
+__device__ __forceinline__ float dpp_shr1_bc(float x) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, x), 0x111, 0xf, 0xf, true));
+}
 // DPP: y[lane] = x[lane + 15 mod 16] within each row (lane 0 gets lane 15)
 __device__ __forceinline__ float dpp_ror1(float x) {
   return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, x), 0x121,
@@ -192,7 +221,7 @@ __device__ __forceinline__ int4 row_entry(int4 raw, bool valid) {
 // --------------------------------------------------------------------------- kernel
 // Per-thread state of the kernel.  Plain members + force-inlined free functions taking it by
 // reference (no lambdas: closures holding pointers to these arrays kept them in scratch).
-template <int RT, int CT, int GD = 2>
+template <int RT, int CT, int GD = 2, int PREC = 0>
 struct State {
   static constexpr int ROWS = 16 * RT;
   static constexpr int PPT = RT / 4;        // 16-B pieces per thread per tensor per k-step (2 or 1)
@@ -205,15 +234,17 @@ struct State {
   int gso[GD], gqo[GD];  // their row sources
   float mxH, mxS;
   // constants of the thread / launch
-  int lane, wave, fr, g16, grt, grow, kp0, hv, NT, CTC;
+  int lane, wave, fr, g16, grt, grow, kp0, hv, hc, NT, CTC;  // hv: 16-B gather pieces per row,
+                                                           // hc: 4-column output pieces per row
   float sA, sAW, inv;
+  int rtabl;  // FK_RTABL builds: Args::rtabl
   char* abuf;
   int4* emap;
   __amdgpu_buffer_rsrc_t wrsrc;
 };
 
-template <int RT, int CT, int ACT, int P, int GD>
-__device__ __forceinline__ void fk_gather(State<RT, CT, GD>& st, const Args& a, int soff, int qoff, int s) {
+template <int RT, int CT, int ACT, int P, int GD, int PREC>
+__device__ __forceinline__ void fk_gather(State<RT, CT, GD, PREC>& st, const Args& a, int soff, int qoff, int s) {
   st.gso[P] = soff;
   st.gqo[P] = qoff;
   const int sb = soff >= 0 ? soff : 0, qb = qoff >= 0 ? qoff : 0;
@@ -221,9 +252,11 @@ __device__ __forceinline__ void fk_gather(State<RT, CT, GD>& st, const Args& a, 
   // no H (dense mode): read S's first rows instead (qoff is -1, the piece is masked at the split),
   // so the load is unconditional and the compiler's vmcnt waits stay counted
   const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H ? a.H : a.S);
+  // fp32: PPT pieces of 4 values; bf16: one piece of 8 values (128-row tiles), the same 8 k
+  constexpr int NP = PREC ? 1 : State<RT, CT, GD, PREC>::PPT;
 #pragma unroll
-  for (int u = 0; u < State<RT, CT, GD>::PPT; ++u) {
-    int p = 8 * s + st.kp0 + u;
+  for (int u = 0; u < NP; ++u) {
+    int p = PREC ? 4 * s + st.g16 : 8 * s + st.kp0 + u;
     p = p < st.hv ? p : 0;
     st.gs[P][u] = S4[sb + p];
     st.gq[P][u] = H4[qb + p];
@@ -232,10 +265,26 @@ __device__ __forceinline__ void fk_gather(State<RT, CT, GD>& st, const Args& a, 
 
 // A = S[src] - act(H[rev]) of the staged piece, scaled by s_A, split into two fp16 parts written in
 // MFMA B-fragment order (row tile grt, lane (k-group, row): 16 B per part) into LDS buffer P
-template <int RT, int CT, int ACT, int P, int BUF, int GD>
-__device__ __forceinline__ void fk_split(State<RT, CT, GD>& st, const Args& a, int s) {
-  using St = State<RT, CT, GD>;
+template <int RT, int CT, int ACT, int P, int BUF, int GD, int PREC>
+__device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC>& st, const Args& a, int s) {
+  using St = State<RT, CT, GD, PREC>;
   const bool sok = st.gso[P] >= 0, qok = st.gqo[P] >= 0;
+  if constexpr (PREC == 1) {
+    // bf16 storage: A in fp32 from the widened pieces, one rounding to bf16, one fragment part
+    static_assert(RT == 8, "bf16 fk tiles are 128 rows");
+    const bool in = 4 * s + st.g16 < st.hv;
+    const uint4 su = __builtin_bit_cast(uint4, st.gs[P][0]), qu = __builtin_bit_cast(uint4, st.gq[P][0]);
+    const unsigned sw[4] = {su.x, su.y, su.z, su.w}, qw[4] = {qu.x, qu.y, qu.z, qu.w};
+    bf16x8 h0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float q0 = act_t<ACT>(bf_lo(qw[c]), a.act, a.alpha), q1 = act_t<ACT>(bf_hi(qw[c]), a.act, a.alpha);
+      h0[2 * c] = (__bf16)((sok && in ? bf_lo(sw[c]) : 0.f) - (qok && in ? q0 : 0.f));
+      h0[2 * c + 1] = (__bf16)((sok && in ? bf_hi(sw[c]) : 0.f) - (qok && in ? q1 : 0.f));
+    }
+    *reinterpret_cast<bf16x8*>(st.abuf + BUF * St::kBufB + st.grt * 1024 + st.lane * 16) = h0;
+    return;
+  }
   float x[4 * St::PPT];
 #pragma unroll
   for (int u = 0; u < St::PPT; ++u) {
@@ -274,47 +323,61 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD>& st, const Args& a, i
   }
 }
 
-template <int RT, int CT, int P, int GD>
-__device__ __forceinline__ void fk_load_w(State<RT, CT, GD>& st, int c, int s) {
+template <int RT, int CT, int P, int GD, int PREC>
+__device__ __forceinline__ void fk_load_w(State<RT, CT, GD, PREC>& st, int c, int s) {
 #pragma unroll
   for (int j = 0; j < CT; ++j) {
     // unconditional (no branch around vector-memory ops keeps the compiler's vmcnt waits counted):
     // a column tile past NT reads beyond the buffer's range, which returns zeros
     const int ct = c * st.CTC + st.wave + 8 * j;
-    const int soff = __builtin_amdgcn_readfirstlane(ct < st.NT ? kImgHdr + ((s * st.NT + ct) * 2) * 1024
-                                                               : 0x7fff0000);
+    // fp32: two parts per block behind the scale header; bf16: the plain bf16 image (one part)
+    const int blk = PREC ? (s * st.NT + ct) * 1024 : kImgHdr + ((s * st.NT + ct) * 2) * 1024;
+    int soff = __builtin_amdgcn_readfirstlane(ct < st.NT ? blk : 0x7fff0000);
+#if FK_RTABL
+    if (st.rtabl & 2) soff = ct < st.NT ? (PREC ? 0 : kImgHdr) : 0x7fff0000;
+#endif
     st.wb[P][j][0] = __builtin_bit_cast(
         uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff, 0));
-    st.wb[P][j][1] = __builtin_bit_cast(
-        uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff + 1024, 0));
+    if constexpr (PREC == 0)
+      st.wb[P][j][1] = __builtin_bit_cast(
+          uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff + 1024, 0));
   }
 }
 
-template <int RT, int CT, int P, int GD>
-__device__ __forceinline__ void fk_mfma(State<RT, CT, GD>& st, int c, int nrt) {
-  using St = State<RT, CT, GD>;
+// one (row tile, column tile) k-step: fp32 = the three split products, bf16 = one bf16 MFMA
+template <int PREC>
+__device__ __forceinline__ f32x4 fk_mac(uint4 w0r, uint4 w1r, f16x8 a0, f16x8 a1, f32x4 t) {
+  if constexpr (PREC == 1) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, w0r), __builtin_bit_cast(bf16x8, a0),
+                                                   t, 0, 0, 0);
+  } else {
+    const f16x8 w0 = as_f16x8(w0r), w1 = as_f16x8(w1r);
+    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, a0, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a1, t, 0, 0, 0);
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a0, t, 0, 0, 0);
+  }
+}
+
+template <int RT, int CT, int P, int GD, int PREC>
+__device__ __forceinline__ void fk_mfma(State<RT, CT, GD, PREC>& st, int c, int nrt) {
+  using St = State<RT, CT, GD, PREC>;
   const char* bb = st.abuf + P * St::kBufB + st.lane * 16;
   // A fragments one row tile ahead; the schedule barriers keep the compiler from hoisting every row
   // tile's fragments (64 VGPRs) above the MFMAs
   f16x8 a0 = *reinterpret_cast<const f16x8*>(bb);
-  f16x8 a1 = *reinterpret_cast<const f16x8*>(bb + St::kPartB);
+  f16x8 a1 = PREC ? a0 : *reinterpret_cast<const f16x8*>(bb + St::kPartB);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     if (rt < nrt) {
       f16x8 n0 = a0, n1 = a1;
       if (rt + 1 < RT) {
         n0 = *reinterpret_cast<const f16x8*>(bb + (rt + 1) * 1024);
-        n1 = *reinterpret_cast<const f16x8*>(bb + St::kPartB + (rt + 1) * 1024);
+        n1 = PREC ? n0 : *reinterpret_cast<const f16x8*>(bb + St::kPartB + (rt + 1) * 1024);
       }
 #pragma unroll
       for (int j = 0; j < CT; ++j) {
         if (c * st.CTC + st.wave + 8 * j < st.NT) {
-          const f16x8 w0 = as_f16x8(st.wb[P][j][0]), w1 = as_f16x8(st.wb[P][j][1]);
-          f32x4 t = st.acc[rt][j];
-          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, a0, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a1, t, 0, 0, 0);
-          t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a0, t, 0, 0, 0);
-          st.acc[rt][j] = t;
+          st.acc[rt][j] = fk_mac<PREC>(st.wb[P][j][0], st.wb[P][j][1], a0, a1, st.acc[rt][j]);
         }
       }
       a0 = n0;
@@ -328,27 +391,22 @@ __device__ __forceinline__ void fk_mfma(State<RT, CT, GD>& st, int c, int nrt) {
 // of the tile computed (rows past the tile hold zeros in the A buffer, so their accumulators keep
 // whatever they held and are never stored).  One scalar branch per step (the NCT switch) instead of
 // one per (row tile, column tile).
-template <int RT, int CT, int P, int GD, int NCT>
-__device__ __forceinline__ void fk_mfma_nb(State<RT, CT, GD>& st) {
-  using St = State<RT, CT, GD>;
+template <int RT, int CT, int P, int GD, int NCT, int PREC>
+__device__ __forceinline__ void fk_mfma_nb(State<RT, CT, GD, PREC>& st) {
+  using St = State<RT, CT, GD, PREC>;
   const char* bb = st.abuf + P * St::kBufB + st.lane * 16;
   f16x8 a0 = *reinterpret_cast<const f16x8*>(bb);
-  f16x8 a1 = *reinterpret_cast<const f16x8*>(bb + St::kPartB);
+  f16x8 a1 = PREC ? a0 : *reinterpret_cast<const f16x8*>(bb + St::kPartB);
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
     f16x8 n0 = a0, n1 = a1;
     if (rt + 1 < RT) {
       n0 = *reinterpret_cast<const f16x8*>(bb + (rt + 1) * 1024);
-      n1 = *reinterpret_cast<const f16x8*>(bb + St::kPartB + (rt + 1) * 1024);
+      n1 = PREC ? n0 : *reinterpret_cast<const f16x8*>(bb + St::kPartB + (rt + 1) * 1024);
     }
 #pragma unroll
     for (int j = 0; j < NCT; ++j) {
-      const f16x8 w0 = as_f16x8(st.wb[P][j][0]), w1 = as_f16x8(st.wb[P][j][1]);
-      f32x4 t = st.acc[rt][j];
-      t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, a0, t, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a1, t, 0, 0, 0);
-      t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a0, t, 0, 0, 0);
-      st.acc[rt][j] = t;
+      st.acc[rt][j] = fk_mac<PREC>(st.wb[P][j][0], st.wb[P][j][1], a0, a1, st.acc[rt][j]);
     }
     a0 = n0;
     a1 = n1;
@@ -356,9 +414,15 @@ __device__ __forceinline__ void fk_mfma_nb(State<RT, CT, GD>& st) {
   }
 }
 
-template <int RT, int CT, int P, int GD>
-__device__ __forceinline__ void fk_mfma_sw(State<RT, CT, GD>& st, int c, int nrt) {
-#if FK_MFMA_MODE == 1
+template <int RT, int CT, int P, int GD, int PREC>
+__device__ __forceinline__ void fk_mfma_sw(State<RT, CT, GD, PREC>& st, int c, int nrt) {
+#if FK_MFMA_MODE == 2
+  // every wave runs all CT column tiles (past NT the W fragments read zeros): one straight-line
+  // MFMA block per step, no per-wave branch
+  (void)c;
+  (void)nrt;
+  fk_mfma_nb<RT, CT, P, GD, CT>(st);
+#elif FK_MFMA_MODE == 1
   // active column tiles of this wave in chunk c (wave-uniform)
   const int first = c * st.CTC + st.wave;
   const int nct = first >= st.NT ? 0 : min(CT, (st.NT - first + 7) / 8);
@@ -380,31 +444,53 @@ __device__ __forceinline__ void fk_mfma_sw(State<RT, CT, GD>& st, int c, int nrt
 // issued by the epilogue of the previous (tile, chunk) as soon as it has stored column tile j, so
 // they land during the rest of that epilogue; fk_resid_scale multiplies them by s_A s_W before the
 // first MFMA of the K loop (48 packed multiplies per tile, no staging registers).
-template <int RT, int CT, int GD>
-__device__ __forceinline__ void fk_resid_load(State<RT, CT, GD>& st, const Args& a, int i, int c, int j) {
-  using St = State<RT, CT, GD>;
-  const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H);
+template <int RT, int CT, int GD, int PREC>
+__device__ __forceinline__ void fk_resid_load(State<RT, CT, GD, PREC>& st, const Args& a, int i, int c, int j) {
+  using St = State<RT, CT, GD, PREC>;
   int pc = 4 * (c * st.CTC + st.wave + 8 * j) + st.g16;
-  pc = pc < st.hv ? pc : 0;
+  pc = pc < st.hc ? pc : 0;
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
-    const int e = st.emap[(i % kEmaps) * St::ROWS + 16 * rt + st.fr].x;
-    st.acc[rt][j] = H4[(int64_t)(e >= 0 ? e : 0) * st.hv + pc];
+    int e = st.emap[(i % kEmaps) * St::ROWS + 16 * rt + st.fr].x;
+#if FK_RTABL
+    if (st.rtabl & 8) e = 0;
+#endif
+    const int64_t r = (int64_t)(e >= 0 ? e : 0) * st.hc + pc;
+    if constexpr (PREC == 1) {  // 4 bf16 (8 B), widened by fk_resid_scale once they have landed
+      const uint2 v = reinterpret_cast<const uint2*>(a.H)[r];
+      st.acc[rt][j] = __builtin_bit_cast(f32x4, uint4{v.x, v.y, 0u, 0u});
+    } else {
+      st.acc[rt][j] = reinterpret_cast<const f32x4*>(a.H)[r];
+    }
   }
 }
 
 // Bias of chunk c, column tile j: an unconditional load (no bias: S's first row, zeroed at use),
 // issued a whole chunk before the epilogue that uses it.
-template <int RT, int CT, int GD>
-__device__ __forceinline__ void fk_bias_load(State<RT, CT, GD>& st, const Args& a, int c, int j) {
-  const f32x4* b4 = reinterpret_cast<const f32x4*>(a.bias ? a.bias : a.S);
+template <int RT, int CT, int GD, int PREC>
+__device__ __forceinline__ void fk_bias_load(State<RT, CT, GD, PREC>& st, const Args& a, int c, int j) {
   int pc = 4 * (c * st.CTC + st.wave + 8 * j) + st.g16;
-  pc = (pc < st.hv && a.bias) ? pc : 0;
-  st.bias[j] = b4[pc];
+  pc = (pc < st.hc && a.bias) ? pc : 0;
+  if constexpr (PREC == 1) {  // raw 8 B, widened at use
+    const uint2 v = reinterpret_cast<const uint2*>(a.bias ? a.bias : a.S)[pc];
+    st.bias[j] = __builtin_bit_cast(f32x4, uint4{v.x, v.y, 0u, 0u});
+  } else {
+    st.bias[j] = reinterpret_cast<const f32x4*>(a.bias ? a.bias : a.S)[pc];
+  }
 }
 
-template <int RT, int CT, int GD>
-__device__ __forceinline__ void fk_resid_scale(State<RT, CT, GD>& st) {
+template <int RT, int CT, int GD, int PREC>
+__device__ __forceinline__ void fk_resid_scale(State<RT, CT, GD, PREC>& st) {
+  if constexpr (PREC == 1) {  // bf16: widen the raw residual pieces (no scale)
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+      for (int j = 0; j < CT; ++j) {
+        const float4 w = bf4_widen(__builtin_bit_cast(uint4, st.acc[rt][j]));
+        st.acc[rt][j] = f32x4{w.x, w.y, w.z, w.w};
+      }
+    return;
+  }
   const f32x4 s4 = f32x4{st.sAW, st.sAW, st.sAW, st.sAW};
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt)
@@ -426,21 +512,41 @@ struct EpiCtx {
   int n;
 };
 
-template <int RTI, int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL>
-__device__ __forceinline__ void fk_epi_row(State<RT, CT, GD>& st, const Args& a, const EpiCtx& x0, int pc,
+template <int RTI, int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL, int PREC>
+__device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC>& st, const Args& a, const EpiCtx& x0, int pc,
                                            bool pok, const f32x4& bj, f32x4& carry, float& ccnt) {
   if (16 * RTI < x0.n) {
-    const int hv = st.hv;
+    const int hc = st.hc;
     const int4 ri = x0.em[16 * RTI + st.fr];
     f32x4 o;
+    uint2 ob = uint2{0u, 0u};  // bf16: the stored (rounded) H_out piece
+    if constexpr (PREC == 1) {
+      // bf16: acc + bias in fp32, one rounding; the aggregation below reads the stored value
+      ob = bf4_pack(st.acc[RTI][J][0] + bj[0], st.acc[RTI][J][1] + bj[1], st.acc[RTI][J][2] + bj[2],
+                    st.acc[RTI][J][3] + bj[3]);
+      const float4 w = bf4_widen(uint4{ob.x, ob.y, 0u, 0u});
+      o = f32x4{w.x, w.y, w.z, w.w};
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[RTI][J][q], st.inv, bj[q]);
-    const bool rok = ri.x >= 0 && pok;
-    if (rok && (ABL & 64) == 0) {
-      x0.O4[(int64_t)ri.x * hv + pc] = o;
-      st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+      for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[RTI][J][q], st.inv, bj[q]);
     }
+    bool rok = ri.x >= 0 && pok;
+#if FK_RTABL
+    if (st.rtabl & 4) rok = false;
+#endif
+    if (rok && (ABL & 64) == 0) {
+      if constexpr (PREC == 1) {
+        reinterpret_cast<uint2*>(x0.O4)[(int64_t)ri.x * hc + pc] = ob;
+      } else {
+        x0.O4[(int64_t)ri.x * hc + pc] = o;
+        st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+      }
+    }
+#if FK_RTABL
+    if (x0.SO4 != nullptr && !(st.rtabl & 32)) {
+#else
     if (x0.SO4 != nullptr) {
+#endif
       // MAXL rounds of x[r] = start[r] ? m[r] : x[r - 1] + m[r] (the carry enters at row 0): a
       // row's value is final once the rounds cover its distance from its node's first row, at
       // most max in-degree - 1 (<= 16 within a row tile); extra rounds leave converged rows as they
@@ -454,6 +560,25 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD>& st, const Args& a,
       for (int q = 0; q < 4; ++q) cin[q] = dpp_ror1(carry[q]);
       float cnt = 1.f;
       const float cinc = SUMONLY ? 0.f : dpp_ror1(ccnt);
+#if FK_EPI2
+      if constexpr (SUMONLY) {
+        // the same left-to-right sums with fewer instructions: the carry enters lane 0's own term
+        // once (m0 = cin + m at a continuing lane 0), then every round is one bound-control DPP
+        // shift (lane 0 reads 0: no copy of an `old` operand) and one fma with keep = !start
+        // (fma(y, 1, m) = y + m and fma(y, 0, m) = m for finite y: the sums are bit-identical)
+        const float keep = start ? 0.f : 1.f;
+        const bool lane0 = st.fr == 0;
+        f32x4 mp;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) mp[q] = lane0 ? fmaf(cin[q], keep, m[q]) : m[q];
+        x = mp;
+#pragma unroll
+        for (int it = 0; it < MAXL; ++it) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[q] = fmaf(dpp_shr1_bc(x[q]), keep, mp[q]);
+        }
+      } else
+#endif
 #pragma unroll
       for (int it = 0; it < MAXL; ++it) {
         f32x4 y;
@@ -476,8 +601,12 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD>& st, const Args& a,
       if ((ri.z & kFlagEnd) && rok && (ABL & 128) == 0) {
         f32x4 r = x;
         if (!SUMONLY && a.reduce == NT_MEAN) r = x / cnt;
-        x0.SO4[(int64_t)ri.y * hv + pc] = r;
-        st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(r[0]), fabsf(r[1])), fmaxf(fabsf(r[2]), fabsf(r[3]))));
+        if constexpr (PREC == 1) {
+          reinterpret_cast<uint2*>(x0.SO4)[(int64_t)ri.y * hc + pc] = bf4_pack(r[0], r[1], r[2], r[3]);
+        } else {
+          x0.SO4[(int64_t)ri.y * hc + pc] = r;
+          st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(r[0]), fabsf(r[1])), fmaxf(fabsf(r[2]), fabsf(r[3]))));
+        }
       }
       carry = x;
       ccnt = cnt;
@@ -487,14 +616,18 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD>& st, const Args& a,
     fk_epi_row<RTI + 1, J, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, pc, pok, bj, carry, ccnt);
 }
 
-template <int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL>
-__device__ __forceinline__ void fk_epi_col(State<RT, CT, GD>& st, const Args& a, const EpiCtx& x0, int i, int c,
+template <int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL, int PREC>
+__device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC>& st, const Args& a, const EpiCtx& x0, int i, int c,
                                            bool load_next, int i_next, int c_next) {
   const int ct = c * st.CTC + st.wave + 8 * J;
   if (ct < st.NT) {
     const int pc = 4 * ct + st.g16;
-    const bool pok = pc < st.hv;
-    const f32x4 bj = (x0.b4 && pok) ? st.bias[J] : f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool pok = pc < st.hc;
+    f32x4 bj = (x0.b4 && pok) ? st.bias[J] : f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (PREC == 1) {  // the raw bf16 bias piece (zero bits stay zero)
+      const float4 w = bf4_widen(__builtin_bit_cast(uint4, bj));
+      bj = f32x4{w.x, w.y, w.z, w.w};
+    }
     f32x4 carry = f32x4{0.f, 0.f, 0.f, 0.f};
     float ccnt = 0.f;
     fk_epi_row<0, J, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, pc, pok, bj, carry, ccnt);
@@ -512,14 +645,14 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD>& st, const Args& a,
     fk_epi_col<J + 1, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, i, c, load_next, i_next, c_next);
 }
 
-template <int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL>
-__device__ __forceinline__ void fk_epilogue(State<RT, CT, GD>& st, const Args& a, int i, int c, int n,
+template <int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL, int PREC>
+__device__ __forceinline__ void fk_epilogue(State<RT, CT, GD, PREC>& st, const Args& a, int i, int c, int n,
                                             bool load_next, int i_next, int c_next) {
   EpiCtx x0;
   x0.b4 = reinterpret_cast<const f32x4*>(a.bias);
   x0.O4 = reinterpret_cast<f32x4*>(a.O);
   x0.SO4 = reinterpret_cast<f32x4*>(a.SO);
-  x0.em = st.emap + (i % kEmaps) * State<RT, CT, GD>::ROWS;
+  x0.em = st.emap + (i % kEmaps) * State<RT, CT, GD, PREC>::ROWS;
   x0.n = n;
   fk_epi_col<0, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, i, c, load_next, i_next, c_next);
 }
@@ -534,11 +667,11 @@ __device__ __forceinline__ void fk_barrier() {
 // 64 no H_out stores, 128 no S_out stores; 256 (results valid): per-phase s_memtime cycle sums into
 // g_pk_stamps (0 residual scale + MFMAs, 1 W issue, 2 split + gather issue, 3 barrier, 4 epilogue,
 // 6 whole loop, 7 waves).
-template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL, int GD = 2, int ABL = 0>
+template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL, int GD = 2, int ABL = 0, int PREC = 0>
 __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   // fused variants (MAXL > 1) read their rows from the row table, plain ones from src / rev
   constexpr bool TABLE = MAXL > 1;
-  using St = State<RT, CT, GD>;
+  using St = State<RT, CT, GD, PREC>;
   constexpr int ROWS = St::ROWS;
   constexpr int kEmapB = kEmaps * ROWS * 16;
   __shared__ __attribute__((aligned(16))) uint4 smem[(2 * St::kBufB + kEmapB) / 16];
@@ -568,21 +701,28 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   st.grt = RT == 8 ? st.wave : (st.wave & 3);
   st.grow = 16 * st.grt + st.fr;
   st.kp0 = RT == 8 ? 2 * st.g16 : 2 * st.g16 + (st.wave >> 2);
-  st.hv = a.hv;
+  st.hv = a.hv;       // fp32: h / 4 (16-B pieces of 4 floats); bf16: h / 8 (of 8 bf16)
+  st.hc = a.h / 4;    // 4-column output pieces per row
+  st.rtabl = a.rtabl;
   st.NT = a.NT;
   st.CTC = 8 * CT;
   st.abuf = reinterpret_cast<char*>(smem);
   st.emap = reinterpret_cast<int4*>(st.abuf + 2 * St::kBufB);
-  st.wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.Wimg, (short)0, (int)image_bytes(a.h), 0x00020000);
+  st.wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.Wimg, (short)0, PREC ? ks_for(a.h) * nt_for(a.h) * 1024 : (int)image_bytes(a.h), 0x00020000);
   st.mxH = 0.f;
   st.mxS = 0.f;
   // scales: s_A from the bound of |A| = |S[src] - act(H[rev])|, s_W from the image header
-  const float bound = a.src ? a.amax_in[1] + (a.rev ? act_bound(a.amax_in[0], a.act, a.alpha) : 0.f)
-                            : a.amax_in[1];
-  st.sA = ldexpf(1.f, scale_exp(bound));
-  const float sW = *reinterpret_cast<const float*>(a.Wimg);
-  st.sAW = st.sA * sW;
-  st.inv = 1.f / st.sAW;  // exact: a power of two
+  if constexpr (PREC == 1) {  // bf16: no split, no scales
+    st.sA = st.sAW = st.inv = 1.f;
+  } else {
+    const float bound = a.src ? a.amax_in[1] + (a.rev ? act_bound(a.amax_in[0], a.act, a.alpha) : 0.f)
+                              : a.amax_in[1];
+    st.sA = ldexpf(1.f, scale_exp(bound));
+    const float sW = *reinterpret_cast<const float*>(a.Wimg);
+    st.sAW = st.sA * sW;
+    st.inv = 1.f / st.sAW;  // exact: a power of two
+  }
   const bool resid = (ABL & 32) == 0 && a.residual && a.H != nullptr;
   const bool info_writer = st.g16 == 0 && (RT == 8 || st.wave < 4);
   const int SPT = a.nchunks * a.KS;  // steps per tile
@@ -703,6 +843,9 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
           const int s3 = (k3 - adv * SPT) % a.KS;
           int so = adv == 0 ? cur.x : nxt.x, qo = adv == 0 ? cur.y : nxt.y;
           if constexpr ((ABL & 1) != 0) so = qo = 0;
+#if FK_RTABL
+          if (st.rtabl & 1) so = qo = 0;
+#endif
           if (P == 0) fk_gather<RT, CT, ACT, 1>(st, a, so, qo, s3);
           else fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s3);
         }

@@ -922,6 +922,8 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   {
     const char* e = getenv("NT_FK_STAGGER");  // timing experiments only
     a.stagger = e ? atoi(e) : 0;
+    const char* r = getenv("NT_FK_RTABL");  // FK_RTABL builds only (timing ablations)
+    a.rtabl = r ? atoi(r) : 0;
   }
   a.ntiles = fused ? (int)ntiles : (int)((u.E + cap - 1) / cap);
   if (a.ntiles == 0) return NT_OK;

@@ -135,7 +135,9 @@ def test_attention_kernel_backward(kind, n, h, monkeypatch):
     (o.pow(2).sum() + (o * w.float().to(DEV)).sum()).backward()
     assert_parity(Xd.grad, ref[0], 1e-5, "Gated dX")
     assert_parity(ro.a.weight.grad, ref[1], 1e-5, "Gated da")
-    assert_parity(ro.a.bias.grad, ref[2], 1e-5, "Gated db")
+    # db = sum_v ds_v is mathematically 0 per molecule (softmax gradients sum to zero): an
+    # ill-conditioned difference, held to the fp32 contract relative to the scale of da
+    assert (ro.a.bias.grad.double().cpu() - ref[2]).abs().max().item() <= 1e-5 * ref[1].abs().max().item(), "Gated db"
     # SDPAttention: X and Q both trained
     Q = torch.randn(len(G), h, dtype=torch.float64)
     Xr, Qr = X.clone().requires_grad_(True), Q.clone().requires_grad_(True)
