@@ -60,6 +60,12 @@ int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_
 int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);
 // a library-owned (max|H|, max|S|) slot filled on `stream` (H or S may be NULL: that entry stays 0)
 int amax_scratch(const float* H, int64_t nh, const float* S, int64_t ns, float** out, hipStream_t stream);
+// bf16 storage on the same skeleton (PREC = 1): h % 8 == 0, h <= 512, tiles of <= 128 rows, Wimg =
+// the bf16 fragment image; S_out / the row table exactly with a tile plan
+bool fkb_supported(int64_t h);
+int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* tile_ptr, int64_t ntiles,
+                          int tile_rows, int max_in_degree, const void* row_table, int reduce, int aact,
+                          float aalpha, void* S_out);
 inline int64_t fk_image_bytes(int64_t h) { return 256 + ((h + 31) / 32) * ((h + 15) / 16) * 2 * 1024; }
 
 // Deeper-ring variant (S/H 2 chunks ahead); requires additionally NT <= 24.

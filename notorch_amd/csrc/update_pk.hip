@@ -948,6 +948,83 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   return launch_fk_narrow<4>(a, maxl, grid, u.stream);
 }
 
+// ------------------------------------------------------------------------------ bf16 on the fk skeleton
+// bf16 storage (PREC = 1): the same persistent kernel with 128-row tiles and 4 column tiles per wave
+// (h <= 512), one bf16 MFMA per (row tile, column tile) and k-step, no split and no scales; W is the
+// plain bf16 fragment image (nt_dmpnn_pack_weight, bf16).
+namespace {
+template <int ACT, int AACT, bool SUMONLY, int MAXL>
+int launch_fkb_t(const fk::Args& a, int grid, hipStream_t stream) {
+  fk::update_fk_kernel<8, 4, ACT, AACT, SUMONLY, MAXL, 2, 0, 1><<<grid, fk::kThreads, 0, stream>>>(a);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+}  // namespace
+
+bool fkb_supported(int64_t h) { return h % 8 == 0 && h >= 8 && h <= 512; }
+
+int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* tile_ptr, int64_t ntiles,
+                          int tile_rows, int max_in_degree, const void* row_table, int reduce, int aact,
+                          float aalpha, void* S_out) {
+  const bool fused = tile_ptr != nullptr;
+  NT_REQUIRE(fkb_supported(u.h), NT_EUNSUPPORTED, "bf16 layer kernel needs h % 8 == 0 and h <= 512");
+  NT_REQUIRE(fused == (S_out != nullptr), NT_EINVAL, "S_out must be given exactly with a tile plan");
+  NT_REQUIRE(!fused || row_table, NT_EINVAL, "bf16 fused mode needs the row table (nt_dmpnn_row_table)");
+  NT_REQUIRE(!fused || (tile_rows >= 1 && tile_rows <= 128), NT_EUNSUPPORTED, "bf16 tiles hold at most 128 rows");
+  NT_REQUIRE(!fused || (max_in_degree >= 0 && max_in_degree <= 32), NT_EUNSUPPORTED,
+             "fused aggregation needs max_in_degree <= 32");
+  NT_REQUIRE((u.E * u.h) / 4 < (int64_t(1) << 31) && (u.V * u.h) / 4 < (int64_t(1) << 31), NT_EUNSUPPORTED,
+             "bf16 update: E*h and V*h must stay below 2^33");
+  fk::Args a;
+  a.H = u.H;
+  a.S = u.S;
+  a.src = u.src;
+  a.rev = u.rev;
+  a.Wimg = (const char*)Wimg;
+  a.bias = u.b;
+  a.amax_in = nullptr;
+  a.amax_out = nullptr;
+  a.V = u.V;
+  a.E = u.E;
+  a.h = (int)u.h;
+  a.hv = (int)(u.h / 8);  // 16-B gather pieces of 8 bf16
+  a.KS = fk::ks_for(u.h) < 4 ? 4 : (fk::ks_for(u.h) + 1) / 2 * 2;
+  a.NT = fk::nt_for(u.h);
+  a.nchunks = 1;
+  a.residual = u.residual;
+  a.act = u.act;
+  a.alpha = u.alpha;
+  a.tile_ptr = tile_ptr;
+  a.rows = fused ? (const int4*)row_table : nullptr;
+  a.reduce = reduce;
+  a.aact = aact;
+  a.aalpha = aalpha;
+  a.O = u.H_out;
+  a.SO = (float*)S_out;
+  a.nxcd = xcd_count();
+  a.stagger = 0;
+  a.rtabl = 0;
+  a.ntiles = fused ? (int)ntiles : (int)((u.E + 127) / 128);
+  if (a.ntiles == 0) return NT_OK;
+  const int grid = a.ntiles < cu_count() ? a.ntiles : cu_count();
+  const bool relu = u.act == NT_ACT_RELU;
+  if (!fused) {
+    if (relu) return launch_fkb_t<NT_ACT_RELU, NT_ACT_IDENTITY, true, 1>(a, grid, u.stream);
+    if (u.act == NT_ACT_IDENTITY) return launch_fkb_t<NT_ACT_IDENTITY, NT_ACT_IDENTITY, true, 1>(a, grid, u.stream);
+    return launch_fkb_t<-1, NT_ACT_IDENTITY, true, 1>(a, grid, u.stream);
+  }
+  const int maxl = max_in_degree - 1;
+  if (relu && reduce == NT_SUM && aact == NT_ACT_RELU)
+    return maxl <= 3   ? launch_fkb_t<NT_ACT_RELU, NT_ACT_RELU, true, 3>(a, grid, u.stream)
+           : maxl <= 8 ? launch_fkb_t<NT_ACT_RELU, NT_ACT_RELU, true, 8>(a, grid, u.stream)
+                       : launch_fkb_t<NT_ACT_RELU, NT_ACT_RELU, true, 16>(a, grid, u.stream);
+  if (relu && reduce == NT_SUM && aact == NT_ACT_IDENTITY)
+    return maxl <= 3   ? launch_fkb_t<NT_ACT_RELU, NT_ACT_IDENTITY, true, 3>(a, grid, u.stream)
+           : maxl <= 8 ? launch_fkb_t<NT_ACT_RELU, NT_ACT_IDENTITY, true, 8>(a, grid, u.stream)
+                       : launch_fkb_t<NT_ACT_RELU, NT_ACT_IDENTITY, true, 16>(a, grid, u.stream);
+  return launch_fkb_t<-1, -1, false, 16>(a, grid, u.stream);
+}
+
 int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_t img_stride, void* img,
             hipStream_t stream) {
   const int KS = fk::ks_for(h), NT = fk::nt_for(h);

@@ -490,7 +490,7 @@ def dmpnn_update_fused(
 
     fp32: ``amax_in`` = (max|H|, max|S|) on the device (computed here with nt_absmax when not given);
     ``amax_out`` (2 zero-filled floats) receives max|H_out|, max|S_out| for the next layer.
-    ``row_table`` (fp32 with a plan): nt_dmpnn_row_table of (perm, dst_sorted, src, rev), built here
+    ``row_table`` (with a plan): nt_dmpnn_row_table of (perm, dst_sorted, src, rev), built here
     when not given (cache it per graph).
     ``zero_fill`` must be True when some node has no in-edge (its S_out row is then 0)."""
     dev = _require_device(H, S, src, rev, Wp, bias, out, S_out, perm, amax_in, amax_out)
@@ -525,7 +525,7 @@ def dmpnn_update_fused(
     else:
         perm = None
         S_out = None
-    if H.dtype == torch.float32 and plan is not None and row_table is None and E > 0:
+    if plan is not None and row_table is None and E > 0:
         row_table = dmpnn_row_table(perm, dsts, src, rev, V)
     if H.dtype == torch.float32 and amax_in is None and E > 0:
         amax_in = torch.zeros(2, dtype=torch.float32, device=dev)

@@ -379,7 +379,7 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
         K.absmax(S, amax[0, 1:2])
     fusable = drop is None and _fused_enabled() and K.fused_supported(V, E, h, H.dtype)
     rows = 64
-    if fusable and fp32:  # the fp32 kernel's tile capacity for every layer of this block
+    if fusable:  # the layer kernel's tile capacity for every layer of this block
         rows = min(K.fused_tile_rows(h, H.dtype, act, reduce, act),
                    K.fused_tile_rows(h, H.dtype, act, reduce, _IDENTITY))
     plan = fused_plan(lay, V, E, rows, H.dtype) if fusable else None
@@ -442,7 +442,7 @@ def row_table(lay: DeviceLayout, dsts: Tensor, src: Tensor, rev: Tensor, V: int)
 def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, residual, keep_states, amax):
     tile_ptr, ntiles, dsts, zero_fill = plan
     d = len(Wps)
-    rt = row_table(lay, dsts, src, rev, S.shape[0]) if H.dtype == torch.float32 else None
+    rt = row_table(lay, dsts, src, rev, S.shape[0])
     states = []
     spare_H: Optional[Tensor] = None
     spare_S: Optional[Tensor] = None
