@@ -549,6 +549,12 @@ static size_t as_part_bytes(int64_t) { return 0; }
 
 static size_t fk_offset(int64_t h) { return f32_image_bytes(h) + x6_part_bytes(h) + as_part_bytes(h); }
 
+// bf16 layer kernel: the fk skeleton (NT_BF16_KERNEL=fk) or the 64-row bf16 kernel (default), read per call
+static bool bf16_fk(int64_t h) {
+  const char* e = getenv("NT_BF16_KERNEL");
+  return e && e[0] == 'f' && nt::fkb_supported(h);
+}
+
 extern "C" size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype) {
   if (h <= 0) return 0;
   if (dtype == NT_BF16) return (nt::bf16_image_bytes(h) + 255) & ~size_t(255);
@@ -611,7 +617,7 @@ extern "C" int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h
 
 extern "C" int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, int agg_act) {
   if (h <= 0) return 0;
-  if (dtype == NT_BF16) return nt::fkb_supported(h) ? 128 : 64;
+  if (dtype == NT_BF16) return bf16_fk(h) ? 128 : 64;
   return nt::fk_tile_rows(h, act, reduce, agg_act, true);
 }
 
@@ -650,7 +656,7 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
   NT_REQUIRE(H != H_out, NT_EINVAL, "H_out must not alias H");
   NT_REQUIRE(aligned16(Wp), NT_EINVAL, "Wp must be 16-byte aligned");
   if (dtype == NT_BF16) {
-    if (fkb_supported(h) && aligned16(H) && aligned16(S) && aligned16(H_out) && (b == nullptr || aligned16(b))) {
+    if (bf16_fk(h) && aligned16(H) && aligned16(S) && aligned16(H_out) && (b == nullptr || aligned16(b))) {
       UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                    0, 0, residual, act, act_alpha, (float*)H_out, as_stream(stream_)};
       return launch_update_fk_bf16(a, Wp, nullptr, 0, 0, 0, nullptr, NT_SUM, NT_ACT_IDENTITY, 0.f, nullptr);
@@ -728,7 +734,7 @@ extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t
              NT_EINVAL, "feature pointers must be 16-byte aligned");
   if (dtype == NT_BF16) {
     // the fk skeleton (128-row tiles) when the plan comes with its row table, else the 64-row kernel
-    if (fkb_supported(h) && (tile_ptr == nullptr || row_table != nullptr)) {
+    if (bf16_fk(h) && (tile_ptr == nullptr || row_table != nullptr)) {
       NT_REQUIRE(row_table == nullptr || aligned16(row_table), NT_EINVAL, "row_table must be 16-byte aligned");
       UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                    0, 0, residual, act, act_alpha, (float*)H_out, as_stream(stream_)};
@@ -761,7 +767,7 @@ extern "C" int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const 
     NT_REQUIRE(h <= 512, NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul: bf16 needs h <= 512");
     if (M == 0) return NT_OK;
     NT_REQUIRE(X && Wp && out && X != out, NT_EINVAL, "NULL pointer or out aliases X");
-    if (fkb_supported(h) && aligned16(X) && aligned16(out)) {  // the bf16 layer kernel's dense mode
+    if (bf16_fk(h) && aligned16(X) && aligned16(out)) {  // the bf16 layer kernel's dense mode
       UpdateArgs a{nullptr, (const float*)X, nullptr, nullptr, Wp, nullptr, M, M, h,
                    0, 0, 0, NT_ACT_IDENTITY, 0.f, (float*)out, as_stream(stream_)};
       return launch_update_fk_bf16(a, Wp, nullptr, 0, 0, 0, nullptr, NT_SUM, NT_ACT_IDENTITY, 0.f, nullptr);

@@ -55,6 +55,14 @@
 #ifndef FK_RTABL
 #define FK_RTABL 0
 #endif
+// FK_DEPHASE (A/B builds): 1 = waves 4-7 run each k-step's split before its MFMAs
+#ifndef FK_DEPHASE
+#define FK_DEPHASE 0
+#endif
+// FK_GATHER2 (A/B builds): 1 = 64-B contiguous row reads per gather instruction (fp32, 128-row tiles)
+#ifndef FK_GATHER2
+#define FK_GATHER2 0
+#endif
 
 namespace nt {
 namespace fk {
@@ -256,7 +264,13 @@ __device__ __forceinline__ void fk_gather(State<RT, CT, GD, PREC>& st, const Arg
   constexpr int NP = PREC ? 1 : State<RT, CT, GD, PREC>::PPT;
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
+#if FK_GATHER2
+    // fp32 128-row tiles: lanes g16 = 0..3 of a row read 64 contiguous bytes per instruction
+    // (pieces g16 and g16 + 4) instead of 16-B pieces at a 32-B stride
+    int p = PREC ? 4 * s + st.g16 : (RT == 8 ? 8 * s + st.g16 + 4 * u : 8 * s + st.kp0 + u);
+#else
     int p = PREC ? 4 * s + st.g16 : 8 * s + st.kp0 + u;
+#endif
     p = p < st.hv ? p : 0;
     st.gs[P][u] = S4[sb + p];
     st.gq[P][u] = H4[qb + p];
@@ -288,7 +302,11 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC>& st, const Args
   float x[4 * St::PPT];
 #pragma unroll
   for (int u = 0; u < St::PPT; ++u) {
+#if FK_GATHER2
+    const bool in = (RT == 8 ? 8 * s + st.g16 + 4 * u : 8 * s + st.kp0 + u) < st.hv;
+#else
     const bool in = 8 * s + st.kp0 + u < st.hv;
+#endif
     const f32x4 sv = st.gs[P][u];
     const f32x4 qv = st.gq[P][u];
 #pragma unroll
@@ -300,6 +318,26 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC>& st, const Args
   }
   char* base = st.abuf + BUF * St::kBufB + st.grt * 1024 + st.lane * 16 +
                (RT == 8 ? 0 : 8 * (st.wave >> 2));
+#if FK_GATHER2
+  if constexpr (RT == 8) {
+    // piece u holds k = 16 u + 4 g16 .. + 3: fragment k-group 2 u + (g16 >> 1), half g16 & 1
+    char* tb = st.abuf + BUF * St::kBufB + st.grt * 1024 + st.fr * 16 + 8 * (st.g16 & 1);
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      f16x4 h0, h1;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const _Float16 t0 = (_Float16)x[4 * u + c];
+        h0[c] = t0;
+        h1[c] = (_Float16)(x[4 * u + c] - (float)t0);
+      }
+      char* dst = tb + (2 * u + (st.g16 >> 1)) * 256;
+      *reinterpret_cast<f16x4*>(dst) = h0;
+      *reinterpret_cast<f16x4*>(dst + St::kPartB) = h1;
+    }
+    return;
+  }
+#endif
   if constexpr (St::PPT == 2) {
     f16x8 h0, h1;
 #pragma unroll
@@ -815,23 +853,25 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
 #pragma unroll
       for (int P = 0; P < 2; ++P) {
         const int k = kb + s0 + P;
-        // (2) MFMAs of step k
-        if constexpr ((ABL & 2) == 0) {
-          if (P == 0) fk_mfma_sw<RT, CT, 0>(st, c, nrt);
-          else fk_mfma_sw<RT, CT, 1>(st, c, nrt);
-        }
-        stamp(0);
-        // (3) W fragments of step k + 2 into the registers step k used
-        {
-          int c2, s2;
-          kcs(k + 2 < SPT ? k + 2 : k + 2 - SPT, c2, s2);
-          if (P == 0) fk_load_w<RT, CT, 0>(st, c2, s2);
-          else fk_load_w<RT, CT, 1>(st, c2, s2);
-        }
-        stamp(1);
-        // (4) split step k + 1's staged piece into the other buffer, then gather step k + 3 into the
-        // freed slot (tile i or i + 1)
-        {
+        auto phase_mfma = [&]() __attribute__((always_inline)) {
+          // (2) MFMAs of step k
+          if constexpr ((ABL & 2) == 0) {
+            if (P == 0) fk_mfma_sw<RT, CT, 0>(st, c, nrt);
+            else fk_mfma_sw<RT, CT, 1>(st, c, nrt);
+          }
+          stamp(0);
+          // (3) W fragments of step k + 2 into the registers step k used
+          {
+            int c2, s2;
+            kcs(k + 2 < SPT ? k + 2 : k + 2 - SPT, c2, s2);
+            if (P == 0) fk_load_w<RT, CT, 0>(st, c2, s2);
+            else fk_load_w<RT, CT, 1>(st, c2, s2);
+          }
+          stamp(1);
+        };
+        auto phase_split = [&]() __attribute__((always_inline)) {
+          // (4) split step k + 1's staged piece into the other buffer, then gather step k + 3 into the
+          // freed slot (tile i or i + 1)
           const int k1 = k + 1 < SPT ? k + 1 : k + 1 - SPT;
           const int s1 = k1 - (k1 / a.KS) * a.KS;
           if constexpr ((ABL & 4) == 0) {
@@ -848,8 +888,23 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
 #endif
           if (P == 0) fk_gather<RT, CT, ACT, 1>(st, a, so, qo, s3);
           else fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s3);
+          stamp(2);
+        };
+#if FK_DEPHASE
+        // the two waves of a SIMD (w, w + 4) run the step's phases in opposite orders, so one
+        // wave's split VALU runs beside its partner's MFMAs instead of both contending for the
+        // matrix pipe and then both for the VALU
+        if (st.wave < 4) {
+          phase_mfma();
+          phase_split();
+        } else {
+          phase_split();
+          phase_mfma();
         }
-        stamp(2);
+#else
+        phase_mfma();
+        phase_split();
+#endif
         if constexpr ((ABL & 16) == 0) fk_barrier();
         stamp(3);
       }
