@@ -77,6 +77,10 @@ def parse():
     p.add_argument("--workload", default="qm9-4096", choices=sorted(WORKLOADS))
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget per thread count")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--event-every", type=int, default=8,
+                   help="the roofline's per-launch HIP events on every N-th step of the timed region (each "
+                        "event record costs the step about 7 us, so recording every step would slow the "
+                        "headline it sits in by about 5 %%)")
     p.add_argument("--no-embedded", action="store_true", help="skip embedded / fresh / end-to-end legs")
     p.add_argument("--no-secondary", action="store_true", help="skip the config-3 / config-5 keys")
     p.add_argument("--no-training", action="store_true", help="skip the training key (N=1 only)")
@@ -373,21 +377,30 @@ def run_workload(name, args, env, dev, headline):
     readout = Sum()
     torch.cuda.synchronize(dev)
 
+    events = []
+    every = max(1, args.event_every)
+    count = [0]
+
     def step():
+        # the per-launch roofline events ride on every `every`-th step (the first of the timed region
+        # included); the others run exactly as a user's forward does
+        _engine.UPDATE_EVENTS = events if count[0] % every == 0 else None
+        count[0] += 1
         for j in jobs:
             readout(block(j.Gd))
 
-    events = []
     with torch.no_grad():
         for _ in range(args.warmup):
             step()
-    _engine.UPDATE_EVENTS = events
+    events.clear()
+    count[0] = 0
     elapsed = timed_steps(step, args.steps, 0, env, dev)
     _engine.UPDATE_EVENTS = None
     info = dict(_engine.LAST_UPDATE_INFO)
     E_rank = sum(j.E for j in jobs)
     units, secs, rate = aggregate_throughput(E_rank * depth * args.steps, elapsed, device=BOOK_DEV)
     res = {"jobs": jobs, "embedding": embedding, "block": block, "readout": readout, "events": events,
+           "event_every": every,
            "info": info, "units": units, "secs": secs, "rate": rate, "batch": batch, "ranges": ranges,
            "name": name, "kind": kind, "h": h, "depth": depth, "bf16": bf16, "n_mols": n_mols,
            "steps": args.steps}
@@ -553,6 +566,8 @@ def summary(res, args, env, pmc_csv=None):
     else:
         traffic, tsrc = committed_traffic(res["name"], kern)
     roof = launch_roofline(jobs, res["events"], info, traffic, tsrc)
+    roof["launch_sampling"] = (f"HIP events on the launch stream around every layer launch of every "
+                               f"{res['event_every']}-th step of the timed region ({len(res['events'])} launches)")
     t_step = res["secs"] / args.steps
     V = sum(j.V for j in jobs)
     E = sum(j.E for j in jobs)

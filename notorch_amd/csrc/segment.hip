@@ -30,7 +30,15 @@ __global__ void __launch_bounds__(256) segment_reduce_vec4(
     const int32_t b = seg_ptr[s], e = seg_ptr[s + 1];
     Reducer4<R> r;
     r.init();
-    for (int32_t j = b; j < e; ++j) {
+    int32_t j = b;
+    for (; j + 4 <= e; j += 4) {  // four rows in flight, pushed in order
+      float4 x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) x[u] = X[(perm ? (int64_t)perm[j + u] : (int64_t)(j + u)) * hv + c];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) r.push(act4_t<ACT>(x[u], act, alpha));
+    }
+    for (; j < e; ++j) {
       const int64_t row = perm ? perm[j] : j;
       r.push(act4_t<ACT>(X[row * hv + c], act, alpha));
     }
@@ -59,6 +67,7 @@ __global__ void __launch_bounds__(256) segment_reduce_scalar(
 }
 
 // ---------------- fused init + first aggregation ----------------
+
 template <int R, int ACT>
 __global__ void __launch_bounds__(256) init_aggregate_vec4(
     const float4* __restrict__ Xv, const float4* __restrict__ Xe, const int64_t* __restrict__ src,
@@ -299,10 +308,10 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
     if (vec) {
       const int64_t hv = h / 4;
       if (hv >= 32) {  // rows of >= 32 pieces: a wave per node, every piece of the row in one pass
-        const int grid = grid_for(V * 64, 256, 256 * 8);  // grid-stride: 32 waves per CU
 #ifndef NT_INIT_PPL1
 #define NT_INIT_PPL1 0  // A/B: 1 = one 64-piece pass at a time (the round-3 kernel)
 #endif
+        const int grid = grid_for(V * 64, 256, 256 * 8);  // grid-stride: 32 waves per CU
         if (hv <= 64 || NT_INIT_PPL1) {
           NT_DISPATCH_RA(reduce, act,
                          (init_aggregate_wave<R_, A_, 1><<<grid, 256, 0, stream>>>(

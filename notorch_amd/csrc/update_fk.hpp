@@ -59,6 +59,17 @@
 #ifndef FK_DEPHASE
 #define FK_DEPHASE 0
 #endif
+// FK_EPI3: the epilogue of 128-row tiles staged through LDS (see fk_epilogue3)
+#ifndef FK_EPI3
+#define FK_EPI3 0
+#endif
+// FK_STAMP (A/B builds): coarse s_memtime stamps (each right after a barrier or around the epilogue,
+// where no LDS / SMEM op is outstanding, so they cost little): per wave and launch the K-loop cycles,
+// the epilogue cycles and the first two k-steps of each unit (the tile-boundary drain), summed into
+// g_pk_stamps[0..3] (+ wave count at [4]); read by nt_debug_fk_stamps
+#ifndef FK_STAMP
+#define FK_STAMP 0
+#endif
 // FK_GATHER2 (A/B builds): 1 = 64-B contiguous row reads per gather instruction (fp32, 128-row tiles)
 #ifndef FK_GATHER2
 #define FK_GATHER2 0
@@ -247,6 +258,9 @@ struct State {
   float sA, sAW, inv;
   int rtabl;  // FK_RTABL builds: Args::rtabl
   char* abuf;
+  float* stage;  // FK_EPI3: 128-row x 128-column output staging (pitch kSP floats)
+  float* lbias;  // FK_EPI3: the bias in fp32 (h floats), loaded once
+  int* nlist;    // FK_EPI3: node segments of the current tile (start rows, count at [kNlistN])
   int4* emap;
   __amdgpu_buffer_rsrc_t wrsrc;
 };
@@ -695,6 +709,158 @@ __device__ __forceinline__ void fk_epilogue(State<RT, CT, GD, PREC>& st, const A
   fk_epi_col<0, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, i, c, load_next, i_next, c_next);
 }
 
+// --------------------------------------------------------------------------- LDS-staged epilogue
+// FK_EPI3 (128-row tiles): per group of 8 output column tiles (128 columns, one tile per wave) the
+// waves write their accumulators into a row-major LDS stage; then every thread takes whole 16-B row
+// pieces (piece p = tid & 31 of rows tid / 32 + 16 m): H_out = acc / s_A s_W + bias + H (the
+// residual read here as contiguous row pieces, so the accumulators start every tile at zero and no
+// load is pending across the tile boundary), stored as full 512-B row segments; the aggregated value
+// aact(H_out) goes back into the stage; then (node, piece) items reduce each node's consecutive
+// rows in order (bit-identical to the CPU scatter) and store S_out.  Three barriers per group.
+constexpr int kSP = 132;     // stage pitch in floats (128 + 4: conflict-free 16-B writes of 16 rows)
+constexpr int kNlistN = 132;  // node list: start rows [0, nseg], nseg at [kNlistN]
+constexpr int kStageB = 128 * kSP * 4;
+constexpr int kLbiasB = 512 * 4;
+constexpr int kNlistB = (kNlistN + 4) * 4;
+
+// residual pieces of group J for this thread's rows (piece tid & 31 of rows tid / 32 + 16 m)
+template <int J, int RT, int CT, int GD, int PREC>
+__device__ __forceinline__ void fk_epi3_resid(State<RT, CT, GD, PREC>& st, const Args& a, const int4* em, int c,
+                                              f32x4 (&rr)[RT]) {
+  const int tid = threadIdx.x, p = tid & 31, rg = tid >> 5;
+  const int col = 16 * (c * st.CTC + 8 * J) + 4 * p;
+  const int pc = col < a.h ? col >> 2 : 0;
+#pragma unroll
+  for (int m = 0; m < RT; ++m) {
+    const int e = em[rg + 16 * m].x;
+    const int64_t r = (int64_t)(e >= 0 ? e : 0) * st.hc + pc;
+    if constexpr (PREC == 1) {
+      const uint2 v = reinterpret_cast<const uint2*>(a.H)[r];
+      rr[m] = __builtin_bit_cast(f32x4, uint4{v.x, v.y, 0u, 0u});
+    } else {
+      rr[m] = reinterpret_cast<const f32x4*>(a.H)[r];
+    }
+  }
+}
+
+template <int J, int RT, int CT, int AACT, int GD, int PREC>
+__device__ __forceinline__ void fk_epi3_group(State<RT, CT, GD, PREC>& st, const Args& a, const int4* em, int c, int n,
+                                              bool resid, f32x4 (&rr)[RT]) {
+  if constexpr (J < CT) {
+    const int cb = 16 * (c * st.CTC + 8 * J);  // first column of the group
+    if (cb < a.h) {
+      const int tid = threadIdx.x, p = tid & 31, rg = tid >> 5;
+      const int col = cb + 4 * p;
+      const bool pok = col < a.h;
+      const int pc = pok ? col >> 2 : 0;  // 4-column piece index in the row
+      // (A) this wave's column tile of the group into the stage
+      if (c * st.CTC + 8 * J + st.wave < st.NT) {
+#pragma unroll
+        for (int rt = 0; rt < RT; ++rt)
+          *reinterpret_cast<f32x4*>(st.stage + (16 * rt + st.fr) * kSP + 16 * st.wave + 4 * st.g16) = st.acc[rt][J];
+      }
+      // group 0's residual pieces now (its accumulators are dead); later groups' were issued during
+      // the previous group
+      if (J == 0 && resid) fk_epi3_resid<0>(st, a, em, c, rr);
+      __syncthreads();
+      if (J == 0 && a.SO != nullptr && st.wave == 0) {  // the tile's node segments (start rows)
+        const int l = st.lane;
+        const bool s0 = l < n && (em[l].z & kFlagStart), s1 = l + 64 < n && (em[l + 64].z & kFlagStart);
+        const unsigned long long m0 = __ballot(s0), m1 = __ballot(s1);
+        const unsigned long long below = (1ull << l) - 1ull;
+        const int c0 = __popcll(m0);
+        if (s0) st.nlist[__popcll(m0 & below)] = l;
+        if (s1) st.nlist[c0 + __popcll(m1 & below)] = l + 64;
+        if (l == 0) {
+          const int ns = c0 + __popcll(m1);
+          st.nlist[ns] = n;
+          st.nlist[kNlistN] = ns;
+        }
+      }
+      // (B) rows: H_out, and aact(H_out) back into the stage
+      const f32x4 b4 = (a.bias && pok) ? *reinterpret_cast<const f32x4*>(st.lbias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int m = 0; m < RT; ++m) {
+        const int r = rg + 16 * m;
+        if (r < n && pok) {
+          const int e = em[r].x;
+          float* sp = st.stage + r * kSP + 4 * p;
+          const f32x4 v = *reinterpret_cast<const f32x4*>(sp);
+          f32x4 o;
+          if constexpr (PREC == 1) {
+            const float4 w = bf4_widen(__builtin_bit_cast(uint4, rr[m]));
+            const f32x4 h4 = resid ? f32x4{w.x, w.y, w.z, w.w} : f32x4{0.f, 0.f, 0.f, 0.f};
+            const uint2 ob = bf4_pack((v[0] + b4[0]) + h4[0], (v[1] + b4[1]) + h4[1], (v[2] + b4[2]) + h4[2],
+                                      (v[3] + b4[3]) + h4[3]);
+            reinterpret_cast<uint2*>(a.O)[(int64_t)e * st.hc + pc] = ob;
+            const float4 s4 = bf4_widen(uint4{ob.x, ob.y, 0u, 0u});
+            o = f32x4{s4.x, s4.y, s4.z, s4.w};
+          } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) o[q] = fmaf(v[q], st.inv, b4[q]) + (resid ? rr[m][q] : 0.f);
+            reinterpret_cast<f32x4*>(a.O)[(int64_t)e * st.hc + pc] = o;
+            st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+          }
+          if (a.SO != nullptr) {
+            f32x4 ag;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) ag[q] = act_t<AACT>(o[q], a.aact, a.aalpha);
+            *reinterpret_cast<f32x4*>(sp) = ag;
+          }
+        }
+      }
+      // the next group's residual pieces, in flight across (C) and the next staging round trip
+      if constexpr (J + 1 < CT) {
+        if (resid && 16 * (c * st.CTC + 8 * (J + 1)) < a.h) fk_epi3_resid<J + 1>(st, a, em, c, rr);
+      }
+      if (a.SO != nullptr) {
+        __syncthreads();
+        // (C) nodes: each node's rows are consecutive in the tile; reduce them in order
+        const int ns = st.nlist[kNlistN];
+        for (int k = rg; k < ns; k += 16) {
+          const int r0 = st.nlist[k], r1 = st.nlist[k + 1];
+          if (pok && (em[r1 - 1].z & kFlagEnd)) {  // hub rows (no end flag) are left to the hub kernel
+            f32x4 x = *reinterpret_cast<const f32x4*>(st.stage + r0 * kSP + 4 * p);
+            for (int r = r0 + 1; r < r1; ++r) {
+              const f32x4 y = *reinterpret_cast<const f32x4*>(st.stage + r * kSP + 4 * p);
+              if (a.reduce == NT_MAX) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], y[q]);
+              } else if (a.reduce == NT_MIN) {
+#pragma unroll
+                for (int q = 0; q < 4; ++q) x[q] = fminf(x[q], y[q]);
+              } else {
+                x = x + y;
+              }
+            }
+            if (a.reduce == NT_MEAN) {
+              const float inv_n = 1.f / (float)(r1 - r0);
+              x = x * f32x4{inv_n, inv_n, inv_n, inv_n};
+            }
+            const int node = em[r0].y;
+            if constexpr (PREC == 1) {
+              reinterpret_cast<uint2*>(a.SO)[(int64_t)node * st.hc + pc] = bf4_pack(x[0], x[1], x[2], x[3]);
+            } else {
+              reinterpret_cast<f32x4*>(a.SO)[(int64_t)node * st.hc + pc] = x;
+              st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+            }
+          }
+        }
+      }
+      if constexpr (J + 1 < CT) __syncthreads();  // the next group overwrites the stage
+    }
+    fk_epi3_group<J + 1, RT, CT, AACT, GD, PREC>(st, a, em, c, n, resid, rr);
+  }
+}
+
+template <int RT, int CT, int AACT, int GD, int PREC>
+__device__ __forceinline__ void fk_epilogue3(State<RT, CT, GD, PREC>& st, const Args& a, int i, int c, int n,
+                                             bool resid) {
+  const int4* em = st.emap + (i % kEmaps) * State<RT, CT, GD, PREC>::ROWS;
+  f32x4 rr[RT];
+  fk_epi3_group<0, RT, CT, AACT, GD, PREC>(st, a, em, c, n, resid, rr);
+}
+
 __device__ __forceinline__ void fk_barrier() {
   // LDS writes of this step retired, then the workgroup barrier (vector-memory loads stay in flight)
   __syncthreads();
@@ -712,7 +878,9 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   using St = State<RT, CT, GD, PREC>;
   constexpr int ROWS = St::ROWS;
   constexpr int kEmapB = kEmaps * ROWS * 16;
-  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * St::kBufB + kEmapB) / 16];
+  constexpr bool EPI3 = FK_EPI3 && RT == 8;
+  constexpr int kExtraB = EPI3 ? kStageB + kLbiasB + kNlistB : 0;
+  __shared__ __attribute__((aligned(16))) uint4 smem[(2 * St::kBufB + kEmapB + kExtraB) / 16];
 
   // XCD-aware persistent walk (blocks b and b + nxcd share an L2): each XCD one contiguous chunk
   int t0 = (int)blockIdx.x, tstride = (int)gridDim.x, ntl;
@@ -746,6 +914,19 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   st.CTC = 8 * CT;
   st.abuf = reinterpret_cast<char*>(smem);
   st.emap = reinterpret_cast<int4*>(st.abuf + 2 * St::kBufB);
+  st.stage = reinterpret_cast<float*>(st.abuf + 2 * St::kBufB + kEmapB);
+  st.lbias = st.stage + (EPI3 ? kStageB / 4 : 0);
+  st.nlist = reinterpret_cast<int*>(st.lbias + (EPI3 ? kLbiasB / 4 : 0));
+  if constexpr (EPI3) {  // the bias in fp32, once (h <= 512 on 128-row tiles)
+    for (int q = tid; q < a.h; q += kThreads) {
+      float b = 0.f;
+      if (a.bias) {
+        if constexpr (PREC == 1) b = __uint_as_float((unsigned)reinterpret_cast<const unsigned short*>(a.bias)[q] << 16);
+        else b = a.bias[q];
+      }
+      st.lbias[q] = b;
+    }
+  }
   st.wrsrc = __builtin_amdgcn_make_buffer_rsrc(
       (void*)a.Wimg, (short)0, PREC ? ks_for(a.h) * nt_for(a.h) * 1024 : (int)image_bytes(a.h), 0x00020000);
   st.mxH = 0.f;
@@ -796,7 +977,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
 
   // ---- prologue: steps 0 and 1 staged, W of step 0, slice 0 split into buffer 0
   __syncthreads();  // emap of tiles 0 and 1
-  if (resid) {
+  if (resid && !EPI3) {  // EPI3 reads the residual in the epilogue: the accumulators start at zero
 #pragma unroll
     for (int j = 0; j < CT; ++j) fk_resid_load(st, a, 0, 0, j);
   }
@@ -842,11 +1023,22 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
       tp = t;
     }
   };
+  [[maybe_unused]] unsigned long long fs_k = 0, fs_e = 0, fs_f = 0, fs_t0 = 0, fs_t1 = 0;
   for (int u = 0; u < U; ++u) {
+#if FK_STAMP
+    fs_t0 = __builtin_amdgcn_s_memtime();
+#endif
     // (1) residual rows (loaded by the previous epilogue) into the accumulators' scale; without a
     // residual the accumulators are zero and the scale leaves them so.  Unconditional, so that no
     // path into the inner loop carries an accumulator load still pending.
-    fk_resid_scale(st);
+    if constexpr (EPI3) {  // accumulators restart at zero (dead across the staged epilogue)
+#pragma unroll
+      for (int rt = 0; rt < RT; ++rt)
+#pragma unroll
+        for (int j = 0; j < CT; ++j) st.acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else {
+      fk_resid_scale(st);
+    }
     const int nrt = (n_cur + 15) >> 4;
     const int kb = c * a.KS;
     for (int s0 = 0; s0 < a.KS; s0 += 2) {
@@ -907,15 +1099,26 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
 #endif
         if constexpr ((ABL & 16) == 0) fk_barrier();
         stamp(3);
+#if FK_STAMP
+        if (s0 == 0 && P == 1) fs_f += __builtin_amdgcn_s_memtime() - fs_t0;
+#endif
       }
     }
     // (5) epilogue of the unit; it starts the next (tile, chunk)'s residual loads
+#if FK_STAMP
+    fs_t1 = __builtin_amdgcn_s_memtime();
+    fs_k += fs_t1 - fs_t0;
+#endif
     const bool last_c = c + 1 == a.nchunks;
     const int i_next = last_c ? (i + 1 < ntl ? i + 1 : i) : i, c_next = last_c ? 0 : c + 1;
     if constexpr ((ABL & 8) == 0) {
-      fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
+      if constexpr (EPI3) fk_epilogue3<RT, CT, AACT, GD>(st, a, i, c, n_cur, resid);
+      else fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
       stamp(4);
     }
+#if FK_STAMP
+    fs_e += __builtin_amdgcn_s_memtime() - fs_t1;
+#endif
     // (6) advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
     c = c_next;
     if (last_c) {
@@ -932,6 +1135,15 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
       h3 = tile_head<RT, TABLE>(a, tile(i + 3));
     }
   }
+#if FK_STAMP
+  if (st.lane == 0) {
+    atomicAdd(&g_pk_stamps[0], fs_k);
+    atomicAdd(&g_pk_stamps[1], fs_e);
+    atomicAdd(&g_pk_stamps[2], fs_f);
+    atomicAdd(&g_pk_stamps[3], (unsigned long long)U);
+    atomicAdd(&g_pk_stamps[4], 1ull);
+  }
+#endif
   if (a.amax_out) {
     const float mh = wave_max(st.mxH), ms = wave_max(st.mxS);
     if (st.lane == 0) {

@@ -1078,6 +1078,17 @@ int amax_scratch(const float* H, int64_t nh, const float* S, int64_t ns, float**
 
 }  // namespace nt
 
+#if FK_STAMP
+// A/B builds only (FK_STAMP): read and reset the fk kernel's coarse stamp sums
+extern "C" __attribute__((visibility("default"))) int nt_debug_fk_stamps(unsigned long long* out5) {
+  if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(nt::g_pk_stamps), 5 * sizeof(unsigned long long), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return 2;
+  unsigned long long z[10] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(nt::g_pk_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : 2;
+}
+#endif
+
 extern "C" __attribute__((visibility("default"))) int nt_device_status(uint32_t* host_out,
                                                                       void* stream) {
   nt::clear_error();

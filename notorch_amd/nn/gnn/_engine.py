@@ -290,7 +290,7 @@ def block_forward(
     drop = (p, seed): training-mode dropout of every layer update (layer l draws from
     dropout_offset(l, E, h))."""
     V = Xv.shape[0]
-    amax = _amax_buffer(len(weights), Xv)
+    amax = _amax_buffer(len(weights), Xv, reuse=not keep_states)
     a0 = None if amax is None else amax[0]
     if len(weights) == 0:
         H, _ = K.dmpnn_init(Xv, Xe, src)
@@ -310,12 +310,32 @@ def block_forward(
 _NO_AMAX = torch.empty(0)  # a state without a valid amax row (bf16, or a path that skips the chain)
 
 
-def _amax_buffer(d: int, X: Tensor) -> Optional[Tensor]:
+# per (device, stream, depth): a ring of _AMAX_RING amax buffers for forwards that keep no states,
+# zeroed all at once every _AMAX_RING forwards instead of one fill kernel per forward
+_AMAX_RING = 64
+_amax_rings: dict = {}
+
+
+def _amax_buffer(d: int, X: Tensor, reuse: bool = False) -> Optional[Tensor]:
     """(d + 1) x 2 zeros: row l = (max|H_l|, max|S_l|), the fp32 layer kernel's split scales (the
-    init writes row 0, layer l reads row l and writes row l + 1).  None for bf16."""
+    init raises row 0, layer l reads row l and raises row l + 1).  None for bf16.
+    reuse (forwards whose states nothing keeps): the next buffer of this stream's ring; the whole ring
+    is zeroed when it wraps, which stream order makes safe (the forward that used a buffer last has
+    finished before the fill that re-zeroes it runs).  Not while a graph is being captured (a replay
+    must re-zero its own buffer)."""
     if X.dtype != torch.float32 or d == 0:
         return None
-    return torch.zeros(d + 1, 2, dtype=torch.float32, device=X.device)
+    if not reuse or torch.cuda.is_current_stream_capturing():
+        return torch.zeros(d + 1, 2, dtype=torch.float32, device=X.device)
+    key = (X.device, torch.cuda.current_stream(X.device).cuda_stream, d)
+    ent = _amax_rings.get(key)
+    if ent is None:
+        ent = _amax_rings[key] = [torch.empty(_AMAX_RING, d + 1, 2, dtype=torch.float32, device=X.device), 0]
+    buf, i = ent
+    if i == 0:
+        buf.zero_()
+    ent[1] = (i + 1) % _AMAX_RING
+    return buf[i]
 
 
 def dropout_offset(l: int, E: int, h: int) -> int:
@@ -350,7 +370,7 @@ def block_forward_embedded(
         H, _ = K.dmpnn_init_embed(node_table, node_types, edge_table, edge_types, src, validate=validate)
         node, H, _ = _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, False)
         return node, H
-    amax = _amax_buffer(len(weights), node_table)
+    amax = _amax_buffer(len(weights), node_table, reuse=True)
     H, S = K.dmpnn_init_embed(node_table, node_types, edge_table, edge_types, src, lay.dst_ptr,
                               lay.dst_perm, act=act, reduce=reduce, validate=validate,
                               amax=None if amax is None else amax[0])
@@ -461,7 +481,8 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
             H, S, src, rev, Wps[l], None if biases[l] is None else biases[l].detach(),
             residual=residual, act=act, plan=(tile_ptr, ntiles, dsts), tile_rows=rows, max_in_degree=maxdeg,
             perm=lay.dst_perm, reduce=reduce, agg_act=_IDENTITY if last else act, zero_fill=zero_fill,
-            amax_in=None if amax is None else amax[l], amax_out=None if amax is None else amax[l + 1],
+            amax_in=None if amax is None else amax[l],
+            amax_out=None if (amax is None or last) else amax[l + 1],  # row d has no reader
             row_table=rt, out=spare_H, S_out=None if last else spare_S,
         )
         if timer is not None:

@@ -282,3 +282,60 @@ def test_pack_fk_only_matches_full_pack():
         a, b = K.dense_matmul(X, full), K.dense_matmul(X, fk)
         assert torch.equal(a, b), h
         assert_parity(a, X.double() @ W.double().t(), FP32_NORM_TOL, f"dense h={h}")
+
+
+@pytest.mark.parametrize("h", [300, 128, 600])
+@pytest.mark.parametrize("reduce", ["sum", "max"])
+def test_fused_init_exact_on_skewed_degrees(h, reduce):
+    """nt_dmpnn_init with the aggregation (the wave-per-node-chunk kernel, chemprop.py:82-83 fused with
+    :37-39): a node of 150 in-edges (several 64-position index windows), runs of zero-in-degree nodes
+    (inside and at the ends of a chunk), one or two column passes (h = 600).  H0 and S bit-identical to
+    the CPU evaluation in the same order; amax raised to (max|H0|, max|S|) exactly."""
+    K = _K()
+    g = torch.Generator().manual_seed(h + len(reduce))
+    V = 61
+    deg = torch.randint(0, 6, (V,), generator=g)
+    deg[0] = 150
+    deg[3:6] = 0
+    deg[8] = 0
+    deg[-2:] = 0
+    dst = torch.repeat_interleave(torch.arange(V), deg)
+    dst = dst[torch.randperm(dst.numel(), generator=g)]
+    E = dst.numel()
+    src = torch.randint(0, V, (E,), generator=g)
+    Xv, Xe = torch.randn(V, h, generator=g), torch.randn(E, h, generator=g)
+    dst_ptr, perm = K.csr_build(dst.to(DEV), V)
+    relu = K.act_code(nn.ReLU())
+    am = torch.zeros(2, device=DEV)
+    H0, S = K.dmpnn_init(Xv.to(DEV), Xe.to(DEV), src.to(DEV), dst_ptr, perm, act=relu, reduce=reduce, amax=am)
+    rH = Xv[src] + Xe
+    assert torch.equal(H0.cpu(), rH)
+    rS = dmpnn_ref.scatter(torch.relu(rH), dst, V, reduce)
+    assert torch.equal(S.cpu(), rS)
+    assert am[0].item() == rH.abs().max().item()
+    assert am[1].item() == rS.abs().max().item()
+    am.zero_()
+    H0b, none = K.dmpnn_init(Xv.to(DEV), Xe.to(DEV), src.to(DEV), amax=am)  # no aggregation: S entry untouched
+    assert none is None and torch.equal(H0b.cpu(), rH)
+    assert am[0].item() == rH.abs().max().item() and am[1].item() == 0.0
+
+
+def test_amax_ring_wraps_bitexact():
+    """Forwards that keep no states take their split-scale rows from a per-stream ring that is zeroed
+    once per wrap (_engine._amax_buffer): 2.5 wraps of no-grad forwards give bit-identical outputs."""
+    from notorch_amd.nn import ChempropBlock, Sum
+    from notorch_amd.nn.gnn import _engine
+
+    G = _graph("qm9", 64, seed=5)
+    h = 128
+    g = torch.Generator().manual_seed(6)
+    Gd = G.update(node_feats=torch.randn(G.num_nodes, h, generator=g),
+                  edge_feats=torch.randn(G.num_edges, h, generator=g)).to(DEV)
+    blk = ChempropBlock(hidden_dim=h, depth=3).to(DEV).eval()
+    with torch.no_grad():
+        first = Sum()(blk(Gd))
+        outs = [Sum()(blk(Gd)) for _ in range(int(2.5 * _engine._AMAX_RING))]
+    torch.cuda.synchronize()
+    assert all(torch.equal(first, o) for o in outs)
+    key = next(k for k in _engine._amax_rings if k[2] == 3)
+    assert _engine._amax_rings[key][0].shape == (_engine._AMAX_RING, 4, 2)

@@ -91,6 +91,10 @@ def main():
         "fk_stagger2": fk_stagger(2),
         "fk_stagger4": fk_stagger(4),
         "init": lambda: K.dmpnn_init(Xv, H, src, lay.dst_ptr, lay.dst_perm, act=relu, amax=amax_out),
+        "init_noamax": lambda: K.dmpnn_init(Xv, H, src, lay.dst_ptr, lay.dst_perm, act=relu),
+        "fk_noamax": lambda: K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=plans[128][0], tile_rows=128,
+                                                  max_in_degree=deg, perm=lay.dst_perm, agg_act=relu, amax_in=amax,
+                                                  row_table=plans[128][1], out=out, S_out=S2),
         "absmax": lambda: K.absmax(H, amax_out[0:1]),
         "pack": lambda: K.pack_weights(W),
     }

@@ -8,7 +8,7 @@ if [ -n "${PARITY:-}" ]; then  # quick parity of each variant build (the wide fu
   for V in $VARIANTS; do
     LIBV=${V%@*}; [ "$LIBV" != "$V" ] && continue
     if [ "$V" = base ]; then L=""; else L="variant:$V"; fi
-    NT_LIB=$L timeout -k 10 300 python -u -m pytest tests/test_gpu_fk.py -x -q -k "wide_plan or far_from" --timeout 120 --timeout-method thread > gpurun_out/ab_parity_$V.log 2>&1 || { echo "parity FAILED for $V"; tail -15 gpurun_out/ab_parity_$V.log; exit 5; }
+    NT_LIB=$L timeout -k 10 300 python -u -m pytest ${PARITY_TESTS:-tests/test_gpu_fk.py -k "wide_plan or far_from"} -x -q --timeout 120 --timeout-method thread > gpurun_out/ab_parity_$V.log 2>&1 || { echo "parity FAILED for $V"; tail -15 gpurun_out/ab_parity_$V.log; exit 5; }
     echo "parity $V: $(tail -1 gpurun_out/ab_parity_$V.log)"
   done
 fi
