@@ -521,7 +521,7 @@ def pipeline_leg(res, dev, workers, n_batches=24, warm=4):
 def training_leg(args, timeout_s=300):
     """Training steps as the reference trains (tools/train_bench.py --json, each in a fresh child
     process: zero_grad + forward + backward + Adam(lr=1e-4).step(), 10 warm-ups and at least 1 s
-    more, median of 50 event-timed steps).  Headline: config 2 on the default (kernel) weight-grad
+    more; 50 steps back to back in rounds of 10 between two events, the median round per step).  Headline: config 2 on the default (kernel) weight-grad
     path; `library` is the same step with NT_WGRAD=library, a comparison only; `config3_bf16` is
     config 3 (zinc-4096, bf16, h=512, depth=5) on the default path."""
     import subprocess
@@ -529,8 +529,9 @@ def training_leg(args, timeout_s=300):
     script = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tools", "train_bench.py")
     out = {"step": "config 2 batch (4096 qm9-shaped molecules, seed 1000), ChempropBlock depth=3 h=300 + Sum, "
                    "zero_grad + forward + backward of sum(readout^2) w.r.t. weights and input features + "
-                   "Adam(lr=1e-4).step() (model.py:153,273), fp32; fresh process per leg; median of 50 after "
-                   "10 warm-ups and >= 1 s of warm-up steps",
+                   "Adam(lr=1e-4).step() (model.py:153,273), fp32; fresh process per leg; 50 steps back to back "
+                   "(no host sync between steps, as a training loop runs) in rounds of 10, median round per "
+                   "step, after 10 warm-ups and >= 1 s of warm-up steps",
            "unit": "edge-messages/s"}
 
     def run(env_extra, extra_args):

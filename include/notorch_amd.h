@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define NT_ABI_VERSION 4
+#define NT_ABI_VERSION 5
 
 #if defined(NT_BUILD)
 #define NT_API __attribute__((visibility("default")))
@@ -172,6 +172,21 @@ NT_API int nt_segment_reduce_chunked(const void* X, const int32_t* perm, const i
                                      const int32_t* seg_ptr, int64_t nseg, int64_t h, int reduce,
                                      int act, float act_alpha, int dtype, float* partial, void* out,
                                      float* amax_out, void* stream);
+
+/*
+ * nt_dmpnn_init fused with layer 0's aggregation on hub graphs (fp32): the chunked reduction above with
+ * the rows computed in pass 1 instead of read, H0[e] = Xv[src[e]] + Xe[e] (chemprop.py:82-83) stored
+ * as it goes, then S[v] = reduce act(H0) over v's chunks (chemprop.py:37-39, layer 0), so H0 is
+ * written once and never re-read.  (perm, chunk_pos, chunk_ptr, seg_ptr) as nt_segment_reduce_chunked
+ * on the dst CSR; H0 E x h, S V x h.  Same H0 as nt_dmpnn_init (bit-identical), same S as
+ * nt_segment_reduce_chunked of that H0.  amax_out (may be NULL): 2 zero-filled device floats raised to
+ * max|H0|, max|S|.
+ */
+NT_API int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64_t* src, const int32_t* perm,
+                                 const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
+                                 const int32_t* seg_ptr, int64_t V, int64_t E, int64_t h, int act,
+                                 float act_alpha, int reduce, int dtype, float* partial, void* H0, void* S,
+                                 float* amax_out, void* stream);
 
 /* Bytes of the packed weight image for one h x h layer (see nt_dmpnn_pack_weight). */
 NT_API size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype);

@@ -411,6 +411,61 @@ __global__ void __launch_bounds__(256) seg_chunk_partial(const T* __restrict__ X
   }
 }
 
+// The initial gather fused into pass 1 (hub graphs, fp32): the chunk's rows are computed, not read,
+// H0[e] = Xv[src[e]] + Xe[e] (stored: every dst-sorted position lies in exactly one chunk) and reduced
+// as act(H0) in the chunk's position order; amax[0] raised to max|H0|.  One lane per (chunk, piece),
+// 4 rows in flight.
+template <bool VEC, int R, int ACT>
+__global__ void __launch_bounds__(256) init_chunk_partial(const float* __restrict__ Xv, const float* __restrict__ Xe,
+                                                          const int64_t* __restrict__ src,
+                                                          const int32_t* __restrict__ perm,
+                                                          const int32_t* __restrict__ chunk_pos,
+                                                          int64_t nchunks, int64_t h, int act, float alpha,
+                                                          float* __restrict__ H0, float* __restrict__ P,
+                                                          float* __restrict__ amax) {
+  constexpr int N = Piece<float, VEC>::N;
+  constexpr int RR = R == NT_MEAN ? NT_SUM : R;  // the mean divides in the combine
+  const int64_t hw = h / N;
+  const int64_t total = nchunks * hw;
+  float m = 0.f;
+  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
+       t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t k = t / hw, c = (t - k * hw) * N;
+    const int32_t b = chunk_pos[k], e = chunk_pos[k + 1];
+    Reducer<RR> r[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) r[i].init();
+    for (int32_t j = b; j < e; j += 4) {
+      int64_t ed[4], sv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) ed[u] = perm[j + u < e ? j + u : b];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) sv[u] = src[ed[u]];
+      float xv[4][N], xe[4][N];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        Piece<float, VEC>::load(Xv + sv[u] * h + c, xv[u]);
+        Piece<float, VEC>::load(Xe + ed[u] * h + c, xe[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (j + u >= e) break;
+        float y[N];
+#pragma unroll
+        for (int i = 0; i < N; ++i) {
+          y[i] = xv[u][i] + xe[u][i];
+          m = fmaxf(m, fabsf(y[i]));
+          r[i].push(act_t<ACT>(y[i], act, alpha));
+        }
+        Piece<float, VEC>::store(H0 + ed[u] * h + c, y);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < N; ++i) P[k * h + c + i] = r[i].acc;  // raw accumulator (chunk non-empty)
+  }
+  if (amax) block_max_to(amax, m);
+}
+
 template <typename T, bool VEC, int R>
 __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict__ P,
                                                          const int32_t* __restrict__ chunk_ptr,
@@ -447,6 +502,31 @@ __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict
     for (int i = 0; i < N; ++i) m = fmaxf(m, fabsf(y[i]));
   }
   if (amax) block_max_to(amax, m);  // fp32 callers: max|out| (the fp32 layer kernel's split scale)
+}
+
+template <bool VEC>
+int launch_init_chunked(const float* Xv, const float* Xe, const int64_t* src, const int32_t* perm,
+                        const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr, const int32_t* seg_ptr,
+                        int64_t nseg, int64_t h, int reduce, int act, float alpha, float* P, float* H0, float* S,
+                        float* amax, hipStream_t stream) {
+  constexpr int N = Piece<float, VEC>::N;
+  if (nchunks > 0) {
+    const int g1 = grid_for(nchunks * (h / N), 256, 256 * 32);
+    NT_DISPATCH_RA(reduce, act,
+                   (init_chunk_partial<VEC, R_, A_><<<g1, 256, 0, stream>>>(
+                       Xv, Xe, src, perm, chunk_pos, nchunks, h, act, alpha, H0, P, amax)));
+    NT_LAUNCH_CHECK();
+  }
+  float* am1 = amax ? amax + 1 : nullptr;
+  const int g2 = grid_for(nseg * (h / N), 256, 256 * 32);
+  switch (reduce) {
+    case NT_SUM: seg_chunk_combine<float, VEC, NT_SUM><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, S, am1); break;
+    case NT_MEAN: seg_chunk_combine<float, VEC, NT_MEAN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, S, am1); break;
+    case NT_MAX: seg_chunk_combine<float, VEC, NT_MAX><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, S, am1); break;
+    default: seg_chunk_combine<float, VEC, NT_MIN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, S, am1); break;
+  }
+  NT_LAUNCH_CHECK();
+  return NT_OK;
 }
 
 template <typename T, bool VEC>
@@ -501,4 +581,28 @@ extern "C" int nt_segment_reduce_chunked(const void* X, const int32_t* perm, con
                                               reduce, act, act_alpha, partial, out, nullptr, stream)
              : launch_chunked<bf16_raw, false>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
                                                reduce, act, act_alpha, partial, out, nullptr, stream);
+}
+
+extern "C" int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64_t* src, const int32_t* perm,
+                                     const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
+                                     const int32_t* seg_ptr, int64_t V, int64_t E, int64_t h, int act,
+                                     float act_alpha, int reduce, int dtype, float* partial, void* H0, void* S,
+                                     float* amax_out, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_init_chunked is fp32 only");
+  NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
+  NT_REQUIRE(V >= 0 && E >= 0 && nchunks >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  if (V == 0) return NT_OK;
+  NT_REQUIRE(chunk_ptr && seg_ptr && S && (nchunks == 0 || (Xv && Xe && src && perm && chunk_pos && partial && H0)),
+             NT_EINVAL, "NULL pointer");
+  hipStream_t stream = as_stream(stream_);
+  const bool al = aligned16(Xv) && aligned16(Xe) && aligned16(H0) && aligned16(S) && aligned16(partial);
+  return (h % 4 == 0 && al)
+             ? launch_init_chunked<true>((const float*)Xv, (const float*)Xe, src, perm, chunk_pos, nchunks, chunk_ptr,
+                                         seg_ptr, V, h, reduce, act, act_alpha, partial, (float*)H0, (float*)S,
+                                         amax_out, stream)
+             : launch_init_chunked<false>((const float*)Xv, (const float*)Xe, src, perm, chunk_pos, nchunks,
+                                          chunk_ptr, seg_ptr, V, h, reduce, act, act_alpha, partial, (float*)H0,
+                                          (float*)S, amax_out, stream);
 }

@@ -315,6 +315,40 @@ def segment_reduce_chunked(
     return out
 
 
+def dmpnn_init_chunked(
+    Xv: Tensor,
+    Xe: Tensor,
+    src: Tensor,
+    seg_ptr: Tensor,
+    perm: Tensor,
+    plan: tuple[Tensor, int, Tensor],
+    *,
+    act: tuple[int, float] = (_lib.NT_ACT_IDENTITY, 0.0),
+    reduce: str = "sum",
+    amax: Tensor | None = None,
+) -> tuple[Tensor, Tensor]:
+    """(H0, S) = dmpnn_init with layer 0's aggregation over the chunk plan of a hub graph (fp32,
+    plan = chunk_plan(seg_ptr)): H0 written once, S combined from per-chunk partials.  amax (2
+    zero-filled device floats, optional) raised to max|H0|, max|S|."""
+    dev = _require_device(Xv, Xe, src, seg_ptr, perm, amax)
+    if Xv.dtype != torch.float32 or Xe.dtype != torch.float32:
+        raise ValueError("dmpnn_init_chunked is fp32 only")
+    _require_amax(amax, Xv.dtype)
+    V, h = Xv.shape
+    E = Xe.shape[0]
+    if Xe.shape[1] != h or src.numel() != E or perm.numel() != E or seg_ptr.numel() != V + 1:
+        raise ValueError("shape mismatch between Xv, Xe, src and the dst CSR")
+    chunk_pos, nchunks, chunk_ptr = plan
+    H0 = torch.empty(E, h, dtype=torch.float32, device=dev)
+    S = torch.empty(V, h, dtype=torch.float32, device=dev)
+    partial = torch.empty(max(nchunks, 1), h, dtype=torch.float32, device=dev)
+    _run(dev, _lib.load().nt_dmpnn_init_chunked,
+         _ptr(Xv.contiguous()), _ptr(Xe.contiguous()), _ptr(src), _ptr(perm), _ptr(chunk_pos), nchunks,
+         _ptr(chunk_ptr), _ptr(seg_ptr), V, E, h, act[0], act[1], reduce_code(reduce), _DTYPE_CODES[torch.float32],
+         _ptr(partial), _ptr(H0), _ptr(S), _ptr(amax), _stream(dev))
+    return H0, S
+
+
 def packed_weight_numel(h: int, dtype: torch.dtype = torch.float32) -> int:
     """Size (in 4-byte words) of one layer's packed weight image for feature dtype ``dtype``."""
     return _lib.load().nt_dmpnn_packed_weight_bytes(h, _DTYPE_CODES[dtype]) // 4

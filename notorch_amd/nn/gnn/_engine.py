@@ -297,8 +297,11 @@ def block_forward(
         return _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states,
                                drop)
     chunks = dst_chunks(lay)
-    if chunks is not None:
-        # hubs: the fused init would walk a hub's in-edges on one wave (polymer-16: 3.17 vs 3.00 ms)
+    if chunks is not None and Xv.dtype == torch.float32:
+        # hubs: the initial gather inside pass 1 of the chunked reduce (the wave-per-node init would walk
+        # a hub's in-edges on one wave), so H0 is written once and not re-read
+        H, S = K.dmpnn_init_chunked(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, chunks, act=act, reduce=reduce, amax=a0)
+    elif chunks is not None:
         H, _ = K.dmpnn_init(Xv, Xe, src, amax=a0)
         S = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks, amax=None if a0 is None else a0[1:2])
     else:

@@ -28,7 +28,7 @@ def test_header_declares_the_boundary():
         "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg", "nt_absmax", "nt_dmpnn_fused_tile_rows",
         "nt_dmpnn_tile_stride", "nt_dmpnn_row_table", "nt_dmpnn_pack_weight_fk", "nt_dmpnn_tile_plan_hubs",
         "nt_dmpnn_mark_hub_rows", "nt_dmpnn_hub_aggregate", "nt_dmpnn_weight_grad_fk",
-        "nt_softmax_pool_backward",
+        "nt_softmax_pool_backward", "nt_dmpnn_init_chunked",
     }
 
 
@@ -48,7 +48,7 @@ def test_abi_version_and_errors_without_gpu():
     from notorch_amd import _lib
 
     lib = _lib.load()
-    assert lib.nt_abi_version() == _lib.ABI_VERSION == 4
+    assert lib.nt_abi_version() == _lib.ABI_VERSION == 5
     assert lib.nt_dmpnn_packed_weight_bytes(300, 0) > 0
     assert lib.nt_dmpnn_packed_weight_bytes(0, 0) == 0
     # argument validation happens before any device call: EINVAL + message

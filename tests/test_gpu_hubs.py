@@ -166,3 +166,29 @@ def test_amax_outputs_of_the_producers():
     Gn = K.dmpnn_edge_backward(Gr, H0, dA, dS, dst, rev_ptr, rev_perm, dst_ptr, amax=gm2)
     assert gm2.item() == Gn.abs().max().item()
     assert _engine.hub_info(lay) is not None
+
+
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+def test_fused_chunked_init_matches_init_then_chunked_reduce(reduce):
+    """nt_dmpnn_init_chunked (hub graphs, fp32): H0 bit-identical to nt_dmpnn_init, S bit-identical to
+    nt_segment_reduce_chunked of that H0 (same chunks, same order), amax exact; h = 300 (16-B pieces)
+    and h = 30 (scalar pieces)."""
+    from notorch_amd import kernels as K
+
+    G = _polymer(2, seed=7)
+    lay = G._nt_layout
+    E, V = G.num_edges, G.num_nodes
+    src = G.edge_index[0].to(DEV)
+    dst_ptr, perm = lay.dst_ptr.to(DEV), lay.dst_perm.to(DEV)
+    chunks = K.chunk_plan(dst_ptr)
+    relu = K.act_code(nn.ReLU())
+    for h in (300, 30):
+        g = torch.Generator().manual_seed(h)
+        Xv, Xe = torch.randn(V, h, generator=g).to(DEV), torch.randn(E, h, generator=g).to(DEV)
+        am = torch.zeros(2, device=DEV)
+        H0, S = K.dmpnn_init_chunked(Xv, Xe, src, dst_ptr, perm, chunks, act=relu, reduce=reduce, amax=am)
+        rH, _ = K.dmpnn_init(Xv, Xe, src)
+        rS = K.segment_reduce_chunked(rH, dst_ptr, perm, V, chunks, reduce=reduce, act=relu)
+        assert torch.equal(H0, rH)
+        assert torch.equal(S, rS)
+        assert am[0].item() == rH.abs().max().item() and am[1].item() == rS.abs().max().item()
