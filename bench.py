@@ -550,6 +550,9 @@ def training_leg(args, timeout_s=300):
 
     out["kernel"] = run({}, [])
     out["library"] = run({"NT_WGRAD": "library"}, [])
+    # the same step with torch's fused Adam implementation (one optimizer kernel instead of torch's
+    # default foreach kernels, about 0.1 ms of tiny launches at config 2): a comparison, not the headline
+    out["kernel_adam_fused"] = run({}, ["--optim", "adam-fused"])
     if "train_ms" in out["kernel"]:
         out.update(weight_grad="kernel", train_ms=out["kernel"]["train_ms"], value=out["kernel"]["value"])
     out["config3_bf16"] = dict(run({}, ["--kind", "zinc", "--h", "512", "--depth", "5", "--dtype", "bf16"]),

@@ -677,23 +677,26 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
     E, h = states[0][0].shape if states else dH.shape
     src_ptr, src_perm, rev_ptr, rev_perm = backward_layout(lay, src, rev, V, E)
     mean_ptr = lay.dst_ptr if reduce == "mean" else None
-    if dH is None:
-        G = torch.zeros(E, h, dtype=dnode.dtype, device=src.device)
-    else:
-        G = dH.contiguous()
+    d = len(weights)
+    gdtype = (dH if dH is not None else dnode).dtype
+    # G = dL/dH_d: the gather of dnode below writes it whole when H_d itself has no gradient (no
+    # E x h zero fill to add it to)
+    G = dH.contiguous() if dH is not None else None
+    if G is None and dnode is None:
+        G = torch.zeros(E, h, dtype=gdtype, device=src.device)
     # fp32: max|G| of the current G, raised by the kernel that writes G (the fp16-split kernels'
-    # scale); None = unknown (nt_absmax computes it)
-    fp32 = G.dtype == torch.float32
+    # scale); None = unknown (nt_absmax computes it).  One zero-filled buffer for every layer's row.
+    fp32 = gdtype == torch.float32
+    gbuf = torch.zeros(d + 1, 2, dtype=torch.float32, device=src.device) if fp32 else None
     gmax_cur = None
     if dnode is not None:
-        gmax_cur = torch.zeros(2, dtype=torch.float32, device=src.device) if fp32 else None
+        gmax_cur = None if gbuf is None else gbuf[d]
         g1 = None if gmax_cur is None else gmax_cur[1:2]
         if maxmin:  # chemprop.py:86 with scatter_max / scatter_min
             arg = K.segment_arg(H_last, lay.dst_ptr, lay.dst_perm, V, reduce)
             G = K.gather_rows_arg(dnode.contiguous(), dst, arg, base=G, amax=g1)
         else:
             G = K.gather_rows(dnode.contiguous(), dst, base=G, seg_ptr=mean_ptr, amax=g1)
-    d = len(weights)
     dWs: list = [None] * d
     dbs: list = [None] * d
     wgrad = os.environ.get("NT_WGRAD", _WGRAD_DEFAULT)
@@ -738,7 +741,7 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             dA = torch.mm(Gu, W)
         del Gu
         dS = K.segment_reduce(dA, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY)
-        gmax_cur = torch.zeros(2, dtype=torch.float32, device=G.device) if fp32 and l > 0 else None
+        gmax_cur = gbuf[l - 1] if fp32 and l > 0 else None
         g1 = None if gmax_cur is None else gmax_cur[1:2]
         if maxmin:  # chemprop.py:39 with scatter_max / scatter_min: the arg of act(H_l) per node
             arg = K.segment_arg(H_l, lay.dst_ptr, lay.dst_perm, V, reduce, act=act)

@@ -38,9 +38,10 @@ def main():
                    help="after the counted warm-ups, keep warming up until this many seconds have passed "
                         "(lets the clocks settle in a fresh process)")
     p.add_argument("--modes", default="kernel,torch")
-    p.add_argument("--optim", default="adam", choices=["adam", "none"],
+    p.add_argument("--optim", default="adam", choices=["adam", "adam-fused", "none"],
                    help="adam: Adam(lr=1e-4).step() in every training step (the reference's default "
-                        "optim_factory); none: forward + backward only")
+                        "optim_factory; torch's foreach implementation); adam-fused: the same optimizer "
+                        "with torch's fused=True implementation; none: forward + backward only")
     p.add_argument("--json", action="store_true", help="print one JSON object instead of the table")
     a = p.parse_args()
     from notorch_amd import _lib
@@ -59,7 +60,9 @@ def main():
     Xv_d = Gd.node_feats.requires_grad_(True)
     Xe_d = Gd.edge_feats.requires_grad_(True)
     E = G.num_edges
-    opt = torch.optim.Adam(blk.parameters(), lr=1e-4) if a.optim == "adam" else None
+    opt = None
+    if a.optim != "none":
+        opt = torch.optim.Adam(blk.parameters(), lr=1e-4, **({"fused": True} if a.optim == "adam-fused" else {}))
 
     def step():
         blk.zero_grad(set_to_none=True)
