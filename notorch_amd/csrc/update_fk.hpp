@@ -240,10 +240,10 @@ __device__ __forceinline__ int4 row_entry(int4 raw, bool valid) {
 // --------------------------------------------------------------------------- kernel
 // Per-thread state of the kernel.  Plain members + force-inlined free functions taking it by
 // reference (no lambdas: closures holding pointers to these arrays kept them in scratch).
-template <int RT, int CT, int GD = 2, int PREC = 0>
+template <int RT, int CT, int GD = 2, int PREC = 0, int NW = 8>
 struct State {
   static constexpr int ROWS = 16 * RT;
-  static constexpr int PPT = RT / 4;        // 16-B pieces per thread per tensor per k-step (2 or 1)
+  static constexpr int PPT = 2 * RT / NW;   // 16-B pieces per thread per tensor per k-step (2 or 1)
   static constexpr int kPartB = RT * 1024;  // one fp16 part of a k-slice
   static constexpr int kBufB = 2 * kPartB;  // both parts
   f32x4 acc[RT][CT];
@@ -265,8 +265,8 @@ struct State {
   __amdgpu_buffer_rsrc_t wrsrc;
 };
 
-template <int RT, int CT, int ACT, int P, int GD, int PREC>
-__device__ __forceinline__ void fk_gather(State<RT, CT, GD, PREC>& st, const Args& a, int soff, int qoff, int s) {
+template <int RT, int CT, int ACT, int P, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_gather(State<RT, CT, GD, PREC, NW>& st, const Args& a, int soff, int qoff, int s) {
   st.gso[P] = soff;
   st.gqo[P] = qoff;
   const int sb = soff >= 0 ? soff : 0, qb = qoff >= 0 ? qoff : 0;
@@ -275,7 +275,7 @@ __device__ __forceinline__ void fk_gather(State<RT, CT, GD, PREC>& st, const Arg
   // so the load is unconditional and the compiler's vmcnt waits stay counted
   const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H ? a.H : a.S);
   // fp32: PPT pieces of 4 values; bf16: one piece of 8 values (128-row tiles), the same 8 k
-  constexpr int NP = PREC ? 1 : State<RT, CT, GD, PREC>::PPT;
+  constexpr int NP = PREC ? 1 : State<RT, CT, GD, PREC, NW>::PPT;
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
 #if FK_GATHER2
@@ -293,9 +293,9 @@ __device__ __forceinline__ void fk_gather(State<RT, CT, GD, PREC>& st, const Arg
 
 // A = S[src] - act(H[rev]) of the staged piece, scaled by s_A, split into two fp16 parts written in
 // MFMA B-fragment order (row tile grt, lane (k-group, row): 16 B per part) into LDS buffer P
-template <int RT, int CT, int ACT, int P, int BUF, int GD, int PREC>
-__device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC>& st, const Args& a, int s) {
-  using St = State<RT, CT, GD, PREC>;
+template <int RT, int CT, int ACT, int P, int BUF, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC, NW>& st, const Args& a, int s) {
+  using St = State<RT, CT, GD, PREC, NW>;
   const bool sok = st.gso[P] >= 0, qok = st.gqo[P] >= 0;
   if constexpr (PREC == 1) {
     // bf16 storage: A in fp32 from the widened pieces, one rounding to bf16, one fragment part
@@ -331,7 +331,7 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC>& st, const Args
     }
   }
   char* base = st.abuf + BUF * St::kBufB + st.grt * 1024 + st.lane * 16 +
-               (RT == 8 ? 0 : 8 * (st.wave >> 2));
+               (RT == NW ? 0 : 8 * (st.wave >> 2));
 #if FK_GATHER2
   if constexpr (RT == 8) {
     // piece u holds k = 16 u + 4 g16 .. + 3: fragment k-group 2 u + (g16 >> 1), half g16 & 1
@@ -375,13 +375,13 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC>& st, const Args
   }
 }
 
-template <int RT, int CT, int P, int GD, int PREC>
-__device__ __forceinline__ void fk_load_w(State<RT, CT, GD, PREC>& st, int c, int s) {
+template <int RT, int CT, int P, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_load_w(State<RT, CT, GD, PREC, NW>& st, int c, int s) {
 #pragma unroll
   for (int j = 0; j < CT; ++j) {
     // unconditional (no branch around vector-memory ops keeps the compiler's vmcnt waits counted):
     // a column tile past NT reads beyond the buffer's range, which returns zeros
-    const int ct = c * st.CTC + st.wave + 8 * j;
+    const int ct = c * st.CTC + st.wave + NW * j;
     // fp32: two parts per block behind the scale header; bf16: the plain bf16 image (one part)
     const int blk = PREC ? (s * st.NT + ct) * 1024 : kImgHdr + ((s * st.NT + ct) * 2) * 1024;
     int soff = __builtin_amdgcn_readfirstlane(ct < st.NT ? blk : 0x7fff0000);
@@ -410,9 +410,9 @@ __device__ __forceinline__ f32x4 fk_mac(uint4 w0r, uint4 w1r, f16x8 a0, f16x8 a1
   }
 }
 
-template <int RT, int CT, int P, int GD, int PREC>
-__device__ __forceinline__ void fk_mfma(State<RT, CT, GD, PREC>& st, int c, int nrt) {
-  using St = State<RT, CT, GD, PREC>;
+template <int RT, int CT, int P, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_mfma(State<RT, CT, GD, PREC, NW>& st, int c, int nrt) {
+  using St = State<RT, CT, GD, PREC, NW>;
   const char* bb = st.abuf + P * St::kBufB + st.lane * 16;
   // A fragments one row tile ahead; the schedule barriers keep the compiler from hoisting every row
   // tile's fragments (64 VGPRs) above the MFMAs
@@ -428,7 +428,7 @@ __device__ __forceinline__ void fk_mfma(State<RT, CT, GD, PREC>& st, int c, int 
       }
 #pragma unroll
       for (int j = 0; j < CT; ++j) {
-        if (c * st.CTC + st.wave + 8 * j < st.NT) {
+        if (c * st.CTC + st.wave + NW * j < st.NT) {
           st.acc[rt][j] = fk_mac<PREC>(st.wb[P][j][0], st.wb[P][j][1], a0, a1, st.acc[rt][j]);
         }
       }
@@ -443,9 +443,9 @@ __device__ __forceinline__ void fk_mfma(State<RT, CT, GD, PREC>& st, int c, int 
 // of the tile computed (rows past the tile hold zeros in the A buffer, so their accumulators keep
 // whatever they held and are never stored).  One scalar branch per step (the NCT switch) instead of
 // one per (row tile, column tile).
-template <int RT, int CT, int P, int GD, int NCT, int PREC>
-__device__ __forceinline__ void fk_mfma_nb(State<RT, CT, GD, PREC>& st) {
-  using St = State<RT, CT, GD, PREC>;
+template <int RT, int CT, int P, int GD, int NCT, int PREC, int NW>
+__device__ __forceinline__ void fk_mfma_nb(State<RT, CT, GD, PREC, NW>& st) {
+  using St = State<RT, CT, GD, PREC, NW>;
   const char* bb = st.abuf + P * St::kBufB + st.lane * 16;
   f16x8 a0 = *reinterpret_cast<const f16x8*>(bb);
   f16x8 a1 = PREC ? a0 : *reinterpret_cast<const f16x8*>(bb + St::kPartB);
@@ -466,8 +466,8 @@ __device__ __forceinline__ void fk_mfma_nb(State<RT, CT, GD, PREC>& st) {
   }
 }
 
-template <int RT, int CT, int P, int GD, int PREC>
-__device__ __forceinline__ void fk_mfma_sw(State<RT, CT, GD, PREC>& st, int c, int nrt) {
+template <int RT, int CT, int P, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_mfma_sw(State<RT, CT, GD, PREC, NW>& st, int c, int nrt) {
 #if FK_MFMA_MODE == 2
   // every wave runs all CT column tiles (past NT the W fragments read zeros): one straight-line
   // MFMA block per step, no per-wave branch
@@ -477,7 +477,7 @@ __device__ __forceinline__ void fk_mfma_sw(State<RT, CT, GD, PREC>& st, int c, i
 #elif FK_MFMA_MODE == 1
   // active column tiles of this wave in chunk c (wave-uniform)
   const int first = c * st.CTC + st.wave;
-  const int nct = first >= st.NT ? 0 : min(CT, (st.NT - first + 7) / 8);
+  const int nct = first >= st.NT ? 0 : min(CT, (st.NT - first + NW - 1) / NW);
   if constexpr (CT >= 4) {
     if (nct == 4) { fk_mfma_nb<RT, CT, P, GD, 4>(st); return; }
   }
@@ -496,10 +496,10 @@ __device__ __forceinline__ void fk_mfma_sw(State<RT, CT, GD, PREC>& st, int c, i
 // issued by the epilogue of the previous (tile, chunk) as soon as it has stored column tile j, so
 // they land during the rest of that epilogue; fk_resid_scale multiplies them by s_A s_W before the
 // first MFMA of the K loop (48 packed multiplies per tile, no staging registers).
-template <int RT, int CT, int GD, int PREC>
-__device__ __forceinline__ void fk_resid_load(State<RT, CT, GD, PREC>& st, const Args& a, int i, int c, int j) {
-  using St = State<RT, CT, GD, PREC>;
-  int pc = 4 * (c * st.CTC + st.wave + 8 * j) + st.g16;
+template <int RT, int CT, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_resid_load(State<RT, CT, GD, PREC, NW>& st, const Args& a, int i, int c, int j) {
+  using St = State<RT, CT, GD, PREC, NW>;
+  int pc = 4 * (c * st.CTC + st.wave + NW * j) + st.g16;
   pc = pc < st.hc ? pc : 0;
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
@@ -519,9 +519,9 @@ __device__ __forceinline__ void fk_resid_load(State<RT, CT, GD, PREC>& st, const
 
 // Bias of chunk c, column tile j: an unconditional load (no bias: S's first row, zeroed at use),
 // issued a whole chunk before the epilogue that uses it.
-template <int RT, int CT, int GD, int PREC>
-__device__ __forceinline__ void fk_bias_load(State<RT, CT, GD, PREC>& st, const Args& a, int c, int j) {
-  int pc = 4 * (c * st.CTC + st.wave + 8 * j) + st.g16;
+template <int RT, int CT, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_bias_load(State<RT, CT, GD, PREC, NW>& st, const Args& a, int c, int j) {
+  int pc = 4 * (c * st.CTC + st.wave + NW * j) + st.g16;
   pc = (pc < st.hc && a.bias) ? pc : 0;
   if constexpr (PREC == 1) {  // raw 8 B, widened at use
     const uint2 v = reinterpret_cast<const uint2*>(a.bias ? a.bias : a.S)[pc];
@@ -531,8 +531,8 @@ __device__ __forceinline__ void fk_bias_load(State<RT, CT, GD, PREC>& st, const 
   }
 }
 
-template <int RT, int CT, int GD, int PREC>
-__device__ __forceinline__ void fk_resid_scale(State<RT, CT, GD, PREC>& st) {
+template <int RT, int CT, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_resid_scale(State<RT, CT, GD, PREC, NW>& st) {
   if constexpr (PREC == 1) {  // bf16: widen the raw residual pieces (no scale)
 #pragma unroll
     for (int rt = 0; rt < RT; ++rt)
@@ -556,6 +556,10 @@ __device__ __forceinline__ void fk_resid_scale(State<RT, CT, GD, PREC>& st) {
 // Column tiles and row tiles are compile-time (template recursion: the loops hold convergent DPP /
 // ballot operations that the unroller leaves alone, and a runtime index puts the accumulators in
 // scratch).
+// 4-wave workgroups keep the bias in LDS instead of CT registers per thread (their 5 column tiles
+// per wave leave no registers for it)
+constexpr bool fk_lds_bias(int NW) { return NW == 4; }
+
 struct EpiCtx {
   const f32x4* b4;
   f32x4* O4;
@@ -564,8 +568,8 @@ struct EpiCtx {
   int n;
 };
 
-template <int RTI, int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL, int PREC>
-__device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC>& st, const Args& a, const EpiCtx& x0, int pc,
+template <int RTI, int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL, int PREC, int NW>
+__device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC, NW>& st, const Args& a, const EpiCtx& x0, int pc,
                                            bool pok, const f32x4& bj, f32x4& carry, float& ccnt) {
   if (16 * RTI < x0.n) {
     const int hc = st.hc;
@@ -668,14 +672,19 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC>& st, const Ar
     fk_epi_row<RTI + 1, J, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, pc, pok, bj, carry, ccnt);
 }
 
-template <int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL, int PREC>
-__device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC>& st, const Args& a, const EpiCtx& x0, int i, int c,
+template <int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL, int PREC, int NW>
+__device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC, NW>& st, const Args& a, const EpiCtx& x0, int i, int c,
                                            bool load_next, int i_next, int c_next) {
-  const int ct = c * st.CTC + st.wave + 8 * J;
+  const int ct = c * st.CTC + st.wave + NW * J;
   if (ct < st.NT) {
     const int pc = 4 * ct + st.g16;
     const bool pok = pc < st.hc;
-    f32x4 bj = (x0.b4 && pok) ? st.bias[J] : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 bj = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (fk_lds_bias(NW)) {  // the bias from LDS (copied once per workgroup): no registers
+      if (x0.b4 && pok) bj = *reinterpret_cast<const f32x4*>(st.lbias + 4 * pc);
+    } else {
+      if (x0.b4 && pok) bj = st.bias[J];
+    }
     if constexpr (PREC == 1) {  // the raw bf16 bias piece (zero bits stay zero)
       const float4 w = bf4_widen(__builtin_bit_cast(uint4, bj));
       bj = f32x4{w.x, w.y, w.z, w.w};
@@ -686,7 +695,7 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC>& st, const Ar
   }
   // column tile J is stored: its accumulators start the next (tile, chunk) (after the last tile the
   // loads re-read this tile's rows and go unused)
-  if (c_next != c) fk_bias_load(st, a, c_next, J);  // column chunks: the next chunk's bias
+  if (!fk_lds_bias(NW) && c_next != c) fk_bias_load(st, a, c_next, J);  // column chunks: the next chunk's bias
   if (load_next) {
     fk_resid_load(st, a, i_next, c_next, J);
   } else {
@@ -697,14 +706,14 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC>& st, const Ar
     fk_epi_col<J + 1, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, i, c, load_next, i_next, c_next);
 }
 
-template <int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL, int PREC>
-__device__ __forceinline__ void fk_epilogue(State<RT, CT, GD, PREC>& st, const Args& a, int i, int c, int n,
+template <int RT, int CT, int AACT, bool SUMONLY, int MAXL, int GD, int ABL, int PREC, int NW>
+__device__ __forceinline__ void fk_epilogue(State<RT, CT, GD, PREC, NW>& st, const Args& a, int i, int c, int n,
                                             bool load_next, int i_next, int c_next) {
   EpiCtx x0;
   x0.b4 = reinterpret_cast<const f32x4*>(a.bias);
   x0.O4 = reinterpret_cast<f32x4*>(a.O);
   x0.SO4 = reinterpret_cast<f32x4*>(a.SO);
-  x0.em = st.emap + (i % kEmaps) * State<RT, CT, GD, PREC>::ROWS;
+  x0.em = st.emap + (i % kEmaps) * State<RT, CT, GD, PREC, NW>::ROWS;
   x0.n = n;
   fk_epi_col<0, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, i, c, load_next, i_next, c_next);
 }
@@ -724,8 +733,8 @@ constexpr int kLbiasB = 512 * 4;
 constexpr int kNlistB = (kNlistN + 4) * 4;
 
 // residual pieces of group J for this thread's rows (piece tid & 31 of rows tid / 32 + 16 m)
-template <int J, int RT, int CT, int GD, int PREC>
-__device__ __forceinline__ void fk_epi3_resid(State<RT, CT, GD, PREC>& st, const Args& a, const int4* em, int c,
+template <int J, int RT, int CT, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_epi3_resid(State<RT, CT, GD, PREC, NW>& st, const Args& a, const int4* em, int c,
                                               f32x4 (&rr)[RT]) {
   const int tid = threadIdx.x, p = tid & 31, rg = tid >> 5;
   const int col = 16 * (c * st.CTC + 8 * J) + 4 * p;
@@ -743,8 +752,8 @@ __device__ __forceinline__ void fk_epi3_resid(State<RT, CT, GD, PREC>& st, const
   }
 }
 
-template <int J, int RT, int CT, int AACT, int GD, int PREC>
-__device__ __forceinline__ void fk_epi3_group(State<RT, CT, GD, PREC>& st, const Args& a, const int4* em, int c, int n,
+template <int J, int RT, int CT, int AACT, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_epi3_group(State<RT, CT, GD, PREC, NW>& st, const Args& a, const int4* em, int c, int n,
                                               bool resid, f32x4 (&rr)[RT]) {
   if constexpr (J < CT) {
     const int cb = 16 * (c * st.CTC + 8 * J);  // first column of the group
@@ -853,10 +862,10 @@ __device__ __forceinline__ void fk_epi3_group(State<RT, CT, GD, PREC>& st, const
   }
 }
 
-template <int RT, int CT, int AACT, int GD, int PREC>
-__device__ __forceinline__ void fk_epilogue3(State<RT, CT, GD, PREC>& st, const Args& a, int i, int c, int n,
+template <int RT, int CT, int AACT, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_epilogue3(State<RT, CT, GD, PREC, NW>& st, const Args& a, int i, int c, int n,
                                              bool resid) {
-  const int4* em = st.emap + (i % kEmaps) * State<RT, CT, GD, PREC>::ROWS;
+  const int4* em = st.emap + (i % kEmaps) * State<RT, CT, GD, PREC, NW>::ROWS;
   f32x4 rr[RT];
   fk_epi3_group<0, RT, CT, AACT, GD, PREC>(st, a, em, c, n, resid, rr);
 }
@@ -871,15 +880,19 @@ __device__ __forceinline__ void fk_barrier() {
 // 64 no H_out stores, 128 no S_out stores; 256 (results valid): per-phase s_memtime cycle sums into
 // g_pk_stamps (0 residual scale + MFMAs, 1 W issue, 2 split + gather issue, 3 barrier, 4 epilogue,
 // 6 whole loop, 7 waves).
-template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL, int GD = 2, int ABL = 0, int PREC = 0>
-__global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
+template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL, int GD = 2, int ABL = 0, int PREC = 0,
+          int NW = 8>
+__global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   // fused variants (MAXL > 1) read their rows from the row table, plain ones from src / rev
   constexpr bool TABLE = MAXL > 1;
-  using St = State<RT, CT, GD, PREC>;
+  using St = State<RT, CT, GD, PREC, NW>;
   constexpr int ROWS = St::ROWS;
   constexpr int kEmapB = kEmaps * ROWS * 16;
-  constexpr bool EPI3 = FK_EPI3 && RT == 8;
-  constexpr int kExtraB = EPI3 ? kStageB + kLbiasB + kNlistB : 0;
+  static_assert(RT == NW || (RT == 4 && NW == 8), "row tiles per wave mapping");
+  constexpr bool EPI3 = FK_EPI3 && RT == 8 && NW == 8;
+  constexpr bool LB = fk_lds_bias(NW);
+  static_assert(!LB || PREC == 0, "LDS bias: fp32 layers");
+  constexpr int kExtraB = EPI3 ? kStageB + kLbiasB + kNlistB : (LB ? kLbiasB : 0);
   __shared__ __attribute__((aligned(16))) uint4 smem[(2 * St::kBufB + kEmapB + kExtraB) / 16];
 
   // XCD-aware persistent walk (blocks b and b + nxcd share an L2): each XCD one contiguous chunk
@@ -904,21 +917,23 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
   st.wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   st.fr = st.lane & 15;
   st.g16 = st.lane >> 4;
-  st.grt = RT == 8 ? st.wave : (st.wave & 3);
+  // one row tile per wave when the waves are as many as the row tiles (128 rows / 8 waves, 64 / 4),
+  // else (64 rows / 8 waves) two waves per row tile, each half the k-pieces
+  st.grt = RT == NW ? st.wave : (st.wave & 3);
   st.grow = 16 * st.grt + st.fr;
-  st.kp0 = RT == 8 ? 2 * st.g16 : 2 * st.g16 + (st.wave >> 2);
+  st.kp0 = RT == NW ? 2 * st.g16 : 2 * st.g16 + (st.wave >> 2);
   st.hv = a.hv;       // fp32: h / 4 (16-B pieces of 4 floats); bf16: h / 8 (of 8 bf16)
   st.hc = a.h / 4;    // 4-column output pieces per row
   st.rtabl = a.rtabl;
   st.NT = a.NT;
-  st.CTC = 8 * CT;
+  st.CTC = NW * CT;
   st.abuf = reinterpret_cast<char*>(smem);
   st.emap = reinterpret_cast<int4*>(st.abuf + 2 * St::kBufB);
   st.stage = reinterpret_cast<float*>(st.abuf + 2 * St::kBufB + kEmapB);
   st.lbias = st.stage + (EPI3 ? kStageB / 4 : 0);
   st.nlist = reinterpret_cast<int*>(st.lbias + (EPI3 ? kLbiasB / 4 : 0));
-  if constexpr (EPI3) {  // the bias in fp32, once (h <= 512 on 128-row tiles)
-    for (int q = tid; q < a.h; q += kThreads) {
+  if constexpr (EPI3 || LB) {  // the bias in fp32, once (h <= 512)
+    for (int q = tid; q < a.h; q += 64 * NW) {
       float b = 0.f;
       if (a.bias) {
         if constexpr (PREC == 1) b = __uint_as_float((unsigned)reinterpret_cast<const unsigned short*>(a.bias)[q] << 16);
@@ -943,7 +958,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
     st.inv = 1.f / st.sAW;  // exact: a power of two
   }
   const bool resid = (ABL & 32) == 0 && a.residual && a.H != nullptr;
-  const bool info_writer = st.g16 == 0 && (RT == 8 || st.wave < 4);
+  const bool info_writer = st.g16 == 0 && st.wave < RT;
   const int SPT = a.nchunks * a.KS;  // steps per tile
 
   // ---- tile info: cur (tile i) and nxt (i + 1) row offsets, raw row of tile i + 2 in flight
@@ -982,7 +997,8 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk_kernel(Args a) {
     for (int j = 0; j < CT; ++j) fk_resid_load(st, a, 0, 0, j);
   }
 #pragma unroll
-  for (int j = 0; j < CT; ++j) fk_bias_load(st, a, 0, j);
+  for (int j = 0; j < CT; ++j)
+    if constexpr (!LB) fk_bias_load(st, a, 0, j);
   auto kcs = [&](int kk, int& cc, int& ss) __attribute__((always_inline)) {  // step in a tile -> chunk, k-step
     cc = kk / a.KS;
     ss = kk - cc * a.KS;

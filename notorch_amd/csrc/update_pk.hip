@@ -844,6 +844,39 @@ bool fk2_selected(int64_t h) {
 #endif
 }
 
+// Fused relu / sum layers given a plan of <= 64-row tiles (h <= 320): two independent 4-wave
+// workgroups per CU (5 column tiles per wave, the bias in LDS), so one workgroup's epilogue runs
+// beside the other's K loop instead of every CU's epilogue bursting at once.  Faster than the
+// 128-row walk on small batches (config 2: 115 vs 125 us), slower on large ones (qm9-32k: 905 vs
+// 894, polymer-16: 720 vs 691): the caller picks the plan rows (_engine.NW4_MAX_EDGES).
+// NT_FK_NW=8 turns it off, NT_FK_NW=4 makes it the tile capacity (tests).
+bool fk_nw4(int64_t h, bool fused, int act, int reduce, int aact) {
+  const char* e = getenv("NT_FK_NW");
+  return !(e && atoi(e) == 8) && fused && act == NT_ACT_RELU && reduce == NT_SUM &&
+         (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY) && fk::nt_for(h) <= 20;
+}
+bool fk_nw4_forced() {
+  const char* e = getenv("NT_FK_NW");
+  return e && atoi(e) == 4;
+}
+
+template <int AACT, int MAXL>
+int launch_fk_nw4_t(const fk::Args& a, int grid, hipStream_t stream) {
+  fk::update_fk_kernel<4, 5, NT_ACT_RELU, AACT, true, MAXL, 2, 0, 0, 4><<<grid, 256, 0, stream>>>(a);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+int launch_fk_nw4(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
+  if (a.aact == NT_ACT_RELU)
+    return maxl <= 3   ? launch_fk_nw4_t<NT_ACT_RELU, 3>(a, grid, stream)
+           : maxl <= 8 ? launch_fk_nw4_t<NT_ACT_RELU, 8>(a, grid, stream)
+                       : launch_fk_nw4_t<NT_ACT_RELU, 16>(a, grid, stream);
+  return maxl <= 3   ? launch_fk_nw4_t<NT_ACT_IDENTITY, 3>(a, grid, stream)
+         : maxl <= 8 ? launch_fk_nw4_t<NT_ACT_IDENTITY, 8>(a, grid, stream)
+                     : launch_fk_nw4_t<NT_ACT_IDENTITY, 16>(a, grid, stream);
+}
+
 // 64-row tiles: every other combination (any reduce, any aggregation act) and h > 384
 template <int CT>
 int launch_fk_narrow(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
@@ -869,7 +902,7 @@ int launch_fk_narrow(const fk::Args& a, int maxl, int grid, hipStream_t stream) 
 // whose act is relu / identity, or with no aggregation (fused < 0); else 64.  (The other variants
 // need more registers than two waves per SIMD hold at 128 rows.)
 int fk_tile_rows(int64_t h, int act, int reduce, int aact, bool fused) {
-  if (fk2_selected(h)) return 64;
+  if (fk2_selected(h) || (fk_nw4_forced() && fk_nw4(h, fused, act, reduce, aact))) return 64;
   const bool wide_ok =
       !fused || (act == NT_ACT_RELU && reduce == NT_SUM && (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY));
   return (fk::nt_for(h) <= 24 && wide_ok) ? 128 : 64;
@@ -935,6 +968,11 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
     return launch_fk2(a, grid, u.stream);
   }
 #endif
+  if (fused && tile_rows <= 64 && fk_nw4(u.h, true, u.act, reduce, aact)) {
+    a.nchunks = 1;
+    const int g4 = a.ntiles < 2 * cu_count() ? a.ntiles : 2 * cu_count();
+    return launch_fk_nw4(a, maxl, g4, u.stream);
+  }
   // up to 3 column tiles per wave (NT <= 24, one chunk); waves past NT skip theirs at run time
   if (cap == 128) {
     a.nchunks = 1;

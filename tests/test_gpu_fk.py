@@ -4,6 +4,8 @@ column-chunked h > 384 path, every aggregation variant, the amax chain that scal
 far from unit magnitude, hidden sizes beyond 512 (the reference accepts any hidden_dim,
 chemprop.py:54), and the kernels' row-capacity check.  Oracle: fp64 evaluation of chemprop.py:36-43 / residual.py:27-28 and
 the CPU scatter of the kernel's own H_out (chemprop.py:37-39, :86); fp32 contract FP32_NORM_TOL."""
+import os
+
 import pytest
 import torch
 import torch.nn as nn
@@ -61,7 +63,7 @@ def test_wide_plan_fused_layer(h, rev_offset, exact_deg):
     W, b = lin.weight.detach(), lin.bias.detach()
     relu = K.act_code(nn.ReLU())
     cap = K.fused_tile_rows(h, torch.float32, relu, "sum", relu)
-    assert cap == 128
+    assert cap == (64 if os.environ.get("NT_FK_NW") == "4" and h <= 320 else 128)  # NT_FK_NW=4: A/B walk
     perm, plan, maxdeg, zf = _layout(G, cap)
     assert max(int(x) for x in (plan[0][1:] - plan[0][:-1]).cpu()) <= cap
     amax_out = torch.zeros(2, device=DEV)
