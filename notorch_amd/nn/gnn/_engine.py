@@ -58,18 +58,20 @@ UPDATE_EVENTS: Optional[list] = None
 LAST_UPDATE_INFO: dict = {}
 
 
-def _note_update(kind: str, dtype: torch.dtype, h: int) -> None:
+def _note_update(kind: str, dtype: torch.dtype, h: int, rows: int = 0) -> None:
     kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
     if dtype == torch.bfloat16:
         info = dict(kernel="update_bf16_kernel (64-edge tiles, bf16 16x16x32 MFMA, fp32 accumulate)",
                     kernel_short="update_bf16", numerics="bf16 storage, bf16 MFMA, fp32 accumulate",
                     products=1)
     elif kind in ("fused", "persistent"):
-        rows = 128 if h <= 384 else 64
+        rows = rows or (128 if h <= 384 else 64)
         tail = ("aggregation of the next layer fused" if kind == "fused"
                 else "no tile plan: hub graph, aggregation by the chunked segment reduce")
-        info = dict(kernel=f"update_fk_kernel (persistent, {rows}-row node-aligned tiles, two-part fp16 split on "
-                           f"16x16x32 fp16 MFMA, {tail})", kernel_short="update_fk",
+        walk = ("two 4-wave workgroups per CU" if kind == "fused" and rows == 64 and h <= 320
+                else "one 8-wave workgroup per CU")
+        info = dict(kernel=f"update_fk_kernel (persistent, {walk}, {rows}-row node-aligned tiles, two-part fp16 "
+                           f"split on 16x16x32 fp16 MFMA, {tail})", kernel_short="update_fk",
                     numerics="fp32 via scaled two-part fp16 split (3 fp16 MFMA products, fp32 accumulate)",
                     products=3)
     else:
@@ -480,7 +482,7 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
     timer = UPDATE_EVENTS
     maxdeg = fused_max_in_degree(lay)
     hubs = hub_info(lay)
-    _note_update("fused", H.dtype, H.shape[1])
+    _note_update("fused", H.dtype, H.shape[1], rows)
     for l in range(d):
         last = l == d - 1
         if keep_states:
