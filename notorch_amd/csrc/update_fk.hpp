@@ -558,7 +558,11 @@ __device__ __forceinline__ void fk_resid_scale(State<RT, CT, GD, PREC, NW>& st) 
 // scratch).
 // 4-wave workgroups keep the bias in LDS instead of CT registers per thread (their 5 column tiles
 // per wave leave no registers for it)
-constexpr bool fk_lds_bias(int NW) { return NW == 4; }
+// (FK_LB8 A/B: also the 8-wave 128-row fp32 walk, h <= 384 there)
+#ifndef FK_LB8
+#define FK_LB8 0
+#endif
+constexpr bool fk_lds_bias(int NW, int RT, int PREC) { return PREC == 0 && (NW == 4 || (FK_LB8 && RT == 8)); }
 
 struct EpiCtx {
   const f32x4* b4;
@@ -680,7 +684,7 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC, NW>& st, cons
     const int pc = 4 * ct + st.g16;
     const bool pok = pc < st.hc;
     f32x4 bj = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (fk_lds_bias(NW)) {  // the bias from LDS (copied once per workgroup): no registers
+    if constexpr (fk_lds_bias(NW, RT, PREC)) {  // the bias from LDS (copied once per workgroup): no registers
       if (x0.b4 && pok) bj = *reinterpret_cast<const f32x4*>(st.lbias + 4 * pc);
     } else {
       if (x0.b4 && pok) bj = st.bias[J];
@@ -695,7 +699,7 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC, NW>& st, cons
   }
   // column tile J is stored: its accumulators start the next (tile, chunk) (after the last tile the
   // loads re-read this tile's rows and go unused)
-  if (!fk_lds_bias(NW) && c_next != c) fk_bias_load(st, a, c_next, J);  // column chunks: the next chunk's bias
+  if (!fk_lds_bias(NW, RT, PREC) && c_next != c) fk_bias_load(st, a, c_next, J);  // column chunks: the next chunk's bias
   if (load_next) {
     fk_resid_load(st, a, i_next, c_next, J);
   } else {
@@ -890,8 +894,7 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   constexpr int kEmapB = kEmaps * ROWS * 16;
   static_assert(RT == NW || (RT == 4 && NW == 8), "row tiles per wave mapping");
   constexpr bool EPI3 = FK_EPI3 && RT == 8 && NW == 8;
-  constexpr bool LB = fk_lds_bias(NW);
-  static_assert(!LB || PREC == 0, "LDS bias: fp32 layers");
+  constexpr bool LB = fk_lds_bias(NW, RT, PREC);
   constexpr int kExtraB = EPI3 ? kStageB + kLbiasB + kNlistB : (LB ? kLbiasB : 0);
   __shared__ __attribute__((aligned(16))) uint4 smem[(2 * St::kBufB + kEmapB + kExtraB) / 16];
 
