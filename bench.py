@@ -58,6 +58,8 @@ PEAK_16BIT_MFMA_TFLOPS = 2500.0  # dense bf16 / fp16 MFMA (MI355X_MICROARCH.md)
 WORKLOADS = {
     # name: (generator, molecules, hidden, depth, storage dtype)
     "qm9-4096": ("qm9", 4096, 300, 3, "f32"),  # BASELINE config 2 (the metric's configuration)
+    "qm9-8192": ("qm9", 8192, 300, 3, "f32"),  # batch-size sweep points (the fp32 layer's walk crossover)
+    "qm9-16k": ("qm9", 16384, 300, 3, "f32"),
     "qm9-32k": ("qm9", 32768, 300, 3, "f32"),  # HBM-scale batch (working set >> Infinity Cache)
     "qm9-125k": ("qm9", 125000, 300, 3, "f32"),  # one GPU's 1M/8 shard size in one batch
     "qm9-1m-sharded": ("qm9v", 1_000_000, 300, 3, "f32"),  # BASELINE config 4 (see header)

@@ -317,9 +317,9 @@ _NO_AMAX = torch.empty(0)  # a state without a valid amax row (bf16, or a path t
 
 # fp32 relu / sum layers on graphs of at most this many edges take 64-row tiles walked by two 4-wave
 # workgroups per CU (overlapping one's epilogue with the other's K loop); larger graphs keep the
-# 128-row walk.  Measured per launch: 78k edges 115 vs 125 us; 456k (polymer-16) 720 vs 691; 620k
-# (qm9-32k) 905 vs 894.
-NW4_MAX_EDGES = 262144
+# 128-row walk.  Measured per launch (tools/r4_sweep.sh, tools/r4_nw4b.sh): 78k edges 115-117 vs
+# 125 us; 155k 243 vs 244; 310k 465 vs 462; 456k (polymer-16) 720 vs 691; 621k 904 vs 895.
+NW4_MAX_EDGES = 131072
 
 # per (device, stream, depth): a ring of _AMAX_RING amax buffers for forwards that keep no states,
 # zeroed all at once every _AMAX_RING forwards instead of one fill kernel per forward
@@ -413,7 +413,7 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
     if fusable:  # the layer kernel's tile capacity for every layer of this block
         rows = min(K.fused_tile_rows(h, H.dtype, act, reduce, act),
                    K.fused_tile_rows(h, H.dtype, act, reduce, _IDENTITY))
-        if rows == 128 and fp32 and h <= 320 and E <= NW4_MAX_EDGES:
+        if rows == 128 and fp32 and h <= 320 and E <= NW4_MAX_EDGES and os.environ.get("NT_FK_NW") != "8":
             rows = 64  # the two-workgroups-per-CU walk of 64-row tiles (update_pk.hip, fk_nw4)
     plan = fused_plan(lay, V, E, rows, H.dtype) if fusable else None
     if plan is not None:
