@@ -28,6 +28,8 @@
 
 #include "common.hpp"
 #include "bf16.hpp"
+#include <string.h>
+
 #include "update.hpp"
 
 namespace nt {
@@ -617,7 +619,10 @@ extern "C" int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h
 
 extern "C" int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, int agg_act) {
   if (h <= 0) return 0;
-  if (dtype == NT_BF16) return bf16_fk(h) ? 128 : 64;
+  if (dtype == NT_BF16) {
+    const char* e = getenv("NT_BF16_KERNEL");
+    return bf16_fk(h) && strncmp(e, "fk4", 3) != 0 ? 128 : 64;  // fk4 (A/B): 64-row tiles, two workgroups per CU
+  }
   return nt::fk_tile_rows(h, act, reduce, agg_act, true);
 }
 

@@ -299,7 +299,7 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC, NW>& st, const 
   const bool sok = st.gso[P] >= 0, qok = st.gqo[P] >= 0;
   if constexpr (PREC == 1) {
     // bf16 storage: A in fp32 from the widened pieces, one rounding to bf16, one fragment part
-    static_assert(RT == 8, "bf16 fk tiles are 128 rows");
+    static_assert(RT == NW, "bf16 fk tiles: one row tile per wave");
     const bool in = 4 * s + st.g16 < st.hv;
     const uint4 su = __builtin_bit_cast(uint4, st.gs[P][0]), qu = __builtin_bit_cast(uint4, st.gq[P][0]);
     const unsigned sw[4] = {su.x, su.y, su.z, su.w}, qw[4] = {qu.x, qu.y, qu.z, qu.w};
@@ -562,7 +562,7 @@ __device__ __forceinline__ void fk_resid_scale(State<RT, CT, GD, PREC, NW>& st) 
 #ifndef FK_LB8
 #define FK_LB8 0
 #endif
-constexpr bool fk_lds_bias(int NW, int RT, int PREC) { return PREC == 0 && (NW == 4 || (FK_LB8 && RT == 8)); }
+constexpr bool fk_lds_bias(int NW, int RT, int PREC) { return NW == 4 || (FK_LB8 && RT == 8 && PREC == 0); }
 
 struct EpiCtx {
   const f32x4* b4;
@@ -689,7 +689,7 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC, NW>& st, cons
     } else {
       if (x0.b4 && pok) bj = st.bias[J];
     }
-    if constexpr (PREC == 1) {  // the raw bf16 bias piece (zero bits stay zero)
+    if constexpr (PREC == 1 && !fk_lds_bias(NW, RT, PREC)) {  // the raw bf16 bias piece (zero bits stay zero)
       const float4 w = bf4_widen(__builtin_bit_cast(uint4, bj));
       bj = f32x4{w.x, w.y, w.z, w.w};
     }

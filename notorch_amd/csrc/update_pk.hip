@@ -997,6 +997,14 @@ int launch_fkb_t(const fk::Args& a, int grid, hipStream_t stream) {
   NT_LAUNCH_CHECK();
   return NT_OK;
 }
+// A/B (NT_BF16_KERNEL=fk4): 64-row bf16 tiles walked by two 4-wave workgroups per CU, 8 column tiles
+// per wave (h <= 512), the bias in LDS
+template <int AACT, int MAXL>
+int launch_fkb4_t(const fk::Args& a, int grid, hipStream_t stream) {
+  fk::update_fk_kernel<4, 8, NT_ACT_RELU, AACT, true, MAXL, 2, 0, 1, 4><<<grid, 256, 0, stream>>>(a);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
 }  // namespace
 
 bool fkb_supported(int64_t h) { return h % 8 == 0 && h >= 8 && h <= 512; }
@@ -1052,6 +1060,18 @@ int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* 
     return launch_fkb_t<-1, NT_ACT_IDENTITY, true, 1>(a, grid, u.stream);
   }
   const int maxl = max_in_degree - 1;
+  {
+    const char* e = getenv("NT_BF16_KERNEL");
+    if (e && e[0] == 'f' && e[1] == 'k' && e[2] == '4' && tile_rows <= 64 && relu && reduce == NT_SUM &&
+        (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY)) {
+      const int g4 = a.ntiles < 2 * cu_count() ? a.ntiles : 2 * cu_count();
+      if (aact == NT_ACT_RELU)
+        return maxl <= 3 ? launch_fkb4_t<NT_ACT_RELU, 3>(a, g4, u.stream)
+                         : launch_fkb4_t<NT_ACT_RELU, 16>(a, g4, u.stream);
+      return maxl <= 3 ? launch_fkb4_t<NT_ACT_IDENTITY, 3>(a, g4, u.stream)
+                       : launch_fkb4_t<NT_ACT_IDENTITY, 16>(a, g4, u.stream);
+    }
+  }
   if (relu && reduce == NT_SUM && aact == NT_ACT_RELU)
     return maxl <= 3   ? launch_fkb_t<NT_ACT_RELU, NT_ACT_RELU, true, 3>(a, grid, u.stream)
            : maxl <= 8 ? launch_fkb_t<NT_ACT_RELU, NT_ACT_RELU, true, 8>(a, grid, u.stream)
