@@ -912,7 +912,14 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   }
   if (ntl <= 0) return;
   auto tile = [&](int i) __attribute__((always_inline)) { return t0 + (i < ntl ? i : ntl - 1) * tstride; };
-  for (int q = a.stagger * (((int)blockIdx.x / (nx > 0 ? nx : 1)) & 3); q > 0; --q) __builtin_amdgcn_s_sleep(127);
+  if constexpr (NW == 4) {
+    // two workgroups per CU: the second half of the grid (the second workgroup of each CU, which the
+    // XCD walk also gives the smaller tile count) starts `stagger` x 8k cycles late, so the pair's
+    // K loops and epilogues start out of phase (A/B: NT_FK_STAGGER)
+    for (int q = (int)blockIdx.x >= (int)gridDim.x / 2 ? a.stagger : 0; q > 0; --q) __builtin_amdgcn_s_sleep(127);
+  } else {
+    for (int q = a.stagger * (((int)blockIdx.x / (nx > 0 ? nx : 1)) & 3); q > 0; --q) __builtin_amdgcn_s_sleep(127);
+  }
 
   St st;
   const int tid = threadIdx.x;
