@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define NT_ABI_VERSION 5
+#define NT_ABI_VERSION 6
 
 #if defined(NT_BUILD)
 #define NT_API __attribute__((visibility("default")))
@@ -213,10 +213,15 @@ NT_API int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h, vo
  *   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b
  * H, S: E x h and V x h; src = edge_index[0], rev = rev_index (int64, arbitrary gather index);
  * Wp = nt_dmpnn_pack_weight image of W; b may be NULL (bias=False).  H_out must not alias H.
+ * fp32 with h % 4 == 0 runs the fp16x3 layer kernel: H, S, H_out and b must then be 16-byte aligned
+ * (NT_EINVAL otherwise), and amax_ws must point at 2 floats of caller-owned device memory that the
+ * call overwrites on `stream` with (max|H|, max|S|) before the layer reads them (the split scales;
+ * stream-ordered: reuse it only for work ordered after this call).  amax_ws may be NULL for bf16 and
+ * for h % 4 != 0 (the exact fp32 tile kernel).  (ABI 6: the library holds no device scratch.)
  */
 NT_API int nt_dmpnn_update(const void* H, const void* S, const int64_t* src, const int64_t* rev,
                     const void* Wp, const void* b, int64_t V, int64_t E, int64_t h, int residual,
-                    int act, float act_alpha, int dtype, void* H_out, void* stream);
+                    int act, float act_alpha, int dtype, float* amax_ws, void* H_out, void* stream);
 
 /*
  * Tile plan for nt_dmpnn_update_fused: cuts the dst-sorted edge order (positions of the
@@ -424,10 +429,12 @@ NT_API int nt_gather_rows_arg(const void* base, const void* X, const int64_t* id
 /* Dense layer GEMM, the backward's dA = G W of nn.Linear (chemprop.py:26,41), trained through
  * lightning_models/model.py:224-241 (the reference runs it as ATen addmm's autograd):
  *   out[i] = X[i] W^T,  i < M,   Wp = nt_dmpnn_pack_weight image of W (h x h; pass the image of W^T
- * for dA = G W).  The persistent bf16x6 MFMA layer kernel without gathers (fp32-accurate).
- * fp32 only; h % 4 == 0, h <= 304; 16-byte aligned; out != X. */
+ * for dA = G W).  fp32 (h % 4 == 0, 16-byte aligned, out != X): the fp16x3 layer kernel without
+ * gathers; amax_in = 2 device floats whose [1] >= max|X| (e.g. written by the kernel that produced
+ * X), or NULL: then amax_ws (2 floats of caller-owned device memory, required) receives
+ * (0, max|X|) on `stream` first.  bf16 (h <= 512): the bf16 layer kernel, amax_in / amax_ws unused. */
 NT_API int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const void* Wp, int dtype,
-                                 const float* amax_in, void* out, void* stream);
+                                 const float* amax_in, float* amax_ws, void* out, void* stream);
 
 /* Weight and bias gradient of one layer (backward of nn.Linear at chemprop.py:26,41, trained through
  * lightning_models/model.py:224-241; the reference runs it as ATen addmm's autograd), with the

@@ -23,7 +23,7 @@ if _NT_LIB.startswith("variant:"):
     LIB_PATH = os.path.join(_LIB_DIR, f"libnotorch_amd_{_NT_LIB.split(':', 1)[1]}.so")
 else:
     LIB_PATH = os.path.join(_LIB_DIR, "libnotorch_amd_diag.so" if DIAG else "libnotorch_amd.so")
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 NT_F32, NT_BF16 = 0, 1
 NT_SUM, NT_MEAN, NT_MAX, NT_MIN = 0, 1, 2, 3
@@ -87,7 +87,7 @@ SIGNATURES: dict[str, tuple] = {
     "nt_dmpnn_pack_weight_fk": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp]),
     "nt_dmpnn_update": (
         _c_int,
-        [_vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp],
+        [_vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp],
     ),
     "nt_dmpnn_tile_stride": (_c_i64, [_c_i64, _c_int, _c_int, _c_int]),
     "nt_dmpnn_tile_count": (_c_i64, [_c_i64, _c_i64]),
@@ -129,7 +129,7 @@ SIGNATURES: dict[str, tuple] = {
          _vp, _vp],
     ),
     "nt_gather_rows_arg": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_int, _vp, _vp, _vp]),
-    "nt_dmpnn_dense_matmul": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, _vp, _vp]),
+    "nt_dmpnn_dense_matmul": (_c_int, [_vp, _c_i64, _c_i64, _vp, _c_int, _vp, _vp, _vp, _vp]),
     "nt_dmpnn_weight_grad_workspace": (_c_i64, [_c_i64, _c_i64]),
     "nt_dmpnn_weight_grad": (
         _c_int,

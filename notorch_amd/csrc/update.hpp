@@ -58,8 +58,8 @@ int fk_row_table(const int32_t* perm, const int32_t* dsts, const int64_t* src, c
 int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_t img_stride, void* img,
             hipStream_t stream);
 int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);
-// a library-owned (max|H|, max|S|) slot filled on `stream` (H or S may be NULL: that entry stays 0)
-int amax_scratch(const float* H, int64_t nh, const float* S, int64_t ns, float** out, hipStream_t stream);
+// the caller's 2-float workspace ws := (max|H|, max|S|) on `stream` (H or S may be NULL: that entry is 0)
+int amax_fill(float* ws, const float* H, int64_t nh, const float* S, int64_t ns, hipStream_t stream);
 // bf16 storage on the same skeleton (PREC = 1): h % 8 == 0, h <= 512, tiles of <= 128 rows, Wimg =
 // the bf16 fragment image; S_out / the row table exactly with a tile plan
 bool fkb_supported(int64_t h);

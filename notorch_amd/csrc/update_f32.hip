@@ -650,7 +650,7 @@ extern "C" int nt_absmax(const void* X, int64_t n, int dtype, float* out, void* 
 extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
                                const int64_t* rev, const void* Wp, const void* b, int64_t V,
                                int64_t E, int64_t h, int residual, int act, float act_alpha,
-                               int dtype, void* H_out, void* stream_) {
+                               int dtype, float* amax_ws, void* H_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
@@ -689,12 +689,13 @@ extern "C" int nt_dmpnn_update(const void* H, const void* S, const int64_t* src,
   }
 #else
   // h % 4 == 0: update_fk_kernel in its plain mode (no aggregation); the split scales come from a
-  // max|H|, max|S| pass into a library-owned scratch slot (the C ABI call carries no amax)
+  // max|H|, max|S| pass into the caller's workspace (the C ABI call carries no amax)
   if (h % 4 == 0) {
     NT_REQUIRE(aligned16(H) && aligned16(S) && aligned16(H_out) && (b == nullptr || aligned16(b)), NT_EINVAL,
                "fp32 with h % 4 == 0 needs 16-byte aligned feature pointers");
-    float* amax = nullptr;
-    int rc = amax_scratch((const float*)H, E * h, (const float*)S, V * h, &amax, stream);
+    NT_REQUIRE(amax_ws != nullptr, NT_EINVAL, "fp32 with h % 4 == 0 needs amax_ws (2 device floats)");
+    float* amax = amax_ws;
+    int rc = amax_fill(amax, (const float*)H, E * h, (const float*)S, V * h, stream);
     if (rc != NT_OK) return rc;
     UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                  0, 0, residual, act, act_alpha, (float*)H_out, stream};
@@ -763,7 +764,7 @@ extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t
 // dense mode (row e of A is X[e]), any h % 4 == 0; amax_in = NULL: the persistent bf16x6 pk kernel
 // (h <= 304).
 extern "C" int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const void* Wp, int dtype,
-                                     const float* amax_in, void* out, void* stream_) {
+                                     const float* amax_in, float* amax_ws, void* out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "nt_dmpnn_dense_matmul: fp32 or bf16");
@@ -791,11 +792,11 @@ extern "C" int nt_dmpnn_dense_matmul(const void* X, int64_t M, int64_t h, const 
   NT_REQUIRE(X != out, NT_EINVAL, "out aliases X");
   NT_REQUIRE(aligned16(X) && aligned16(out) && aligned16(Wp), NT_EINVAL, "pointers must be 16-byte aligned");
 #ifndef NT_DIAG
-  if (!amax_in) {  // max|X| into a library-owned scratch slot
-    float* slot = nullptr;
-    int rc = amax_scratch(nullptr, 0, (const float*)X, M * h, &slot, as_stream(stream_));
+  if (!amax_in) {  // max|X| into the caller's workspace
+    NT_REQUIRE(amax_ws != nullptr, NT_EINVAL, "fp32 without amax_in needs amax_ws (2 device floats)");
+    int rc = amax_fill(amax_ws, nullptr, 0, (const float*)X, M * h, as_stream(stream_));
     if (rc != NT_OK) return rc;
-    amax_in = slot;
+    amax_in = amax_ws;
   }
 #endif
   if (amax_in) {

@@ -1,0 +1,377 @@
+// fp32 D-MPNN layer kernel at ONE wave per SIMD ("fw"), fused with the sum aggregation its output
+// feeds.  Included by update_pk.hip after update_fk.hpp (same numerics, image, tile plan and row
+// table as update_fk_kernel; it reuses that header's helpers).
+//
+//   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b        (chemprop.py:36-43,
+//                                                                                 residual.py:27-28)
+//   S_out[v] = sum_{e: dst[e] = v} aact(H_out[e])                                  (chemprop.py:37-39,
+//                                                                                 :86 with identity)
+//
+// Why a second skeleton.  update_fk_kernel runs two waves per SIMD that meet at one workgroup barrier
+// per k-step, so both waves of a SIMD issue their MFMAs in the same window and then their split VALU
+// in the same window: the matrix pipe idles while the split runs (MFMA busy 17 % at config 2).  Here
+// a 256-thread workgroup (4 waves, one per SIMD, up to 512 registers each) walks 128-row tiles, and
+// each wave issues its step's MFMAs (all 8 row tiles x its NCT column tiles x 3 split products)
+// with the side work of the same step placed between them: the W fragments of the next step, the
+// split of the next step's gathered A slice into the other LDS buffer, and the gathers of the step
+// after that.  The single wave keeps the MFMA stream and the VALU stream in one instruction stream,
+// so the split rides in the MFMA issue gaps instead of after them.
+//
+// Numerics are update_fk_kernel's bit for bit (same split, same s_A / s_W, same product order
+// W1 A0 + W0 A1 + W0 A0 per k-step in ascending k, the residual entering the accumulator scaled by
+// s_A s_W, the same epilogue rounding and the same left-to-right segmented node sums), so either
+// kernel may run any layer of a forward.
+//
+// Thread roles.  Gather / split: thread (wave w, lane l) stages row 32 w + (l & 31) of the tile,
+// k-groups 2 q and 2 q + 1 (q = l >> 5) of each 32-deep k-step: four 16-B pieces of S[src] and of
+// H[rev] per step (lanes l and l + 32 read the two halves of one 128-B row segment).  MFMA /
+// epilogue: wave w owns column tiles w, w + 4, ... (NCT of them, compile time) for all 8 row tiles;
+// lane l holds row l & 15 of a row tile, columns 4 (l >> 4) .. + 3 of a column tile.
+#pragma once
+
+#include "update_fk.hpp"
+
+namespace nt {
+namespace fw {
+
+using fk::Args;
+using fk::f16x4;
+using fk::f16x8;
+using fk::f32x4;
+
+constexpr int kThreads = 256;
+constexpr int kRT = 8;                // row tiles per tile
+constexpr int kRows = 16 * kRT;       // 128
+constexpr int kPartB = kRT * 1024;    // one fp16 part of a k-slice (8 KiB)
+constexpr int kBufB = 2 * kPartB;     // both parts
+constexpr int kEmaps = 4;             // row-info buffers (tile index mod 4)
+constexpr int kEmapB = kEmaps * kRows * 16;
+constexpr int kBiasB = 320 * 4;
+constexpr int kMaxNT = 20;            // h <= 320
+constexpr int kLdsB = 2 * kBufB + kEmapB + kBiasB;
+
+template <int NCT>
+struct St {
+  f32x4 acc[kRT][NCT];
+  uint4 wb[2][NCT][2];     // W fragments (parity, column tile, part)
+  f32x4 gs[2][4], gq[2][4];  // gathered pieces of two k-steps (slot, piece)
+  int gso[2], gqo[2];      // their row sources (float4 offsets, -1: none)
+  float mxH, mxS;
+  int lane, wave, fr, g16, grow, q, hv, hc, NT;
+  float sA, sAW, inv;
+  char* abuf;
+  int4* emap;
+  float* lbias;
+  __amdgpu_buffer_rsrc_t wrsrc;
+};
+
+// pieces 8 s + 4 q + u (u < 4) of the thread's row of S[src] and H[rev] into slot P
+template <int NCT, int P>
+__device__ __forceinline__ void fw_gather(St<NCT>& st, const Args& a, int soff, int qoff, int s) {
+  st.gso[P] = soff;
+  st.gqo[P] = qoff;
+  const int sb = soff >= 0 ? soff : 0, qb = qoff >= 0 ? qoff : 0;
+  const f32x4* S4 = reinterpret_cast<const f32x4*>(a.S);
+  const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H ? a.H : a.S);
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    int p = 8 * s + 4 * st.q + u;
+    p = p < st.hv ? p : 0;
+    st.gs[P][u] = S4[sb + p];
+    st.gq[P][u] = H4[qb + p];
+  }
+}
+
+// item v (k-group 2 q + v) of slot P: A = S[src] - act(H[rev]) scaled by s_A, split into two fp16
+// parts written in MFMA B-fragment order into LDS buffer BUF
+template <int NCT, int ACT, int P, int BUF>
+__device__ __forceinline__ void fw_split(St<NCT>& st, const Args& a, int s, int v) {
+  const bool sok = st.gso[P] >= 0, qok = st.gqo[P] >= 0;
+  f16x8 h0, h1;
+#pragma unroll
+  for (int uu = 0; uu < 2; ++uu) {
+    const int u = 2 * v + uu;
+    const bool in = 8 * s + 4 * st.q + u < st.hv;
+    const f32x4 sv = st.gs[P][u];
+    const f32x4 qv = st.gq[P][u];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float qa = act_t<ACT>(qv[c], a.act, a.alpha);
+      const float x = ((sok && in ? sv[c] : 0.f) - (qok && in ? qa : 0.f)) * st.sA;
+      const _Float16 t0 = (_Float16)x;
+      h0[4 * uu + c] = t0;
+      h1[4 * uu + c] = (_Float16)(x - (float)t0);
+    }
+  }
+  char* base = st.abuf + BUF * kBufB + (st.grow >> 4) * 1024 + ((2 * st.q + v) * 16 + (st.grow & 15)) * 16;
+  *reinterpret_cast<f16x8*>(base) = h0;
+  *reinterpret_cast<f16x8*>(base + kPartB) = h1;
+}
+
+// W fragments of k-step s, column tiles [J0, J1) of this wave, into parity P
+template <int NCT, int P, int J0, int J1>
+__device__ __forceinline__ void fw_load_w(St<NCT>& st, int s) {
+#pragma unroll
+  for (int j = J0; j < J1; ++j) {
+    const int ct = st.wave + 4 * j;
+    const int soff = __builtin_amdgcn_readfirstlane(fk::kImgHdr + ((s * st.NT + ct) * 2) * 1024);
+    st.wb[P][j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff, 0));
+    st.wb[P][j][1] =
+        __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff + 1024, 0));
+  }
+}
+
+// residual rows of tile i, column tile j, straight into the accumulators (scaled before the K loop)
+template <int NCT>
+__device__ __forceinline__ void fw_resid_load(St<NCT>& st, const Args& a, int i, int j) {
+  int pc = 4 * (st.wave + 4 * j) + st.g16;
+  pc = pc < st.hc ? pc : 0;
+#pragma unroll
+  for (int rt = 0; rt < kRT; ++rt) {
+    const int e = st.emap[(i % kEmaps) * kRows + 16 * rt + st.fr].x;
+    st.acc[rt][j] = reinterpret_cast<const f32x4*>(a.H)[(int64_t)(e >= 0 ? e : 0) * st.hc + pc];
+  }
+}
+
+// One k-step: MFMAs of step k (LDS buffer P, W parity P) with the side work of the step between
+// the row tiles: W of step k + 1 into parity 1 - P, the split of the staged step k + 1 (slot 1 - P)
+// into buffer 1 - P, then the gathers of step k + 3 into the freed slot.  Row tiles past the tile's
+// rows (nrt) are skipped as a whole (wave-uniform).
+template <int NCT, int ACT, int P>
+__device__ __forceinline__ void fw_step(St<NCT>& st, const Args& a, int s_w1, int s_split, int s_g, int g_soff,
+                                        int g_qoff, int nrt) {
+  const char* bb = st.abuf + P * kBufB + st.lane * 16;
+  f16x8 a0 = *reinterpret_cast<const f16x8*>(bb);
+  f16x8 a1 = *reinterpret_cast<const f16x8*>(bb + kPartB);
+  fk::sfor<kRT>([&](auto RTc) {
+    constexpr int rt = decltype(RTc)::value;
+    f16x8 n0 = a0, n1 = a1;
+    if constexpr (rt + 1 < kRT) {
+      n0 = *reinterpret_cast<const f16x8*>(bb + (rt + 1) * 1024);
+      n1 = *reinterpret_cast<const f16x8*>(bb + kPartB + (rt + 1) * 1024);
+    }
+    if (rt < 6 || rt < nrt) {
+#pragma unroll
+      for (int j = 0; j < NCT; ++j) st.acc[rt][j] = fk::fk_mac<0>(st.wb[P][j][0], st.wb[P][j][1], a0, a1, st.acc[rt][j]);
+    }
+    // side work of this row tile
+    if constexpr (rt == 0) fw_load_w<NCT, 1 - P, 0, (NCT + 1) / 2>(st, s_w1);
+    if constexpr (rt == 1) fw_load_w<NCT, 1 - P, (NCT + 1) / 2, NCT>(st, s_w1);
+    if constexpr (rt == 2) fw_split<NCT, ACT, 1 - P, 1 - P>(st, a, s_split, 0);
+    if constexpr (rt == 3) fw_split<NCT, ACT, 1 - P, 1 - P>(st, a, s_split, 1);
+    if constexpr (rt == 4) fw_gather<NCT, 1 - P>(st, a, g_soff, g_qoff, s_g);
+    a0 = n0;
+    a1 = n1;
+    __builtin_amdgcn_sched_barrier(0);
+  });
+  __syncthreads();
+}
+
+// epilogue unit (row tile RTI, column tile J): scale + bias, H_out piece, the segmented node scan
+// (MAXL rounds, carries between row tiles) and S_out at node ends.  As fk_epi_row (SUMONLY).
+template <int RTI, int J, int NCT, int AACT, int MAXL>
+__device__ __forceinline__ void fw_epi_row(St<NCT>& st, const Args& a, const int4* em, int n, int pc, bool pok,
+                                           const f32x4& bj, f32x4& carry) {
+  if (16 * RTI < n) {
+    const int hc = st.hc;
+    const int4 ri = em[16 * RTI + st.fr];
+    f32x4 o;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[RTI][J][q], st.inv, bj[q]);
+    const bool rok = ri.x >= 0 && pok;
+    if (rok) {
+      reinterpret_cast<f32x4*>(a.O)[(int64_t)ri.x * hc + pc] = o;
+      st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+    }
+    const bool start = (ri.z & fk::kFlagStart) != 0;
+    f32x4 m;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) m[q] = act_t<AACT>(o[q], a.aact, a.aalpha);
+    f32x4 x = m, cin;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) cin[q] = fk::dpp_ror1(carry[q]);
+#pragma unroll
+    for (int it = 0; it < MAXL; ++it) {
+      f32x4 y;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) y[q] = fk::dpp_shr1(cin[q], x[q]);
+      x = start ? m : y + m;
+    }
+    if ((ri.z & fk::kFlagEnd) && rok) {
+      reinterpret_cast<f32x4*>(a.SO)[(int64_t)ri.y * hc + pc] = x;
+      st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+    }
+    carry = x;
+  }
+  if constexpr (RTI + 1 < kRT) fw_epi_row<RTI + 1, J, NCT, AACT, MAXL>(st, a, em, n, pc, pok, bj, carry);
+}
+
+template <int J, int NCT, int AACT, int MAXL>
+__device__ __forceinline__ void fw_epi_col(St<NCT>& st, const Args& a, const int4* em, int n, bool load_next,
+                                           int i_next) {
+  const int pc = 4 * (st.wave + 4 * J) + st.g16;
+  const bool pok = pc < st.hc;
+  f32x4 bj = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (a.bias && pok) bj = *reinterpret_cast<const f32x4*>(st.lbias + 4 * pc);
+  f32x4 carry = f32x4{0.f, 0.f, 0.f, 0.f};
+  fw_epi_row<0, J, NCT, AACT, MAXL>(st, a, em, n, pc, pok, bj, carry);
+  // column tile J is stored: its accumulators take the next tile's residual rows
+  if (load_next) {
+    fw_resid_load(st, a, i_next, J);
+  } else {
+#pragma unroll
+    for (int rt = 0; rt < kRT; ++rt) st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if constexpr (J + 1 < NCT) fw_epi_col<J + 1, NCT, AACT, MAXL>(st, a, em, n, load_next, i_next);
+}
+
+template <int NCT, int ACT, int AACT, int MAXL>
+__device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int tstride, int ntl) {
+  auto tile = [&](int i) __attribute__((always_inline)) { return t0 + (i < ntl ? i : ntl - 1) * tstride; };
+  St<NCT> st;
+  const int tid = threadIdx.x;
+  st.lane = tid & 63;
+  st.wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  st.fr = st.lane & 15;
+  st.g16 = st.lane >> 4;
+  st.grow = 32 * st.wave + (st.lane & 31);
+  st.q = st.lane >> 5;
+  st.hv = a.hv;
+  st.hc = a.h / 4;
+  st.NT = a.NT;
+  st.abuf = smem;
+  st.emap = reinterpret_cast<int4*>(smem + 2 * kBufB);
+  st.lbias = reinterpret_cast<float*>(smem + 2 * kBufB + kEmapB);
+  for (int c = tid; c < a.h; c += kThreads) st.lbias[c] = a.bias ? a.bias[c] : 0.f;
+  st.wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.Wimg, (short)0, (int)fk::image_bytes(a.h), 0x00020000);
+  st.mxH = 0.f;
+  st.mxS = 0.f;
+  {
+    const float bound = a.amax_in[1] + (a.rev ? fk::act_bound(a.amax_in[0], a.act, a.alpha) : 0.f);
+    st.sA = ldexpf(1.f, fk::scale_exp(bound));
+    const float sW = *reinterpret_cast<const float*>(a.Wimg);
+    st.sAW = st.sA * sW;
+    st.inv = 1.f / st.sAW;
+  }
+  const bool resid = a.residual && a.H != nullptr;
+  const bool info_writer = st.q == 0;
+  const int SPT = a.KS;
+
+  // ---- tile info: cur (tile i) and nxt (i + 1) row offsets, raw row of tile i + 2 in flight
+  int2 cur, nxt;
+  int n_cur, n_nxt;
+  int4 raw2;
+  fk::TileHead h2, h3;
+  {
+    const fk::TileHead h0 = fk::tile_head<kRT, true>(a, tile(0));
+    const int4 r0 = fk::row_raw<kRT, true>(a, h0, st.grow);
+    const fk::TileHead h1 = fk::tile_head<kRT, true>(a, tile(1));
+    const int4 r1 = fk::row_raw<kRT, true>(a, h1, st.grow);
+    h2 = fk::tile_head<kRT, true>(a, tile(2));
+    raw2 = fk::row_raw<kRT, true>(a, h2, st.grow);
+    h3 = fk::tile_head<kRT, true>(a, tile(3));
+    const bool v0 = st.grow < h0.n, v1 = st.grow < h1.n;
+    cur = fk::row_offsets(a, r0, v0);
+    nxt = fk::row_offsets(a, r1, v1);
+    if (info_writer) {
+      st.emap[0 * kRows + st.grow] = fk::row_entry(r0, v0);
+      st.emap[1 * kRows + st.grow] = fk::row_entry(r1, v1);
+    }
+    if ((h0.n > kRows || (ntl > 1 && h1.n > kRows)) && tid == 0) atomicOr(&g_pk_timeout, 2u);
+    n_cur = h0.n < kRows ? h0.n : kRows;
+    n_nxt = h1.n < kRows ? h1.n : kRows;
+  }
+#pragma unroll
+  for (int r = 0; r < kRT; ++r)
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) st.acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  __syncthreads();  // emap of tiles 0 and 1, the bias
+  if (resid) {
+#pragma unroll
+    for (int j = 0; j < NCT; ++j) fw_resid_load(st, a, 0, j);
+  }
+  // steps 0 and 1 gathered, W of step 0, step 0 split into buffer 0, step 2 gathered
+  fw_gather<NCT, 0>(st, a, cur.x, cur.y, 0);
+  fw_gather<NCT, 1>(st, a, cur.x, cur.y, 1);
+  fw_load_w<NCT, 0, 0, NCT>(st, 0);
+  fw_split<NCT, ACT, 0, 0>(st, a, 0, 0);
+  fw_split<NCT, ACT, 0, 0>(st, a, 0, 1);
+  fw_gather<NCT, 0>(st, a, cur.x, cur.y, 2 % SPT);
+  __syncthreads();
+
+  for (int i = 0; i < ntl; ++i) {
+    {  // residual rows (loaded by the previous epilogue) into the accumulators' scale
+      const f32x4 s4 = f32x4{st.sAW, st.sAW, st.sAW, st.sAW};
+#pragma unroll
+      for (int rt = 0; rt < kRT; ++rt)
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) st.acc[rt][j] = st.acc[rt][j] * s4;
+    }
+    const int nrt = (n_cur + 15) >> 4;
+    for (int k = 0; k < SPT; k += 2) {
+      // step k (parity 0) and k + 1 (parity 1); W one step ahead (the next tile's step 0 after the
+      // last), split one step ahead, gathers three steps ahead (into the next tile at the end)
+      {
+        const int k3 = k + 3, adv = k3 >= SPT ? 1 : 0;
+        fw_step<NCT, ACT, 0>(st, a, k + 1, k + 1, k3 - adv * SPT, adv ? nxt.x : cur.x, adv ? nxt.y : cur.y, nrt);
+      }
+      {
+        const int k1 = k + 2 < SPT ? k + 2 : 0;
+        const int k3 = k + 4, adv = k3 >= SPT ? 1 : 0;
+        fw_step<NCT, ACT, 1>(st, a, k1, k1, k3 - adv * SPT, adv ? nxt.x : cur.x, adv ? nxt.y : cur.y, nrt);
+      }
+    }
+    const bool more = i + 1 < ntl;
+    const int4* em = st.emap + (i % kEmaps) * kRows;
+    fw_epi_col<0, NCT, AACT, MAXL>(st, a, em, n_cur, resid && more, i + 1);
+    // advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
+    cur = nxt;
+    n_cur = n_nxt;
+    const bool v2 = st.grow < h2.n;
+    nxt = fk::row_offsets(a, raw2, v2);
+    if (info_writer) st.emap[((i + 2) % kEmaps) * kRows + st.grow] = fk::row_entry(raw2, v2);
+    if (h2.n > kRows && i + 2 < ntl && tid == 0) atomicOr(&g_pk_timeout, 2u);
+    n_nxt = h2.n < kRows ? h2.n : kRows;
+    h2 = h3;
+    raw2 = fk::row_raw<kRT, true>(a, h2, st.grow);
+    h3 = fk::tile_head<kRT, true>(a, tile(i + 4));
+  }
+  if (a.amax_out) {
+    const float mh = fk::wave_max(st.mxH), ms = fk::wave_max(st.mxS);
+    if (st.lane == 0) {
+      fk::atomic_max_abs(a.amax_out, mh);
+      fk::atomic_max_abs(a.amax_out + 1, ms);
+    }
+  }
+}
+
+// Fused relu / sum layers, h <= 320 (NT <= 20), tiles of <= 128 rows: waves with ceil(NT / 4)
+// column tiles run fw_run<CTM>, the others (NT % 4 != 0) fw_run<CTM - 1>.
+template <int CTM, int ACT, int AACT, int MAXL>
+__global__ void __launch_bounds__(kThreads, 1) update_fw_kernel(Args a) {
+  __shared__ __attribute__((aligned(16))) char smem[kLdsB];
+  int t0 = (int)blockIdx.x, tstride = (int)gridDim.x, ntl;
+  const int nx = a.nxcd;
+  if (nx > 1 && (int)gridDim.x % nx == 0) {
+    const int x = (int)blockIdx.x % nx, chunk = (a.ntiles + nx - 1) / nx;
+    const int lo = x * chunk, hi = min(a.ntiles, lo + chunk);
+    t0 = lo + (int)blockIdx.x / nx;
+    tstride = (int)gridDim.x / nx;
+    ntl = hi > t0 ? (hi - t0 + tstride - 1) / tstride : 0;
+  } else {
+    ntl = (a.ntiles - t0 + tstride - 1) / tstride;
+  }
+  if (ntl <= 0) return;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int nct = (a.NT - wave + 3) / 4;
+  if constexpr (CTM > 1) {
+    if (nct < CTM) {
+      fw_run<CTM - 1, ACT, AACT, MAXL>(a, smem, t0, tstride, ntl);
+      return;
+    }
+  }
+  fw_run<CTM, ACT, AACT, MAXL>(a, smem, t0, tstride, ntl);
+}
+
+}  // namespace fw
+}  // namespace nt

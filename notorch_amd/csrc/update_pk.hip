@@ -44,6 +44,7 @@ __device__ unsigned long long g_pk_stamps[10];
 // the fp16x3 layer kernel (shares g_pk_timeout: bit 1 = bounded wait gave up, bit 2 = a tile larger
 // than the fk kernel's row capacity)
 #include "update_fk.hpp"
+#include "update_fw.hpp"  // one wave per SIMD variant of the fused layer
 #ifdef NT_DIAG
 #include "update_fk2.hpp"  // A/B: LDS-staged output variant (NT_FK=2)
 #endif
@@ -877,6 +878,41 @@ int launch_fk_nw4(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
                      : launch_fk_nw4_t<NT_ACT_IDENTITY, 16>(a, grid, stream);
 }
 
+// One-wave-per-SIMD walk (update_fw_kernel): fused relu layers with a sum aggregation whose act is
+// relu / identity, 257 <= h <= 320 (five column tiles per wave), tiles of <= 128 rows.
+bool fw_supported(int64_t h, int act, int reduce, int aact) {
+  const int nt = fk::nt_for(h);
+  return act == NT_ACT_RELU && reduce == NT_SUM && (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY) && nt > 16 &&
+         nt <= fw::kMaxNT;
+}
+// A/B switch: NT_FK_FW=1 / 0 (read once per process) selects update_fw_kernel where it applies;
+// nt_debug_set_fw overrides it (tests and kernel benches switch within one process)
+int g_fw_override = -1;
+bool fw_selected() {
+  static const int v = [] {
+    const char* e = getenv("NT_FK_FW");
+    return e && e[0] == '1' ? 1 : 0;
+  }();
+  return (g_fw_override >= 0 ? g_fw_override : v) != 0;
+}
+
+template <int AACT, int MAXL>
+int launch_fw_t(const fk::Args& a, int grid, hipStream_t stream) {
+  fw::update_fw_kernel<5, NT_ACT_RELU, AACT, MAXL><<<grid, fw::kThreads, 0, stream>>>(a);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+int launch_fw(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
+  if (a.aact == NT_ACT_RELU)
+    return maxl <= 3   ? launch_fw_t<NT_ACT_RELU, 3>(a, grid, stream)
+           : maxl <= 8 ? launch_fw_t<NT_ACT_RELU, 8>(a, grid, stream)
+                       : launch_fw_t<NT_ACT_RELU, 16>(a, grid, stream);
+  return maxl <= 3   ? launch_fw_t<NT_ACT_IDENTITY, 3>(a, grid, stream)
+         : maxl <= 8 ? launch_fw_t<NT_ACT_IDENTITY, 8>(a, grid, stream)
+                     : launch_fw_t<NT_ACT_IDENTITY, 16>(a, grid, stream);
+}
+
 // 64-row tiles: every other combination (any reduce, any aggregation act) and h > 384
 template <int CT>
 int launch_fk_narrow(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
@@ -968,6 +1004,10 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
     return launch_fk2(a, grid, u.stream);
   }
 #endif
+  if (fused && fw_selected() && fw_supported(u.h, u.act, reduce, aact)) {
+    a.nchunks = 1;
+    return launch_fw(a, maxl, grid, u.stream);
+  }
   if (fused && tile_rows <= 64 && fk_nw4(u.h, true, u.act, reduce, aact)) {
     a.nchunks = 1;
     const int g4 = a.ntiles < 2 * cu_count() ? a.ntiles : 2 * cu_count();
@@ -1111,26 +1151,13 @@ int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream) {
   return NT_OK;
 }
 
-// Split-scale scratch for the C ABI entry points that carry no amax (nt_dmpnn_update,
-// nt_dmpnn_dense_matmul without amax_in): a ring of (max|H|, max|S|) slots in device memory owned by
-// the library.  Each call takes the next slot (host-side counter), zeroes it on its stream and runs
-// the max passes into it, so calls on different streams get different slots; a slot is reused only
-// after kAmaxRing later calls, long after its layer kernel has read it.
-constexpr int kAmaxRing = 4096;
-__device__ float g_amax_ring[kAmaxRing][2];
-
-int amax_scratch(const float* H, int64_t nh, const float* S, int64_t ns, float** out, hipStream_t stream) {
-  static std::atomic<unsigned> next{0};
-  float* base = nullptr;
-  if (hipGetSymbolAddress((void**)&base, HIP_SYMBOL(g_amax_ring)) != hipSuccess) {
-    set_error("amax scratch: hipGetSymbolAddress failed");
-    return NT_EHIP;
-  }
-  float* slot = base + 2 * (next.fetch_add(1, std::memory_order_relaxed) % kAmaxRing);
-  NT_HIP(hipMemsetAsync(slot, 0, 2 * sizeof(float), stream));
-  int rc = H ? fk_absmax(H, nh, slot, stream) : NT_OK;
-  if (rc == NT_OK && S) rc = fk_absmax(S, ns, slot + 1, stream);
-  *out = slot;
+// Split scales for the C ABI entry points that carry no amax (nt_dmpnn_update, nt_dmpnn_dense_matmul
+// without amax_in): the caller's 2-float device workspace, zeroed and filled on the call's stream, so
+// every use is ordered by the stream like the layer kernel that reads it.
+int amax_fill(float* ws, const float* H, int64_t nh, const float* S, int64_t ns, hipStream_t stream) {
+  NT_HIP(hipMemsetAsync(ws, 0, 2 * sizeof(float), stream));
+  int rc = H ? fk_absmax(H, nh, ws, stream) : NT_OK;
+  if (rc == NT_OK && S) rc = fk_absmax(S, ns, ws + 1, stream);
   return rc;
 }
 
@@ -1146,6 +1173,13 @@ extern "C" __attribute__((visibility("default"))) int nt_debug_fk_stamps(unsigne
   return hipMemcpyToSymbol(HIP_SYMBOL(nt::g_pk_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : 2;
 }
 #endif
+
+// Debug-only (not part of include/notorch_amd.h): select the fp32 fused layer walk (-1: the default,
+// 0: update_fk_kernel, 1: update_fw_kernel where it applies)
+extern "C" __attribute__((visibility("default"))) int nt_debug_set_fw(int v) {
+  nt::g_fw_override = v;
+  return 0;
+}
 
 extern "C" __attribute__((visibility("default"))) int nt_device_status(uint32_t* host_out,
                                                                       void* stream) {

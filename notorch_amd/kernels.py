@@ -411,9 +411,12 @@ def dmpnn_update(
     else:
         _require_feat("out", out, H.dtype)
     lib = _lib.load()
+    # fp32 split scales: a 2-float device workspace owned by the caller (ABI 6), allocated on the
+    # current stream by the caching allocator, so its reuse is stream-ordered
+    ws = torch.empty(2, dtype=torch.float32, device=dev) if code == NT_F32 and h % 4 == 0 else None
     _run(dev, lib.nt_dmpnn_update,
          _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
-         act[0], act[1], code, _ptr(out), _stream(dev))
+         act[0], act[1], code, _ptr(ws), _ptr(out), _stream(dev))
     return out
 
 
@@ -604,7 +607,7 @@ def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None, *, kernel: st
     if code == NT_BF16:
         if h > 512:
             raise ValueError("dense_matmul: bf16 needs h <= 512")
-        _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_BF16, None, _ptr(out),
+        _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_BF16, None, None, _ptr(out),
              _stream(dev))
         return out
     if kernel == "fk":
@@ -615,7 +618,10 @@ def dense_matmul(X: Tensor, Wp: Tensor, out: Tensor | None = None, *, kernel: st
             _require_amax(amax, X.dtype)
     elif kernel != "pk":
         raise ValueError("kernel must be 'fk' or 'pk'")
-    _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_F32, _ptr(amax), _ptr(out),
+    # kernel = "pk" passes no amax: the diagnostic library then runs the bf16x6 kernel, the shipping one
+    # the fk kernel with max|X| written into this caller-owned workspace (ABI 6)
+    ws = torch.empty(2, dtype=torch.float32, device=dev) if amax is None else None
+    _run(dev, _lib.load().nt_dmpnn_dense_matmul, _ptr(X), M, h, _ptr(Wp), NT_F32, _ptr(amax), _ptr(ws), _ptr(out),
          _stream(dev))
     return out
 

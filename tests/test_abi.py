@@ -48,12 +48,19 @@ def test_abi_version_and_errors_without_gpu():
     from notorch_amd import _lib
 
     lib = _lib.load()
-    assert lib.nt_abi_version() == _lib.ABI_VERSION == 5
+    assert lib.nt_abi_version() == _lib.ABI_VERSION == 6
     assert lib.nt_dmpnn_packed_weight_bytes(300, 0) > 0
     assert lib.nt_dmpnn_packed_weight_bytes(0, 0) == 0
     # argument validation happens before any device call: EINVAL + message
-    rc = lib.nt_dmpnn_update(None, None, None, None, None, None, 0, 0, 0, 1, 1, 0.0, 0, None, None)
+    rc = lib.nt_dmpnn_update(None, None, None, None, None, None, 0, 0, 0, 1, 1, 0.0, 0, None, None, None)
     assert rc == 1 and b"bad sizes" in lib.nt_last_error()
+    # ABI 6: the fp32 split-scale workspace is the caller's (no library-owned device scratch); the
+    # check precedes any device call, so fake aligned pointers reach it
+    fake = [ctypes.c_void_p(0x1000 * (i + 1)) for i in range(6)]
+    rc = lib.nt_dmpnn_update(*fake, 4, 8, 16, 1, 1, 0.0, 0, None, ctypes.c_void_p(0x9000), None)
+    assert rc == 1 and b"amax_ws" in lib.nt_last_error()
+    rc = lib.nt_dmpnn_dense_matmul(fake[0], 8, 16, fake[1], 0, None, None, fake[2], None)
+    assert rc == 1 and b"amax_ws" in lib.nt_last_error()
     rc = lib.nt_segment_reduce(None, None, None, 4, 8, 9, 0, 0.0, 0, None, None)
     assert rc == 1 and b"reduce" in lib.nt_last_error()
     rc = lib.nt_segment_reduce(None, None, None, 4, 8, 0, 0, 0.0, 1, None, None)

@@ -1,0 +1,105 @@
+"""A/B of the fp32 fused layer walks on one batch: update_fk_kernel (nt_debug_set_fw(0)) against
+update_fw_kernel (nt_debug_set_fw(1)) on the same 128-row plan -- bit-exact comparison of H_out,
+S_out and the amax chain, then interleaved timings.
+Usage: python tools/fw_check.py [--kind qm9] [--mols 4096] [--h 300] [--rev nodes] [--rounds 5]"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+from notorch_amd import _lib  # noqa: E402
+from notorch_amd import kernels as K  # noqa: E402
+from notorch_amd.data.synth import make_batch  # noqa: E402
+
+
+def timeit(fn, reps=10):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    return statistics.median(ts)
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--kind", default="qm9")
+    p.add_argument("--mols", type=int, default=4096)
+    p.add_argument("--h", type=int, default=300)
+    p.add_argument("--rev", default="nodes")
+    p.add_argument("--rounds", type=int, default=5)
+    p.add_argument("--rows", type=int, default=128)
+    p.add_argument("--agg", default="relu")
+    a = p.parse_args()
+    lib = _lib.load()
+    setfw = getattr(lib, "nt_debug_set_fw")
+    setfw.argtypes = [ctypes.c_int]
+    G = make_batch(a.kind, a.mols, seed=0).collate(a.rev).to("cuda")
+    V, E, h = G.num_nodes, G.num_edges, a.h
+    lay = G._nt_layout
+    gen = torch.Generator(device="cuda").manual_seed(0)
+    H = torch.randn(E, h, device="cuda", generator=gen)
+    S = torch.randn(V, h, device="cuda", generator=gen)
+    W = torch.randn(h, h, device="cuda", generator=gen) / 17
+    b = torch.randn(h, device="cuda", generator=gen)
+    Wp = K.pack_weights(W)
+    src, rev = G.edge_index[0].contiguous(), G.rev_index
+    relu = K.act_code(torch.nn.ReLU())
+    agg = relu if a.agg == "relu" else K.act_code(torch.nn.Identity())
+    amax = torch.zeros(2, device="cuda")
+    K.absmax(H, amax[0:1])
+    K.absmax(S, amax[1:2])
+    deg = int((lay.dst_ptr[1:] - lay.dst_ptr[:-1]).max().item())
+    plan = K.tile_plan(lay.dst_ptr, E, deg, rows=a.rows, ncu=K.PLAN_NCU)
+    rt = K.dmpnn_row_table(lay.dst_perm, plan[2], src, rev, V)
+    plan64 = K.tile_plan(lay.dst_ptr, E, deg, rows=64, ncu=K.PLAN_NCU)
+    rt64 = K.dmpnn_row_table(lay.dst_perm, plan64[2], src, rev, V)
+    outs = {}
+
+    def run(v, out, S2, am):
+        pl, rtab, rows = (plan64, rt64, 64) if v == 2 else (plan, rt, a.rows)
+
+        def f():
+            setfw(1 if v == 1 else 0)
+            K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=pl, tile_rows=rows, max_in_degree=deg,
+                                 perm=lay.dst_perm, agg_act=agg, amax_in=amax, amax_out=am, row_table=rtab, out=out,
+                                 S_out=S2)
+        return f
+
+    fns = {}
+    for v in (0, 1, 2):
+        out, S2, am = torch.full_like(H, float("nan")), torch.full_like(S, float("nan")), torch.zeros(2, device="cuda")
+        outs[v] = (out, S2, am)
+        fns[v] = run(v, out, S2, am)
+        fns[v]()
+    torch.cuda.synchronize()
+    st = K.device_status() if hasattr(K, "device_status") else None
+    print(f"{a.kind}-{a.mols} rev={a.rev} V={V} E={E} h={h} deg={deg} tiles={plan[1]} status={st}")
+    (o0, s0, m0), (o1, s1, m1) = outs[0], outs[1]
+    eqH, eqS, eqM = torch.equal(o0, o1), torch.equal(s0, s1), torch.equal(m0, m1)
+    dH = (o0 - o1).abs().max().item() / o0.abs().max().item()
+    dS = (s0 - s1).abs().max().item() / s0.abs().max().item()
+    print(f"bit-exact H {eqH} S {eqS} amax {eqM}  (norm max diff H {dH:.3e} S {dS:.3e}; nan {o1.isnan().sum().item()})")
+    o2, s2, m2 = outs[2]
+    print(f"fk 64-row walk bit-exact vs 128-row: H {torch.equal(o0, o2)} S {torch.equal(s0, s2)}")
+    res = {0: [], 1: [], 2: []}
+    for _ in range(a.rounds):
+        for v in (0, 1, 2):
+            res[v].append(timeit(fns[v]))
+    for v, name in ((0, "fk128"), (1, "fw128"), (2, "fk64")):
+        med = statistics.median(res[v])
+        print(f"{name}: median {med:7.1f} us  {2 * E * h * h / (med * 1e-6) / 1e12:6.1f} TF/s fp32-equivalent")
+    setfw(-1)
+    if not (eqH and eqS and eqM):
+        sys.exit(3)
+
+
+if __name__ == "__main__":
+    main()
