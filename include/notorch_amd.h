@@ -64,6 +64,11 @@ NT_API int nt_abi_version(void);
 /* Message of the last failed call on this thread ("" if none). */
 NT_API const char* nt_last_error(void);
 
+/* Which layer-kernel variant the last nt_dmpnn_update / nt_dmpnn_update_fused / nt_dmpnn_dense_matmul
+ * call on this thread launched (a static string, e.g. "update_fw_kernel: one 4-wave workgroup per CU,
+ * 128-row tiles"; "" before any such call).  For reports and bench labels only. */
+NT_API const char* nt_last_kernel(void);
+
 /*
  * GraphEmbedding (notorch/nn/gnn/embed.py:11-36), one sum-mode nn.EmbeddingBag (embed.py:21-22,29):
  *   out[i] = sum_{j < k} table[idx[i * k + j]]          (ascending j, fp32 accumulation)

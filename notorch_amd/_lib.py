@@ -51,6 +51,7 @@ _c_int, _c_i64, _c_f32, _c_size, _vp = (
 SIGNATURES: dict[str, tuple] = {
     "nt_abi_version": (_c_int, []),
     "nt_last_error": (ctypes.c_char_p, []),
+    "nt_last_kernel": (ctypes.c_char_p, []),
     "nt_embed_bag": (_c_int, [_vp, _c_i64, _vp, _c_i64, _c_i64, _c_i64, _c_int, _vp, _vp]),
     "nt_dmpnn_init_embed": (
         _c_int,

@@ -537,6 +537,7 @@ int launch_upd(const void* H, const void* S, const int64_t* src, const int64_t* 
     NT_HIP(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, lds));
   const int64_t slots = 2 * (int64_t)cu_count();  // two resident workgroups per CU (LDS-bound)
   const int64_t g = grid < slots ? grid : slots;
+  set_last_kernel("update_bf16_kernel: two 4-wave workgroups per CU, 64-edge tiles");
   kern<<<(unsigned)g, kThreads, lds, stream>>>(
       (const bf16_t*)H, (const bf16_t*)S, src, rev, (const uint4*)Wp, (const bf16_t*)b, V, E, (int)h,
       KS, NTn, residual, act, alpha, (bf16_t*)H_out, agg, (int)grid, xcd_count());

@@ -15,6 +15,8 @@ namespace nt {
 // ---- error plumbing (thread-local last error, returned through nt_last_error) ----
 void set_error(const std::string& msg);
 void clear_error();
+// record the layer kernel variant a call launched (a static string), read by nt_last_kernel
+void set_last_kernel(const char* name);
 
 #define NT_REQUIRE(cond, code, msg)                      \
   do {                                                   \

@@ -63,6 +63,7 @@ int amax_fill(float* ws, const float* H, int64_t nh, const float* S, int64_t ns,
 // bf16 storage on the same skeleton (PREC = 1): h % 8 == 0, h <= 512, tiles of <= 128 rows, Wimg =
 // the bf16 fragment image; S_out / the row table exactly with a tile plan
 bool fkb_supported(int64_t h);
+int bf16_kernel_env();  // NT_BF16_KERNEL, read once: 0 default, 1 fk, 2 fk4
 int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* tile_ptr, int64_t ntiles,
                           int tile_rows, int max_in_degree, const void* row_table, int reduce, int aact,
                           float aalpha, void* S_out);

@@ -499,6 +499,7 @@ static int dispatch_cpw(const float* H, const float* S, const int64_t* src, cons
                         const float4* Wp, const float* b, int64_t V, int64_t E, int h,
                         const UpdateGeom& g, int residual, int act, float alpha, float* H_out,
                         bool vec, hipStream_t stream) {
+  set_last_kernel("update_f32_tile_kernel: exact fp32 MFMA tiles (h % 4 != 0)");
 #define NT_CASE(C)                                                                          \
   case C:                                                                                   \
     return dispatch_act_vec<BM, C>(H, S, src, rev, Wp, b, V, E, h, g, residual, act, alpha, \
@@ -551,11 +552,8 @@ static size_t as_part_bytes(int64_t) { return 0; }
 
 static size_t fk_offset(int64_t h) { return f32_image_bytes(h) + x6_part_bytes(h) + as_part_bytes(h); }
 
-// bf16 layer kernel: the fk skeleton (NT_BF16_KERNEL=fk) or the 64-row bf16 kernel (default), read per call
-static bool bf16_fk(int64_t h) {
-  const char* e = getenv("NT_BF16_KERNEL");
-  return e && e[0] == 'f' && nt::fkb_supported(h);
-}
+// bf16 layer kernel: the fk skeleton (NT_BF16_KERNEL=fk / fk4, read once) or the 64-row bf16 kernel
+static bool bf16_fk(int64_t h) { return nt::bf16_kernel_env() != 0 && nt::fkb_supported(h); }
 
 extern "C" size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype) {
   if (h <= 0) return 0;
@@ -620,8 +618,7 @@ extern "C" int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h
 extern "C" int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, int agg_act) {
   if (h <= 0) return 0;
   if (dtype == NT_BF16) {
-    const char* e = getenv("NT_BF16_KERNEL");
-    return bf16_fk(h) && strncmp(e, "fk4", 3) != 0 ? 128 : 64;  // fk4 (A/B): 64-row tiles, two workgroups per CU
+    return bf16_fk(h) && nt::bf16_kernel_env() != 2 ? 128 : 64;  // fk4 (A/B): 64-row tiles, two workgroups per CU
   }
   return nt::fk_tile_rows(h, act, reduce, agg_act, true);
 }

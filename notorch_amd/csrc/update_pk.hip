@@ -743,6 +743,8 @@ namespace nt {
 namespace {
 template <int RT, int CT, int ACT, int AACT, bool SUMONLY, int MAXL>
 int launch_fk_t(const fk::Args& a, int grid, hipStream_t stream) {
+  set_last_kernel(RT == 8 ? "update_fk_kernel: one 8-wave workgroup per CU, 128-row tiles"
+                          : "update_fk_kernel: one 8-wave workgroup per CU, 64-row tiles");
   fk::update_fk_kernel<RT, CT, ACT, AACT, SUMONLY, MAXL><<<grid, fk::kThreads, 0, stream>>>(a);
   NT_LAUNCH_CHECK();
   return NT_OK;
@@ -851,18 +853,23 @@ bool fk2_selected(int64_t h) {
 // 128-row walk on small batches (config 2: 115 vs 125 us), slower on large ones (qm9-32k: 905 vs
 // 894, polymer-16: 720 vs 691): the caller picks the plan rows (_engine.NW4_MAX_EDGES).
 // NT_FK_NW=8 turns it off, NT_FK_NW=4 makes it the tile capacity (tests).
+// NT_FK_NW (A/B, read once per process): 8 = never the two-workgroup walk, 4 = always its 64-row plans
+int fk_nw_env() {
+  static const int v = [] {
+    const char* e = getenv("NT_FK_NW");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
 bool fk_nw4(int64_t h, bool fused, int act, int reduce, int aact) {
-  const char* e = getenv("NT_FK_NW");
-  return !(e && atoi(e) == 8) && fused && act == NT_ACT_RELU && reduce == NT_SUM &&
+  return fk_nw_env() != 8 && fused && act == NT_ACT_RELU && reduce == NT_SUM &&
          (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY) && fk::nt_for(h) <= 20;
 }
-bool fk_nw4_forced() {
-  const char* e = getenv("NT_FK_NW");
-  return e && atoi(e) == 4;
-}
+bool fk_nw4_forced() { return fk_nw_env() == 4; }
 
 template <int AACT, int MAXL>
 int launch_fk_nw4_t(const fk::Args& a, int grid, hipStream_t stream) {
+  set_last_kernel("update_fk_kernel: two 4-wave workgroups per CU, 64-row tiles");
   fk::update_fk_kernel<4, 5, NT_ACT_RELU, AACT, true, MAXL, 2, 0, 0, 4><<<grid, 256, 0, stream>>>(a);
   NT_LAUNCH_CHECK();
   return NT_OK;
@@ -898,6 +905,7 @@ bool fw_selected() {
 
 template <int AACT, int MAXL>
 int launch_fw_t(const fk::Args& a, int grid, hipStream_t stream) {
+  set_last_kernel("update_fw_kernel: one 4-wave workgroup per CU (one wave per SIMD), 128-row tiles");
   fw::update_fw_kernel<5, NT_ACT_RELU, AACT, MAXL><<<grid, fw::kThreads, 0, stream>>>(a);
   NT_LAUNCH_CHECK();
   return NT_OK;
@@ -989,10 +997,18 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   a.SO = S_out;
   a.nxcd = xcd_count();
   {
-    const char* e = getenv("NT_FK_STAGGER");  // timing experiments only
-    a.stagger = e ? atoi(e) : 0;
-    const char* r = getenv("NT_FK_RTABL");  // FK_RTABL builds only (timing ablations)
-    a.rtabl = r ? atoi(r) : 0;
+    // timing experiments only, read once per process: NT_FK_STAGGER (start delay of half the grid),
+    // NT_FK_RTABL (FK_RTABL builds: ablations)
+    static const int stagger = [] {
+      const char* e = getenv("NT_FK_STAGGER");
+      return e ? atoi(e) : 0;
+    }();
+    static const int rtabl = [] {
+      const char* e = getenv("NT_FK_RTABL");
+      return e ? atoi(e) : 0;
+    }();
+    a.stagger = stagger;
+    a.rtabl = rtabl;
   }
   a.ntiles = fused ? (int)ntiles : (int)((u.E + cap - 1) / cap);
   if (a.ntiles == 0) return NT_OK;
@@ -1033,6 +1049,7 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
 namespace {
 template <int ACT, int AACT, bool SUMONLY, int MAXL>
 int launch_fkb_t(const fk::Args& a, int grid, hipStream_t stream) {
+  set_last_kernel("update_fk_kernel (bf16): one 8-wave workgroup per CU, 128-row tiles");
   fk::update_fk_kernel<8, 4, ACT, AACT, SUMONLY, MAXL, 2, 0, 1><<<grid, fk::kThreads, 0, stream>>>(a);
   NT_LAUNCH_CHECK();
   return NT_OK;
@@ -1041,6 +1058,7 @@ int launch_fkb_t(const fk::Args& a, int grid, hipStream_t stream) {
 // per wave (h <= 512), the bias in LDS
 template <int AACT, int MAXL>
 int launch_fkb4_t(const fk::Args& a, int grid, hipStream_t stream) {
+  set_last_kernel("update_fk_kernel (bf16): two 4-wave workgroups per CU, 64-row tiles");
   fk::update_fk_kernel<4, 8, NT_ACT_RELU, AACT, true, MAXL, 2, 0, 1, 4><<<grid, 256, 0, stream>>>(a);
   NT_LAUNCH_CHECK();
   return NT_OK;
@@ -1048,6 +1066,17 @@ int launch_fkb4_t(const fk::Args& a, int grid, hipStream_t stream) {
 }  // namespace
 
 bool fkb_supported(int64_t h) { return h % 8 == 0 && h >= 8 && h <= 512; }
+
+// NT_BF16_KERNEL (A/B, read once per process): 0 = the 64-row bf16 kernel (default), 1 = "fk" (the
+// fk skeleton, 128-row tiles), 2 = "fk4" (its two-workgroup 64-row walk)
+int bf16_kernel_env() {
+  static const int v = [] {
+    const char* e = getenv("NT_BF16_KERNEL");
+    if (!(e && e[0] == 'f' && e[1] == 'k')) return 0;
+    return e[2] == '4' ? 2 : 1;
+  }();
+  return v;
+}
 
 int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* tile_ptr, int64_t ntiles,
                           int tile_rows, int max_in_degree, const void* row_table, int reduce, int aact,
@@ -1101,8 +1130,7 @@ int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* 
   }
   const int maxl = max_in_degree - 1;
   {
-    const char* e = getenv("NT_BF16_KERNEL");
-    if (e && e[0] == 'f' && e[1] == 'k' && e[2] == '4' && tile_rows <= 64 && relu && reduce == NT_SUM &&
+    if (bf16_kernel_env() == 2 && tile_rows <= 64 && relu && reduce == NT_SUM &&
         (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY)) {
       const int g4 = a.ntiles < 2 * cu_count() ? a.ntiles : 2 * cu_count();
       if (aact == NT_ACT_RELU)

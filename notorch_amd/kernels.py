@@ -330,15 +330,23 @@ def dmpnn_init_chunked(
     """(H0, S) = dmpnn_init with layer 0's aggregation over the chunk plan of a hub graph (fp32,
     plan = chunk_plan(seg_ptr)): H0 written once, S combined from per-chunk partials.  amax (2
     zero-filled device floats, optional) raised to max|H0|, max|S|."""
-    dev = _require_device(Xv, Xe, src, seg_ptr, perm, amax)
+    chunk_pos, nchunks, chunk_ptr = plan
+    dev = _require_device(Xv, Xe, src, seg_ptr, perm, chunk_pos, chunk_ptr, amax)
     if Xv.dtype != torch.float32 or Xe.dtype != torch.float32:
         raise ValueError("dmpnn_init_chunked is fp32 only")
     _require_amax(amax, Xv.dtype)
+    _require_i64("src", src)
+    for name, t in (("seg_ptr", seg_ptr), ("perm", perm), ("chunk_pos", chunk_pos), ("chunk_ptr", chunk_ptr)):
+        if t.dtype != torch.int32:
+            raise TypeError(f"{name} must be int32")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
     V, h = Xv.shape
     E = Xe.shape[0]
     if Xe.shape[1] != h or src.numel() != E or perm.numel() != E or seg_ptr.numel() != V + 1:
         raise ValueError("shape mismatch between Xv, Xe, src and the dst CSR")
-    chunk_pos, nchunks, chunk_ptr = plan
+    if chunk_pos.numel() != nchunks + 1 or chunk_ptr.numel() != V + 1:
+        raise ValueError("plan must be chunk_plan(seg_ptr): chunk_pos[nchunks + 1], chunk_ptr[V + 1]")
     H0 = torch.empty(E, h, dtype=torch.float32, device=dev)
     S = torch.empty(V, h, dtype=torch.float32, device=dev)
     partial = torch.empty(max(nchunks, 1), h, dtype=torch.float32, device=dev)

@@ -36,12 +36,14 @@ and run autograd (``_torch_block``).
 from __future__ import annotations
 
 import os
+import threading
 import weakref
 from typing import Optional, Sequence
 
 import torch
 from torch import Tensor
 
+from notorch_amd import _lib
 from notorch_amd import kernels as K
 from notorch_amd._lib import NT_ACT_IDENTITY
 from notorch_amd.data.models.graph import DeviceLayout
@@ -59,25 +61,22 @@ LAST_UPDATE_INFO: dict = {}
 
 
 def _note_update(kind: str, dtype: torch.dtype, h: int, rows: int = 0) -> None:
+    """Record which layer kernel the forward ran (bench labels): the variant is the library's own
+    report of its last launch (nt_last_kernel), so the label cannot drift from the dispatch."""
     kp, np_ = 32 * ((h + 31) // 32), 16 * ((h + 15) // 16)
+    launched = _lib.load().nt_last_kernel().decode()
+    short = launched.split(" ")[0].rstrip(":") or "update"
     if dtype == torch.bfloat16:
-        info = dict(kernel="update_bf16_kernel (64-edge tiles, bf16 16x16x32 MFMA, fp32 accumulate)",
-                    kernel_short="update_bf16", numerics="bf16 storage, bf16 MFMA, fp32 accumulate",
-                    products=1)
-    elif kind in ("fused", "persistent"):
-        rows = rows or (128 if h <= 384 else 64)
-        tail = ("aggregation of the next layer fused" if kind == "fused"
-                else "no tile plan: hub graph, aggregation by the chunked segment reduce")
-        walk = ("two 4-wave workgroups per CU" if kind == "fused" and rows == 64 and h <= 320
-                else "one 8-wave workgroup per CU")
-        info = dict(kernel=f"update_fk_kernel (persistent, {walk}, {rows}-row node-aligned tiles, two-part fp16 "
-                           f"split on 16x16x32 fp16 MFMA, {tail})", kernel_short="update_fk",
-                    numerics="fp32 via scaled two-part fp16 split (3 fp16 MFMA products, fp32 accumulate)",
+        info = dict(numerics="bf16 storage, bf16 MFMA, fp32 accumulate", products=1)
+    elif short in ("update_fk_kernel", "update_fw_kernel"):
+        info = dict(numerics="fp32 via scaled two-part fp16 split (3 fp16 MFMA products, fp32 accumulate)",
                     products=3)
     else:
-        info = dict(kernel="nt_dmpnn_update (unfused fp32 update kernel)", kernel_short="update",
-                    numerics="fp32 via bf16x6 split", products=6)
-    info.update(fused=kind == "fused", kpad=kp, npad=np_)
+        info = dict(numerics="exact fp32 MFMA", products=1)
+    tail = {"fused": "aggregation of the next layer fused",
+            "persistent": "no tile plan: hub graph, aggregation by the chunked segment reduce"}.get(kind, "unfused")
+    info.update(kernel=f"{launched} ({tail})", kernel_short=short.replace("_kernel", ""),
+                fused=kind == "fused", kpad=kp, npad=np_, rows=rows)
     LAST_UPDATE_INFO.clear()
     LAST_UPDATE_INFO.update(info)
 
@@ -325,6 +324,7 @@ NW4_MAX_EDGES = 131072
 # zeroed all at once every _AMAX_RING forwards instead of one fill kernel per forward
 _AMAX_RING = 64
 _amax_rings: dict = {}
+_amax_lock = threading.Lock()
 
 
 def _amax_buffer(d: int, X: Tensor, reuse: bool = False) -> Optional[Tensor]:
@@ -339,13 +339,14 @@ def _amax_buffer(d: int, X: Tensor, reuse: bool = False) -> Optional[Tensor]:
     if not reuse or torch.cuda.is_current_stream_capturing():
         return torch.zeros(d + 1, 2, dtype=torch.float32, device=X.device)
     key = (X.device, torch.cuda.current_stream(X.device).cuda_stream, d)
-    ent = _amax_rings.get(key)
-    if ent is None:
-        ent = _amax_rings[key] = [torch.empty(_AMAX_RING, d + 1, 2, dtype=torch.float32, device=X.device), 0]
-    buf, i = ent
-    if i == 0:
-        buf.zero_()
-    ent[1] = (i + 1) % _AMAX_RING
+    with _amax_lock:  # threads sharing a stream take distinct slots; the wrap-time zeroing is enqueued once
+        ent = _amax_rings.get(key)
+        if ent is None:
+            ent = _amax_rings[key] = [torch.empty(_AMAX_RING, d + 1, 2, dtype=torch.float32, device=X.device), 0]
+        buf, i = ent
+        if i == 0:
+            buf.zero_()
+        ent[1] = (i + 1) % _AMAX_RING
     return buf[i]
 
 
@@ -425,7 +426,6 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
     # without its aggregation (a separate segment reduce)
     persistent = fusable and fp32
     timer = UPDATE_EVENTS
-    _note_update("persistent" if persistent else "unfused", H.dtype, h)
     for l in range(d):
         if keep_states:  # the amax row is valid where the persistent kernel keeps the chain
             states.append((H, S, amax[l] if amax is not None and ((persistent and drop is None) or l == 0)
@@ -446,6 +446,8 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
         if timer is not None:
             ev[1].record()
             timer.append(ev)
+        if l == 0:
+            _note_update("persistent" if persistent else "unfused", H.dtype, h)
         if l < d - 1:
             S = _aggregate(Hn, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks,
                            out=None if keep_states else S, amax=amax[l + 1, 1:2] if persistent else None)
@@ -482,7 +484,6 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
     timer = UPDATE_EVENTS
     maxdeg = fused_max_in_degree(lay)
     hubs = hub_info(lay)
-    _note_update("fused", H.dtype, H.shape[1], rows)
     for l in range(d):
         last = l == d - 1
         if keep_states:
@@ -505,6 +506,8 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
             K.hub_aggregate(Hn, lay.dst_perm, lay.dst_ptr, hubs[0], Sn, reduce=reduce,
                             act=_IDENTITY if last else act,
                             amax=None if (amax is None or last) else amax[l + 1, 1:2])
+        if l == 0:
+            _note_update("fused", H.dtype, H.shape[1], rows)
         if not keep_states:
             spare_H = H
             spare_S = S

@@ -18,7 +18,7 @@ def header_functions():
 def test_header_declares_the_boundary():
     names = header_functions()
     assert set(names) == {
-        "nt_abi_version", "nt_last_error", "nt_csr_workspace_bytes", "nt_csr_build", "nt_dropout_residual",
+        "nt_abi_version", "nt_last_error", "nt_last_kernel", "nt_csr_workspace_bytes", "nt_csr_build", "nt_dropout_residual",
         "nt_dmpnn_init", "nt_segment_reduce", "nt_dmpnn_packed_weight_bytes",
         "nt_dmpnn_pack_weight", "nt_dmpnn_update", "nt_dmpnn_tile_count", "nt_dmpnn_tile_plan",
         "nt_dmpnn_update_fused", "nt_dmpnn_message", "nt_dmpnn_edge_backward", "nt_gather_rows",
@@ -49,6 +49,7 @@ def test_abi_version_and_errors_without_gpu():
 
     lib = _lib.load()
     assert lib.nt_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.nt_last_kernel() == b""  # no layer call yet on this thread
     assert lib.nt_dmpnn_packed_weight_bytes(300, 0) > 0
     assert lib.nt_dmpnn_packed_weight_bytes(0, 0) == 0
     # argument validation happens before any device call: EINVAL + message
