@@ -12,8 +12,9 @@
 // bound at 2^14: the A rows by s_A (from amax_in = max|H|, max|S| of the inputs, written by the
 // kernels that produced them), W by s_W (stored in the image header by the pack kernel).  Three
 // v_mfma_f32_16x16x32_f16 products per k-step, W1 A0 + W0 A1 + W0 A0, accumulate in fp32; the
-// dropped W1 A1 term and the two split roundings are ~2^-22 relative, i.e. the result is as close to
-// fp64 as an fp32 GEMM's (3.5e-7 normalised at config 2).  Half the MFMA work of a bf16x6 split and
+// dropped W1 A1 term and the two split roundings are ~2^-22 relative: 8.6e-7 normalised from fp64 at
+// config 2, 2.7x the fp32 CPU oracle's 3.2e-7 (tests/test_gpu_numerics.py).  The scale is per tensor:
+// rows far below the tensor's max (< 1e-4 of it) lose the low part to fp16 subnormals.  Half the MFMA work of a bf16x6 split and
 // two thirds of its operand bytes.  The residual row enters the accumulator scaled by s_A s_W while
 // the K loop runs; the epilogue multiplies by the exact inverse and adds the bias.
 //

@@ -160,6 +160,54 @@ def test_block_bf16_config3_shape():
     _block_case("zinc", 4096, 512, 5)
 
 
+# The bf16 forward's sharper criterion (the one the bf16 backward uses, test_gpu_bf16_backward.py):
+# against fp64 truth evaluated on the same bf16-valued inputs and weights, the device block + readout
+# is no further than BF16_FACTOR x PyTorch's own bf16 evaluation of the same restatement
+# (oracle/dmpnn_ref.py, chemprop.py:81-88, residual.py:27-28, agg.py:27) run with torch ops in bf16
+# on the same device, on the normalised max error and on the relative L2 error.
+BF16_FACTOR = 2.0
+
+
+def _rel_l2(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / b.norm().clamp_min(1e-300)).item()
+
+
+def test_block_bf16_config3_no_further_from_fp64_than_torch_bf16():
+    from notorch_amd.nn import ChempropBlock, Sum
+
+    h, depth = 512, 5
+    G = _graph("zinc", 4096, seed=0)
+    torch.manual_seed(0)
+    emb_v = nn.EmbeddingBag(42, h, mode="sum")
+    emb_e = nn.EmbeddingBag(13, h, mode="sum")
+    with torch.no_grad():
+        Xv, Xe = emb_v(G.node_feats).to(BF), emb_e(G.edge_feats).to(BF)
+    blk = ChempropBlock(hidden_dim=h, depth=depth).eval().to(BF)
+    Ws, bs = dmpnn_ref.block_params(blk)
+    ei, rev, bni = G.edge_index.to(DEV), G.rev_index.to(DEV), G.batch_node_index.to(DEV)
+
+    def restated(dtype):
+        with torch.inference_mode():
+            n, e = dmpnn_ref.chemprop_block(Xv.to(DEV, dtype), Xe.to(DEV, dtype), ei, rev,
+                                            [W.to(DEV, dtype) for W in Ws], [b.to(DEV, dtype) for b in bs])
+            return e, n, dmpnn_ref.readout(n, bni, len(G), "sum")
+
+    truth = restated(torch.float64)
+    torch_bf16 = restated(BF)
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
+    with torch.no_grad():
+        out_G = blk.to(DEV)(Gd)
+        dev = (out_G.edge_feats, out_G.node_feats, Sum()(out_G))
+    for what, d, t, ref in zip(("edge", "node", "readout"), dev, torch_bf16, truth):
+        e_dev, e_t = norm_err(d, ref), norm_err(t, ref)
+        l_dev, l_t = _rel_l2(d, ref), _rel_l2(t, ref)
+        print(f"config 3 {what}: device vs fp64 max {e_dev:.3e} L2 {l_dev:.3e}; torch bf16 vs fp64 max {e_t:.3e} "
+              f"L2 {l_t:.3e}")
+        assert e_dev <= BF16_FACTOR * e_t, f"{what}: max err {e_dev:.3e} > {BF16_FACTOR} x torch bf16 {e_t:.3e}"
+        assert l_dev <= BF16_FACTOR * l_t, f"{what}: L2 err {l_dev:.3e} > {BF16_FACTOR} x torch bf16 {l_t:.3e}"
+
+
 @pytest.mark.parametrize("opts", [dict(), dict(residual=False), dict(bias=False), dict(reduce="mean"),
                                   dict(act=nn.SiLU), dict(shared=True)])
 def test_block_bf16_options(opts):

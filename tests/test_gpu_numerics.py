@@ -24,8 +24,12 @@ DEV = "cuda"
 # config 2 (round 4): edge 8.6e-7 vs the fp32 CPU oracle's 3.2e-7 (2.7x).  The device may be up to
 # this factor further from fp64 than the fp32 CPU oracle, and must stay inside the 1e-5 contract.
 KFP32 = 4.0
-# per-row relative error bound for rows 1e4 below the tensor's max (fp32 contract per row)
-ROW_TOL = 1e-5
+# per-row relative error bound by how far a row sits below the tensor's max.  The split scale is per
+# tensor (s_A from max|A|): a row 1e-k below the max has its low fp16 part 2^-11 x 1e-k x 2^14 in
+# scaled units, which falls into fp16's subnormal range (< 2^-14) once k > ~4, so per-row fp32
+# accuracy holds down to 1e-4 of the tensor max and degrades below it towards the one-part fp16
+# floor 2^-11; the normalised fp32 contract (1e-5 of the tensor max) holds throughout.
+ROW_TOL = {1e-3: 1e-5, 1e-4: 1e-5, 1e-6: 1e-4, 1e-8: 2.0 ** -10}
 
 
 def _K():
@@ -94,7 +98,7 @@ def _row_rel_err(out, ref):
     return (num[keep] / den[keep])
 
 
-@pytest.mark.parametrize("small", [1e-4, 1e-3])
+@pytest.mark.parametrize("small", [1e-3, 1e-4, 1e-6, 1e-8])
 def test_mixed_magnitude_rows_per_row_error(small):
     """Every other molecule's feature rows scaled by `small` (fixed rev mode, so a row's src / rev
     partners belong to its own molecule): one launch with one per-tensor split scale; the per-row
@@ -131,8 +135,10 @@ def test_mixed_magnitude_rows_per_row_error(small):
     print(f"rows x{small:g}: H_out per-row rel err max {eH[~big_e].max():.3e} (unit rows {eH[big_e].max():.3e}); "
           f"S_out {eS_small.max():.3e} (unit rows {eS_big.max():.3e})")
     assert_parity(Hn, rH, FP32_NORM_TOL, "H (normalised)")
-    assert eH.max().item() <= ROW_TOL, f"H_out per-row relative error {eH.max():.3e}"
-    assert eS.max().item() <= ROW_TOL, f"S_out per-row relative error {eS.max():.3e}"
+    assert_parity(Sn, rS, FP32_NORM_TOL, "S (normalised)")
+    assert eH[big_e].max().item() <= 1e-5, f"unit rows: H_out per-row relative error {eH[big_e].max():.3e}"
+    assert eH.max().item() <= ROW_TOL[small], f"H_out per-row relative error {eH.max():.3e}"
+    assert eS.max().item() <= ROW_TOL[small], f"S_out per-row relative error {eS.max():.3e}"
 
 
 def test_extreme_magnitude_operands_stay_finite():
