@@ -64,6 +64,8 @@ int amax_fill(float* ws, const float* H, int64_t nh, const float* S, int64_t ns,
 // the bf16 fragment image; S_out / the row table exactly with a tile plan
 bool fkb_supported(int64_t h);
 int bf16_kernel_env();  // NT_BF16_KERNEL, read once: 0 default, 1 fk, 2 fk4
+// the one-wave-per-SIMD fused walk (update_fw_kernel) takes this fused layer (128-row plans)
+bool fw_active(int64_t h, int dtype, int act, int reduce, int aact);
 int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* tile_ptr, int64_t ntiles,
                           int tile_rows, int max_in_degree, const void* row_table, int reduce, int aact,
                           float aalpha, void* S_out);

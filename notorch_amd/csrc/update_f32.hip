@@ -618,6 +618,7 @@ extern "C" int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h
 extern "C" int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, int agg_act) {
   if (h <= 0) return 0;
   if (dtype == NT_BF16) {
+    if (nt::fw_active(h, NT_BF16, act, reduce, agg_act)) return 128;
     return bf16_fk(h) && nt::bf16_kernel_env() != 2 ? 128 : 64;  // fk4 (A/B): 64-row tiles, two workgroups per CU
   }
   return nt::fk_tile_rows(h, act, reduce, agg_act, true);
@@ -736,8 +737,10 @@ extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t
                  (b == nullptr || aligned16(b)) && (S_out == nullptr || aligned16(S_out)),
              NT_EINVAL, "feature pointers must be 16-byte aligned");
   if (dtype == NT_BF16) {
-    // the fk skeleton (128-row tiles) when the plan comes with its row table, else the 64-row kernel
-    if (bf16_fk(h) && (tile_ptr == nullptr || row_table != nullptr)) {
+    // the fk skeleton (128-row tiles) when the plan comes with its row table, else the 64-row kernel;
+    // the one-wave-per-SIMD walk for fused relu / sum layers whose plan has a row table
+    const bool fwb = tile_ptr != nullptr && row_table != nullptr && fw_active(h, NT_BF16, act, reduce, agg_act);
+    if ((bf16_fk(h) || fwb) && (tile_ptr == nullptr || row_table != nullptr)) {
       NT_REQUIRE(row_table == nullptr || aligned16(row_table), NT_EINVAL, "row_table must be 16-byte aligned");
       UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
                    0, 0, residual, act, act_alpha, (float*)H_out, as_stream(stream_)};

@@ -31,6 +31,23 @@
 
 #include "update_fk.hpp"
 
+#ifndef FW_ONE_PATH
+#define FW_ONE_PATH 0
+#endif
+#ifndef FW_EPI_FENCE
+#define FW_EPI_FENCE 0
+#endif
+// FW_STAMP (A/B builds): s_memtime sums per wave into g_pk_stamps: [0] K loops, [1] epilogues,
+// [2] first step pair of each tile (the tile-start wait), [3] tiles, [4] waves, [5] whole walk
+#ifndef FW_STAMP
+#define FW_STAMP 0
+#endif
+// FW_ABL (A/B builds, timing ablations, results invalid): Args::rtabl bits (NT_FK_RTABL) -- 1 gathers
+// read row 0, 4 no H_out / S_out stores, 8 residual rows read row 0, 32 no aggregation scan
+#ifndef FW_ABL
+#define FW_ABL 0
+#endif
+
 namespace nt {
 namespace fw {
 
@@ -42,20 +59,24 @@ using fk::f32x4;
 constexpr int kThreads = 256;
 constexpr int kRT = 8;                // row tiles per tile
 constexpr int kRows = 16 * kRT;       // 128
-constexpr int kPartB = kRT * 1024;    // one fp16 part of a k-slice (8 KiB)
-constexpr int kBufB = 2 * kPartB;     // both parts
+constexpr int kPartB = kRT * 1024;    // one fp16 / bf16 part of a k-slice (8 KiB)
 constexpr int kEmaps = 4;             // row-info buffers (tile index mod 4)
 constexpr int kEmapB = kEmaps * kRows * 16;
-constexpr int kBiasB = 320 * 4;
-constexpr int kMaxNT = 20;            // h <= 320
-constexpr int kLdsB = 2 * kBufB + kEmapB + kBiasB;
+constexpr int kBiasB = 512 * 4;
+constexpr int kMaxNT = 20;            // fp32: h <= 320
+constexpr int kMaxNTb = 32;           // bf16: h <= 512
+// PREC 0: fp32 storage, two fp16 parts per k-slice; 1: bf16 storage, one bf16 part
+constexpr int buf_bytes(int PREC) { return PREC ? kPartB : 2 * kPartB; }
+constexpr int lds_bytes(int PREC) { return 2 * buf_bytes(PREC) + kEmapB + kBiasB; }
 
-template <int NCT>
+template <int NCT, int PREC>
 struct St {
+  static constexpr int NPART = PREC ? 1 : 2;  // operand parts per fragment
+  static constexpr int NPC = PREC ? 2 : 4;    // 16-B gather pieces per thread, tensor and k-step
   f32x4 acc[kRT][NCT];
-  uint4 wb[2][NCT][2];     // W fragments (parity, column tile, part)
-  f32x4 gs[2][4], gq[2][4];  // gathered pieces of two k-steps (slot, piece)
-  int gso[2], gqo[2];      // their row sources (float4 offsets, -1: none)
+  uint4 wb[2][NCT][NPART];     // W fragments (parity, column tile, part)
+  f32x4 gs[2][NPC], gq[2][NPC];  // gathered pieces of two k-steps (slot, piece)
+  int gso[2], gqo[2];          // their row sources (16-B piece offsets, -1: none)
   float mxH, mxS;
   int lane, wave, fr, g16, grow, q, hv, hc, NT;
   float sA, sAW, inv;
@@ -65,17 +86,22 @@ struct St {
   __amdgpu_buffer_rsrc_t wrsrc;
 };
 
-// pieces 8 s + 4 q + u (u < 4) of the thread's row of S[src] and H[rev] into slot P
-template <int NCT, int P>
-__device__ __forceinline__ void fw_gather(St<NCT>& st, const Args& a, int soff, int qoff, int s) {
+// the thread's pieces of k-step s (fp32: 8 s + 4 q + u, u < 4; bf16: 4 s + 2 q + u, u < 2) of its
+// row of S[src] and H[rev] into slot P
+template <int NCT, int PREC, int P>
+__device__ __forceinline__ void fw_gather(St<NCT, PREC>& st, const Args& a, int soff, int qoff, int s) {
+  using S_ = St<NCT, PREC>;
   st.gso[P] = soff;
   st.gqo[P] = qoff;
-  const int sb = soff >= 0 ? soff : 0, qb = qoff >= 0 ? qoff : 0;
+  int sb = soff >= 0 ? soff : 0, qb = qoff >= 0 ? qoff : 0;
+#if FW_ABL
+  if (a.rtabl & 1) sb = qb = 0;
+#endif
   const f32x4* S4 = reinterpret_cast<const f32x4*>(a.S);
   const f32x4* H4 = reinterpret_cast<const f32x4*>(a.H ? a.H : a.S);
 #pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    int p = 8 * s + 4 * st.q + u;
+  for (int u = 0; u < S_::NPC; ++u) {
+    int p = 2 * S_::NPC * s + S_::NPC * st.q + u;
     p = p < st.hv ? p : 0;
     st.gs[P][u] = S4[sb + p];
     st.gq[P][u] = H4[qb + p];
@@ -84,9 +110,26 @@ __device__ __forceinline__ void fw_gather(St<NCT>& st, const Args& a, int soff, 
 
 // item v (k-group 2 q + v) of slot P: A = S[src] - act(H[rev]) scaled by s_A, split into two fp16
 // parts written in MFMA B-fragment order into LDS buffer BUF
-template <int NCT, int ACT, int P, int BUF>
-__device__ __forceinline__ void fw_split(St<NCT>& st, const Args& a, int s, int v) {
+template <int NCT, int PREC, int ACT, int P, int BUF>
+__device__ __forceinline__ void fw_split(St<NCT, PREC>& st, const Args& a, int s, int v) {
   const bool sok = st.gso[P] >= 0, qok = st.gqo[P] >= 0;
+  char* base = st.abuf + BUF * buf_bytes(PREC) + (st.grow >> 4) * 1024 + ((2 * st.q + v) * 16 + (st.grow & 15)) * 16;
+  if constexpr (PREC == 1) {
+    // bf16: piece v holds k-group 2 q + v (8 values); A in fp32 from the widened values, rounded to
+    // bf16 once (as update_bf16_kernel)
+    const bool in = 4 * s + 2 * st.q + v < st.hv;
+    const uint4 su = __builtin_bit_cast(uint4, st.gs[P][v]), qu = __builtin_bit_cast(uint4, st.gq[P][v]);
+    const unsigned sw[4] = {su.x, su.y, su.z, su.w}, qw[4] = {qu.x, qu.y, qu.z, qu.w};
+    fk::bf16x8 hb;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const float q0 = act_t<ACT>(fk::bf_lo(qw[c]), a.act, a.alpha), q1 = act_t<ACT>(fk::bf_hi(qw[c]), a.act, a.alpha);
+      hb[2 * c] = (__bf16)((sok && in ? fk::bf_lo(sw[c]) : 0.f) - (qok && in ? q0 : 0.f));
+      hb[2 * c + 1] = (__bf16)((sok && in ? fk::bf_hi(sw[c]) : 0.f) - (qok && in ? q1 : 0.f));
+    }
+    *reinterpret_cast<fk::bf16x8*>(base) = hb;
+    return;
+  }
   f16x8 h0, h1;
 #pragma unroll
   for (int uu = 0; uu < 2; ++uu) {
@@ -94,41 +137,56 @@ __device__ __forceinline__ void fw_split(St<NCT>& st, const Args& a, int s, int 
     const bool in = 8 * s + 4 * st.q + u < st.hv;
     const f32x4 sv = st.gs[P][u];
     const f32x4 qv = st.gq[P][u];
+    // per piece: the scale s_A, or 0 for a masked operand (a row past the tile, k past h, no src /
+    // rev); x = fma(s, fs, -act(q) fq) rounds once, = fp32(s - act(q)) s_A exactly (power of two);
+    // relu(q) fq = max(q fq, 0) as fq >= 0.  A masked read is of valid memory (row 0 / piece 0):
+    // finite by the contract, so its product with 0 is 0.
+    const float fs = sok && in ? st.sA : 0.f, fq = qok && in ? st.sA : 0.f;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-      const float qa = act_t<ACT>(qv[c], a.act, a.alpha);
-      const float x = ((sok && in ? sv[c] : 0.f) - (qok && in ? qa : 0.f)) * st.sA;
+      float qs;
+      if constexpr (ACT == NT_ACT_RELU) qs = fmaxf(qv[c] * fq, 0.f);
+      else qs = act_t<ACT>(qv[c], a.act, a.alpha) * fq;
+      float x = fmaf(sv[c], fs, -qs);
+      // x is the fp32 value of A s_A: keep hipcc from fusing the fma into the fp16 conversion
+      // (v_fma_mix* would round the exact product to fp16 once, not fp32 x to fp16)
+      asm volatile("" : "+v"(x));
       const _Float16 t0 = (_Float16)x;
       h0[4 * uu + c] = t0;
       h1[4 * uu + c] = (_Float16)(x - (float)t0);
     }
   }
-  char* base = st.abuf + BUF * kBufB + (st.grow >> 4) * 1024 + ((2 * st.q + v) * 16 + (st.grow & 15)) * 16;
   *reinterpret_cast<f16x8*>(base) = h0;
   *reinterpret_cast<f16x8*>(base + kPartB) = h1;
 }
 
 // W fragments of k-step s, column tiles [J0, J1) of this wave, into parity P
-template <int NCT, int P, int J0, int J1>
-__device__ __forceinline__ void fw_load_w(St<NCT>& st, int s) {
+template <int NCT, int PREC, int P, int J0, int J1>
+__device__ __forceinline__ void fw_load_w(St<NCT, PREC>& st, int s) {
 #pragma unroll
   for (int j = J0; j < J1; ++j) {
     const int ct = st.wave + 4 * j;
-    const int soff = __builtin_amdgcn_readfirstlane(fk::kImgHdr + ((s * st.NT + ct) * 2) * 1024);
+    // fp32: two parts per block behind the scale header; bf16: the plain bf16 image (one part)
+    const int blk = PREC ? (s * st.NT + ct) * 1024 : fk::kImgHdr + ((s * st.NT + ct) * 2) * 1024;
+    const int soff = __builtin_amdgcn_readfirstlane(blk);
     st.wb[P][j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff, 0));
-    st.wb[P][j][1] =
-        __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff + 1024, 0));
+    if constexpr (PREC == 0)
+      st.wb[P][j][1] =
+          __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff + 1024, 0));
   }
 }
 
 // residual rows of tile i, column tile j, straight into the accumulators (scaled before the K loop)
-template <int NCT>
-__device__ __forceinline__ void fw_resid_load(St<NCT>& st, const Args& a, int i, int j) {
+template <int NCT, int PREC>
+__device__ __forceinline__ void fw_resid_load(St<NCT, PREC>& st, const Args& a, int i, int j) {
   int pc = 4 * (st.wave + 4 * j) + st.g16;
   pc = pc < st.hc ? pc : 0;
 #pragma unroll
   for (int rt = 0; rt < kRT; ++rt) {
-    const int e = st.emap[(i % kEmaps) * kRows + 16 * rt + st.fr].x;
+    int e = st.emap[(i % kEmaps) * kRows + 16 * rt + st.fr].x;
+#if FW_ABL
+    if (a.rtabl & 8) e = 0;
+#endif
     st.acc[rt][j] = reinterpret_cast<const f32x4*>(a.H)[(int64_t)(e >= 0 ? e : 0) * st.hc + pc];
   }
 }
@@ -137,29 +195,30 @@ __device__ __forceinline__ void fw_resid_load(St<NCT>& st, const Args& a, int i,
 // the row tiles: W of step k + 1 into parity 1 - P, the split of the staged step k + 1 (slot 1 - P)
 // into buffer 1 - P, then the gathers of step k + 3 into the freed slot.  Row tiles past the tile's
 // rows (nrt) are skipped as a whole (wave-uniform).
-template <int NCT, int ACT, int P>
-__device__ __forceinline__ void fw_step(St<NCT>& st, const Args& a, int s_w1, int s_split, int s_g, int g_soff,
+template <int NCT, int PREC, int ACT, int P>
+__device__ __forceinline__ void fw_step(St<NCT, PREC>& st, const Args& a, int s_w1, int s_split, int s_g, int g_soff,
                                         int g_qoff, int nrt) {
-  const char* bb = st.abuf + P * kBufB + st.lane * 16;
+  const char* bb = st.abuf + P * buf_bytes(PREC) + st.lane * 16;
   f16x8 a0 = *reinterpret_cast<const f16x8*>(bb);
-  f16x8 a1 = *reinterpret_cast<const f16x8*>(bb + kPartB);
+  f16x8 a1 = PREC ? a0 : *reinterpret_cast<const f16x8*>(bb + kPartB);
   fk::sfor<kRT>([&](auto RTc) {
     constexpr int rt = decltype(RTc)::value;
     f16x8 n0 = a0, n1 = a1;
     if constexpr (rt + 1 < kRT) {
       n0 = *reinterpret_cast<const f16x8*>(bb + (rt + 1) * 1024);
-      n1 = *reinterpret_cast<const f16x8*>(bb + kPartB + (rt + 1) * 1024);
+      if constexpr (PREC == 0) n1 = *reinterpret_cast<const f16x8*>(bb + kPartB + (rt + 1) * 1024);
     }
     if (rt < 6 || rt < nrt) {
 #pragma unroll
-      for (int j = 0; j < NCT; ++j) st.acc[rt][j] = fk::fk_mac<0>(st.wb[P][j][0], st.wb[P][j][1], a0, a1, st.acc[rt][j]);
+      for (int j = 0; j < NCT; ++j)
+        st.acc[rt][j] = fk::fk_mac<PREC>(st.wb[P][j][0], st.wb[P][j][PREC ? 0 : 1], a0, a1, st.acc[rt][j]);
     }
     // side work of this row tile
-    if constexpr (rt == 0) fw_load_w<NCT, 1 - P, 0, (NCT + 1) / 2>(st, s_w1);
-    if constexpr (rt == 1) fw_load_w<NCT, 1 - P, (NCT + 1) / 2, NCT>(st, s_w1);
-    if constexpr (rt == 2) fw_split<NCT, ACT, 1 - P, 1 - P>(st, a, s_split, 0);
-    if constexpr (rt == 3) fw_split<NCT, ACT, 1 - P, 1 - P>(st, a, s_split, 1);
-    if constexpr (rt == 4) fw_gather<NCT, 1 - P>(st, a, g_soff, g_qoff, s_g);
+    if constexpr (rt == 0) fw_load_w<NCT, PREC, 1 - P, 0, (NCT + 1) / 2>(st, s_w1);
+    if constexpr (rt == 1) fw_load_w<NCT, PREC, 1 - P, (NCT + 1) / 2, NCT>(st, s_w1);
+    if constexpr (rt == 2) fw_split<NCT, PREC, ACT, 1 - P, 1 - P>(st, a, s_split, 0);
+    if constexpr (rt == 3) fw_split<NCT, PREC, ACT, 1 - P, 1 - P>(st, a, s_split, 1);
+    if constexpr (rt == 4) fw_gather<NCT, PREC, 1 - P>(st, a, g_soff, g_qoff, s_g);
     a0 = n0;
     a1 = n1;
     __builtin_amdgcn_sched_barrier(0);
@@ -167,21 +226,51 @@ __device__ __forceinline__ void fw_step(St<NCT>& st, const Args& a, int s_w1, in
   __syncthreads();
 }
 
-// epilogue unit (row tile RTI, column tile J): scale + bias, H_out piece, the segmented node scan
-// (MAXL rounds, carries between row tiles) and S_out at node ends.  As fk_epi_row (SUMONLY).
-template <int RTI, int J, int NCT, int AACT, int MAXL>
-__device__ __forceinline__ void fw_epi_row(St<NCT>& st, const Args& a, const int4* em, int n, int pc, bool pok,
-                                           const f32x4& bj, f32x4& carry) {
+// bf16 residual pieces of column tile J (8 B = 4 bf16 per row tile), issued a column tile ahead
+template <int NCT, int PREC>
+__device__ __forceinline__ void fw_resid_bf(St<NCT, PREC>& st, const Args& a, const int4* em, int J, uint2 (&rr)[kRT]) {
+  int pc = 4 * (st.wave + 4 * J) + st.g16;
+  pc = pc < st.hc ? pc : 0;
+#pragma unroll
+  for (int rt = 0; rt < kRT; ++rt) {
+    const int e = em[16 * rt + st.fr].x;
+    rr[rt] = reinterpret_cast<const uint2*>(a.H)[(int64_t)(e >= 0 ? e : 0) * st.hc + pc];
+  }
+}
+
+// epilogue unit (row tile RTI, column tile J): H_out piece, the segmented node scan (MAXL rounds,
+// carries between row tiles) and S_out at node ends.  As fk_epi_row (SUMONLY).  fp32: H_out =
+// acc / (s_A s_W) + b (the residual is in acc).  bf16: H_out = bf16((acc + b) + H[e]) as
+// update_bf16_kernel, the scan over the stored (rounded) values.
+template <int RTI, int J, int NCT, int PREC, int AACT, int MAXL>
+__device__ __forceinline__ void fw_epi_row(St<NCT, PREC>& st, const Args& a, const int4* em, int n, int pc, bool pok,
+                                           const f32x4& bj, f32x4& carry, const uint2 (&rr)[kRT], bool resid) {
   if (16 * RTI < n) {
     const int hc = st.hc;
     const int4 ri = em[16 * RTI + st.fr];
     f32x4 o;
+    uint2 ob = uint2{0u, 0u};
+    if constexpr (PREC == 1) {
+      const float4 r = resid ? fk::bf4_widen(uint4{rr[RTI].x, rr[RTI].y, 0u, 0u}) : float4{0.f, 0.f, 0.f, 0.f};
+      ob = fk::bf4_pack((st.acc[RTI][J][0] + bj[0]) + r.x, (st.acc[RTI][J][1] + bj[1]) + r.y,
+                        (st.acc[RTI][J][2] + bj[2]) + r.z, (st.acc[RTI][J][3] + bj[3]) + r.w);
+      const float4 w = fk::bf4_widen(uint4{ob.x, ob.y, 0u, 0u});
+      o = f32x4{w.x, w.y, w.z, w.w};
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[RTI][J][q], st.inv, bj[q]);
-    const bool rok = ri.x >= 0 && pok;
+      for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[RTI][J][q], st.inv, bj[q]);
+    }
+    bool rok = ri.x >= 0 && pok;
+#if FW_ABL
+    if (a.rtabl & 4) rok = false;
+#endif
     if (rok) {
-      reinterpret_cast<f32x4*>(a.O)[(int64_t)ri.x * hc + pc] = o;
-      st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+      if constexpr (PREC == 1) {
+        reinterpret_cast<uint2*>(a.O)[(int64_t)ri.x * hc + pc] = ob;
+      } else {
+        reinterpret_cast<f32x4*>(a.O)[(int64_t)ri.x * hc + pc] = o;
+        st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+      }
     }
     const bool start = (ri.z & fk::kFlagStart) != 0;
     f32x4 m;
@@ -190,6 +279,9 @@ __device__ __forceinline__ void fw_epi_row(St<NCT>& st, const Args& a, const int
     f32x4 x = m, cin;
 #pragma unroll
     for (int q = 0; q < 4; ++q) cin[q] = fk::dpp_ror1(carry[q]);
+#if FW_ABL
+    if (!(a.rtabl & 32))
+#endif
 #pragma unroll
     for (int it = 0; it < MAXL; ++it) {
       f32x4 y;
@@ -198,37 +290,49 @@ __device__ __forceinline__ void fw_epi_row(St<NCT>& st, const Args& a, const int
       x = start ? m : y + m;
     }
     if ((ri.z & fk::kFlagEnd) && rok) {
-      reinterpret_cast<f32x4*>(a.SO)[(int64_t)ri.y * hc + pc] = x;
-      st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+      if constexpr (PREC == 1) {
+        reinterpret_cast<uint2*>(a.SO)[(int64_t)ri.y * hc + pc] = fk::bf4_pack(x[0], x[1], x[2], x[3]);
+      } else {
+        reinterpret_cast<f32x4*>(a.SO)[(int64_t)ri.y * hc + pc] = x;
+        st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+      }
     }
     carry = x;
   }
-  if constexpr (RTI + 1 < kRT) fw_epi_row<RTI + 1, J, NCT, AACT, MAXL>(st, a, em, n, pc, pok, bj, carry);
+#if FW_EPI_FENCE
+  __builtin_amdgcn_sched_barrier(0);
+#endif
+  if constexpr (RTI + 1 < kRT) fw_epi_row<RTI + 1, J, NCT, PREC, AACT, MAXL>(st, a, em, n, pc, pok, bj, carry, rr, resid);
 }
 
-template <int J, int NCT, int AACT, int MAXL>
-__device__ __forceinline__ void fw_epi_col(St<NCT>& st, const Args& a, const int4* em, int n, bool load_next,
-                                           int i_next) {
+template <int J, int NCT, int PREC, int AACT, int MAXL>
+__device__ __forceinline__ void fw_epi_col(St<NCT, PREC>& st, const Args& a, const int4* em, int n, bool resid,
+                                           bool load_next, int i_next, uint2 (&rr0)[kRT], uint2 (&rr1)[kRT]) {
+  uint2(&rr)[kRT] = (J & 1) ? rr1 : rr0;
+  if constexpr (PREC == 1) {  // the next column tile's residual pieces, in flight across this one
+    if (J + 1 < NCT && resid) fw_resid_bf(st, a, em, J + 1, (J & 1) ? rr0 : rr1);
+  }
   const int pc = 4 * (st.wave + 4 * J) + st.g16;
   const bool pok = pc < st.hc;
   f32x4 bj = f32x4{0.f, 0.f, 0.f, 0.f};
   if (a.bias && pok) bj = *reinterpret_cast<const f32x4*>(st.lbias + 4 * pc);
   f32x4 carry = f32x4{0.f, 0.f, 0.f, 0.f};
-  fw_epi_row<0, J, NCT, AACT, MAXL>(st, a, em, n, pc, pok, bj, carry);
-  // column tile J is stored: its accumulators take the next tile's residual rows
-  if (load_next) {
+  fw_epi_row<0, J, NCT, PREC, AACT, MAXL>(st, a, em, n, pc, pok, bj, carry, rr, resid);
+  // column tile J is stored: fp32 -- its accumulators take the next tile's residual rows; bf16 --
+  // they restart at zero (the residual enters in the epilogue)
+  if (PREC == 0 && load_next) {
     fw_resid_load(st, a, i_next, J);
   } else {
 #pragma unroll
     for (int rt = 0; rt < kRT; ++rt) st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
-  if constexpr (J + 1 < NCT) fw_epi_col<J + 1, NCT, AACT, MAXL>(st, a, em, n, load_next, i_next);
+  if constexpr (J + 1 < NCT) fw_epi_col<J + 1, NCT, PREC, AACT, MAXL>(st, a, em, n, resid, load_next, i_next, rr0, rr1);
 }
 
-template <int NCT, int ACT, int AACT, int MAXL>
+template <int NCT, int PREC, int ACT, int AACT, int MAXL>
 __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int tstride, int ntl) {
   auto tile = [&](int i) __attribute__((always_inline)) { return t0 + (i < ntl ? i : ntl - 1) * tstride; };
-  St<NCT> st;
+  St<NCT, PREC> st;
   const int tid = threadIdx.x;
   st.lane = tid & 63;
   st.wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -240,13 +344,23 @@ __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int ts
   st.hc = a.h / 4;
   st.NT = a.NT;
   st.abuf = smem;
-  st.emap = reinterpret_cast<int4*>(smem + 2 * kBufB);
-  st.lbias = reinterpret_cast<float*>(smem + 2 * kBufB + kEmapB);
-  for (int c = tid; c < a.h; c += kThreads) st.lbias[c] = a.bias ? a.bias[c] : 0.f;
-  st.wrsrc = __builtin_amdgcn_make_buffer_rsrc((void*)a.Wimg, (short)0, (int)fk::image_bytes(a.h), 0x00020000);
+  st.emap = reinterpret_cast<int4*>(smem + 2 * buf_bytes(PREC));
+  st.lbias = reinterpret_cast<float*>(smem + 2 * buf_bytes(PREC) + kEmapB);
+  for (int c = tid; c < a.h; c += kThreads) {
+    float b = 0.f;
+    if (a.bias) {
+      if constexpr (PREC == 1) b = __uint_as_float((unsigned)reinterpret_cast<const unsigned short*>(a.bias)[c] << 16);
+      else b = a.bias[c];
+    }
+    st.lbias[c] = b;
+  }
+  st.wrsrc = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)a.Wimg, (short)0, PREC ? fk::ks_for(a.h) * fk::nt_for(a.h) * 1024 : (int)fk::image_bytes(a.h), 0x00020000);
   st.mxH = 0.f;
   st.mxS = 0.f;
-  {
+  if constexpr (PREC == 1) {
+    st.sA = st.sAW = st.inv = 1.f;
+  } else {
     const float bound = a.amax_in[1] + (a.rev ? fk::act_bound(a.amax_in[0], a.act, a.alpha) : 0.f);
     st.sA = ldexpf(1.f, fk::scale_exp(bound));
     const float sW = *reinterpret_cast<const float*>(a.Wimg);
@@ -286,21 +400,29 @@ __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int ts
 #pragma unroll
     for (int j = 0; j < NCT; ++j) st.acc[r][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   __syncthreads();  // emap of tiles 0 and 1, the bias
-  if (resid) {
+  if (PREC == 0 && resid) {
 #pragma unroll
     for (int j = 0; j < NCT; ++j) fw_resid_load(st, a, 0, j);
   }
   // steps 0 and 1 gathered, W of step 0, step 0 split into buffer 0, step 2 gathered
-  fw_gather<NCT, 0>(st, a, cur.x, cur.y, 0);
-  fw_gather<NCT, 1>(st, a, cur.x, cur.y, 1);
-  fw_load_w<NCT, 0, 0, NCT>(st, 0);
-  fw_split<NCT, ACT, 0, 0>(st, a, 0, 0);
-  fw_split<NCT, ACT, 0, 0>(st, a, 0, 1);
-  fw_gather<NCT, 0>(st, a, cur.x, cur.y, 2 % SPT);
+  fw_gather<NCT, PREC, 0>(st, a, cur.x, cur.y, 0);
+  fw_gather<NCT, PREC, 1>(st, a, cur.x, cur.y, 1);
+  fw_load_w<NCT, PREC, 0, 0, NCT>(st, 0);
+  fw_split<NCT, PREC, ACT, 0, 0>(st, a, 0, 0);
+  fw_split<NCT, PREC, ACT, 0, 0>(st, a, 0, 1);
+  fw_gather<NCT, PREC, 0>(st, a, cur.x, cur.y, 2 % SPT);
   __syncthreads();
 
+  uint2 rr0[kRT], rr1[kRT];
+  [[maybe_unused]] unsigned long long ts_k = 0, ts_e = 0, ts_f = 0, ts_0 = 0, ts_1 = 0, ts_w = 0;
+#if FW_STAMP
+  ts_w = __builtin_amdgcn_s_memtime();
+#endif
   for (int i = 0; i < ntl; ++i) {
-    {  // residual rows (loaded by the previous epilogue) into the accumulators' scale
+#if FW_STAMP
+    ts_0 = __builtin_amdgcn_s_memtime();
+#endif
+    if constexpr (PREC == 0) {  // residual rows (loaded by the previous epilogue) into the accumulators' scale
       const f32x4 s4 = f32x4{st.sAW, st.sAW, st.sAW, st.sAW};
 #pragma unroll
       for (int rt = 0; rt < kRT; ++rt)
@@ -313,17 +435,28 @@ __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int ts
       // last), split one step ahead, gathers three steps ahead (into the next tile at the end)
       {
         const int k3 = k + 3, adv = k3 >= SPT ? 1 : 0;
-        fw_step<NCT, ACT, 0>(st, a, k + 1, k + 1, k3 - adv * SPT, adv ? nxt.x : cur.x, adv ? nxt.y : cur.y, nrt);
+        fw_step<NCT, PREC, ACT, 0>(st, a, k + 1, k + 1, k3 - adv * SPT, adv ? nxt.x : cur.x, adv ? nxt.y : cur.y, nrt);
       }
       {
         const int k1 = k + 2 < SPT ? k + 2 : 0;
         const int k3 = k + 4, adv = k3 >= SPT ? 1 : 0;
-        fw_step<NCT, ACT, 1>(st, a, k1, k1, k3 - adv * SPT, adv ? nxt.x : cur.x, adv ? nxt.y : cur.y, nrt);
+        fw_step<NCT, PREC, ACT, 1>(st, a, k1, k1, k3 - adv * SPT, adv ? nxt.x : cur.x, adv ? nxt.y : cur.y, nrt);
       }
+#if FW_STAMP
+      if (k == 0) ts_f += __builtin_amdgcn_s_memtime() - ts_0;
+#endif
     }
+#if FW_STAMP
+    ts_1 = __builtin_amdgcn_s_memtime();
+    ts_k += ts_1 - ts_0;
+#endif
     const bool more = i + 1 < ntl;
     const int4* em = st.emap + (i % kEmaps) * kRows;
-    fw_epi_col<0, NCT, AACT, MAXL>(st, a, em, n_cur, resid && more, i + 1);
+    if (PREC == 1 && resid) fw_resid_bf(st, a, em, 0, rr0);
+    fw_epi_col<0, NCT, PREC, AACT, MAXL>(st, a, em, n_cur, resid, resid && more, i + 1, rr0, rr1);
+#if FW_STAMP
+    ts_e += __builtin_amdgcn_s_memtime() - ts_1;
+#endif
     // advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
     cur = nxt;
     n_cur = n_nxt;
@@ -343,13 +476,24 @@ __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int ts
       fk::atomic_max_abs(a.amax_out + 1, ms);
     }
   }
+#if FW_STAMP
+  if (st.lane == 0) {
+    atomicAdd(&g_pk_stamps[0], ts_k);
+    atomicAdd(&g_pk_stamps[1], ts_e);
+    atomicAdd(&g_pk_stamps[2], ts_f);
+    atomicAdd(&g_pk_stamps[3], (unsigned long long)ntl);
+    atomicAdd(&g_pk_stamps[4], 1ull);
+    atomicAdd(&g_pk_stamps[5], __builtin_amdgcn_s_memtime() - ts_w);
+  }
+#endif
 }
 
-// Fused relu / sum layers, h <= 320 (NT <= 20), tiles of <= 128 rows: waves with ceil(NT / 4)
-// column tiles run fw_run<CTM>, the others (NT % 4 != 0) fw_run<CTM - 1>.
-template <int CTM, int ACT, int AACT, int MAXL>
+// Fused relu / sum layers, tiles of <= 128 rows; fp32 (PREC 0) h <= 320 (NT <= 20), bf16 (PREC 1)
+// h <= 512 (NT <= 32): waves with ceil(NT / 4) column tiles run fw_run<CTM>, the others
+// (NT % 4 != 0) fw_run<CTM - 1>.
+template <int CTM, int PREC, int ACT, int AACT, int MAXL>
 __global__ void __launch_bounds__(kThreads, 1) update_fw_kernel(Args a) {
-  __shared__ __attribute__((aligned(16))) char smem[kLdsB];
+  __shared__ __attribute__((aligned(16))) char smem[lds_bytes(PREC)];
   int t0 = (int)blockIdx.x, tstride = (int)gridDim.x, ntl;
   const int nx = a.nxcd;
   if (nx > 1 && (int)gridDim.x % nx == 0) {
@@ -364,13 +508,13 @@ __global__ void __launch_bounds__(kThreads, 1) update_fw_kernel(Args a) {
   if (ntl <= 0) return;
   const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
   const int nct = (a.NT - wave + 3) / 4;
-  if constexpr (CTM > 1) {
+  if constexpr (CTM > 1 && !FW_ONE_PATH) {
     if (nct < CTM) {
-      fw_run<CTM - 1, ACT, AACT, MAXL>(a, smem, t0, tstride, ntl);
+      fw_run<CTM - 1, PREC, ACT, AACT, MAXL>(a, smem, t0, tstride, ntl);
       return;
     }
   }
-  fw_run<CTM, ACT, AACT, MAXL>(a, smem, t0, tstride, ntl);
+  fw_run<CTM, PREC, ACT, AACT, MAXL>(a, smem, t0, tstride, ntl);
 }
 
 }  // namespace fw

@@ -885,13 +885,6 @@ int launch_fk_nw4(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
                      : launch_fk_nw4_t<NT_ACT_IDENTITY, 16>(a, grid, stream);
 }
 
-// One-wave-per-SIMD walk (update_fw_kernel): fused relu layers with a sum aggregation whose act is
-// relu / identity, 257 <= h <= 320 (five column tiles per wave), tiles of <= 128 rows.
-bool fw_supported(int64_t h, int act, int reduce, int aact) {
-  const int nt = fk::nt_for(h);
-  return act == NT_ACT_RELU && reduce == NT_SUM && (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY) && nt > 16 &&
-         nt <= fw::kMaxNT;
-}
 // A/B switch: NT_FK_FW=1 / 0 (read once per process) selects update_fw_kernel where it applies;
 // nt_debug_set_fw overrides it (tests and kernel benches switch within one process)
 int g_fw_override = -1;
@@ -906,9 +899,27 @@ bool fw_selected() {
 template <int AACT, int MAXL>
 int launch_fw_t(const fk::Args& a, int grid, hipStream_t stream) {
   set_last_kernel("update_fw_kernel: one 4-wave workgroup per CU (one wave per SIMD), 128-row tiles");
-  fw::update_fw_kernel<5, NT_ACT_RELU, AACT, MAXL><<<grid, fw::kThreads, 0, stream>>>(a);
+  fw::update_fw_kernel<5, 0, NT_ACT_RELU, AACT, MAXL><<<grid, fw::kThreads, 0, stream>>>(a);
   NT_LAUNCH_CHECK();
   return NT_OK;
+}
+
+template <int AACT, int MAXL>
+int launch_fwb_t(const fk::Args& a, int grid, hipStream_t stream) {
+  set_last_kernel("update_fw_kernel (bf16): one 4-wave workgroup per CU (one wave per SIMD), 128-row tiles");
+  fw::update_fw_kernel<8, 1, NT_ACT_RELU, AACT, MAXL><<<grid, fw::kThreads, 0, stream>>>(a);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+int launch_fwb(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
+  if (a.aact == NT_ACT_RELU)
+    return maxl <= 3   ? launch_fwb_t<NT_ACT_RELU, 3>(a, grid, stream)
+           : maxl <= 8 ? launch_fwb_t<NT_ACT_RELU, 8>(a, grid, stream)
+                       : launch_fwb_t<NT_ACT_RELU, 16>(a, grid, stream);
+  return maxl <= 3   ? launch_fwb_t<NT_ACT_IDENTITY, 3>(a, grid, stream)
+         : maxl <= 8 ? launch_fwb_t<NT_ACT_IDENTITY, 8>(a, grid, stream)
+                     : launch_fwb_t<NT_ACT_IDENTITY, 16>(a, grid, stream);
 }
 
 int launch_fw(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
@@ -950,6 +961,15 @@ int fk_tile_rows(int64_t h, int act, int reduce, int aact, bool fused) {
   const bool wide_ok =
       !fused || (act == NT_ACT_RELU && reduce == NT_SUM && (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY));
   return (fk::nt_for(h) <= 24 && wide_ok) ? 128 : 64;
+}
+
+// the one-wave-per-SIMD walk for this fused layer (A/B switch fw_selected): fp32 257 <= h <= 320,
+// bf16 449 <= h <= 512 (eight column tiles per wave), relu layers with a relu / identity sum
+bool fw_active(int64_t h, int dtype, int act, int reduce, int aact) {
+  if (!fw_selected() || act != NT_ACT_RELU || reduce != NT_SUM || !(aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY))
+    return false;
+  const int nt = fk::nt_for(h);
+  return dtype == NT_BF16 ? (h % 8 == 0 && nt > 28 && nt <= fw::kMaxNTb) : (nt > 16 && nt <= fw::kMaxNT);
 }
 
 int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in, float* amax_out,
@@ -1020,7 +1040,7 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
     return launch_fk2(a, grid, u.stream);
   }
 #endif
-  if (fused && fw_selected() && fw_supported(u.h, u.act, reduce, aact)) {
+  if (fused && fw_active(u.h, NT_F32, u.act, reduce, aact)) {
     a.nchunks = 1;
     return launch_fw(a, maxl, grid, u.stream);
   }
@@ -1129,6 +1149,7 @@ int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* 
     return launch_fkb_t<-1, NT_ACT_IDENTITY, true, 1>(a, grid, u.stream);
   }
   const int maxl = max_in_degree - 1;
+  if (fw_active(u.h, NT_BF16, u.act, reduce, aact)) return launch_fwb(a, maxl, grid, u.stream);
   {
     if (bf16_kernel_env() == 2 && tile_rows <= 64 && relu && reduce == NT_SUM &&
         (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY)) {
@@ -1190,6 +1211,17 @@ int amax_fill(float* ws, const float* H, int64_t nh, const float* S, int64_t ns,
 }
 
 }  // namespace nt
+
+#if FW_STAMP
+// A/B builds only (FW_STAMP): read and reset the fw kernel's stamp sums (6 values)
+extern "C" __attribute__((visibility("default"))) int nt_debug_fw_stamps(unsigned long long* out6) {
+  if (hipMemcpyFromSymbol(out6, HIP_SYMBOL(nt::g_pk_stamps), 6 * sizeof(unsigned long long), 0,
+                          hipMemcpyDeviceToHost) != hipSuccess)
+    return 2;
+  unsigned long long z[10] = {0};
+  return hipMemcpyToSymbol(HIP_SYMBOL(nt::g_pk_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : 2;
+}
+#endif
 
 #if FK_STAMP
 // A/B builds only (FK_STAMP): read and reset the fk kernel's coarse stamp sums

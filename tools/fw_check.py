@@ -87,6 +87,25 @@ def main():
     dH = (o0 - o1).abs().max().item() / o0.abs().max().item()
     dS = (s0 - s1).abs().max().item() / s0.abs().max().item()
     print(f"bit-exact H {eqH} S {eqS} amax {eqM}  (norm max diff H {dH:.3e} S {dS:.3e}; nan {o1.isnan().sum().item()})")
+    if not eqH:  # where the walks disagree: rows by position in their tile, columns by tile / wave
+        diff = (o0 != o1)
+        nd = int(diff.sum())
+        rows = diff.any(1).nonzero().flatten()
+        cols = diff.any(0).nonzero().flatten()
+        tp = plan[0].cpu().long()
+        dsts_pos = torch.empty(E, dtype=torch.long)
+        dsts_pos[lay.dst_perm.cpu().long()] = torch.arange(E)
+        pos = dsts_pos[rows.cpu()]
+        tile = torch.searchsorted(tp, pos, right=True) - 1
+        inrow = pos - tp[tile]
+        print(f"  H mismatches: {nd} elements in {rows.numel()} rows, {cols.numel()} columns")
+        print(f"  row-in-tile histogram (by 16): {torch.bincount(inrow // 16, minlength=8).tolist()}")
+        ct = cols.cpu() // 16
+        print(f"  column tiles: {torch.bincount(ct, minlength=(h + 15) // 16).tolist()}")
+        print(f"  tiles touched: {tile.unique().numel()} of {plan[1]}; first rows {rows[:8].tolist()} cols {cols[:8].tolist()}")
+        r0 = rows[0].item()
+        c0 = diff[r0].nonzero().flatten()[:4].tolist()
+        print(f"  row {r0}: fk {o0[r0, c0].tolist()} fw {o1[r0, c0].tolist()}")
     o2, s2, m2 = outs[2]
     print(f"fk 64-row walk bit-exact vs 128-row: H {torch.equal(o0, o2)} S {torch.equal(s0, s2)}")
     res = {0: [], 1: [], 2: []}
@@ -96,6 +115,18 @@ def main():
     for v, name in ((0, "fk128"), (1, "fw128"), (2, "fk64")):
         med = statistics.median(res[v])
         print(f"{name}: median {med:7.1f} us  {2 * E * h * h / (med * 1e-6) / 1e12:6.1f} TF/s fp32-equivalent")
+    if hasattr(lib, "nt_debug_fw_stamps"):  # FW_STAMP build: where the fw walk's cycles go
+        import ctypes as C
+        buf = (C.c_ulonglong * 6)()
+        lib.nt_debug_fw_stamps(buf)  # reset
+        for _ in range(10):
+            fns[1]()
+        torch.cuda.synchronize()
+        lib.nt_debug_fw_stamps(buf)
+        k, e, f, t, w, tot = list(buf)
+        print(f"stamps per wave per launch: K loops {k / w:.0f} cyc ({k / t:.0f} per tile), epilogues {e / w:.0f} "
+              f"({e / t:.0f} per tile), first step pair {f / t:.0f} per tile, whole walk {tot / w:.0f}; "
+              f"tiles/wave {t / w * 10 / 10:.2f}")
     setfw(-1)
     if not (eqH and eqS and eqM):
         sys.exit(3)
