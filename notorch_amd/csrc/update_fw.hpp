@@ -37,13 +37,23 @@
 #ifndef FW_EPI_FENCE
 #define FW_EPI_FENCE 0
 #endif
+// FW_EPI_RT: the row-tile-outer epilogue (fw_epilogue_rt); 0: column-tile-outer (fw_epi_col)
+#ifndef FW_EPI_RT
+#define FW_EPI_RT 1
+#endif
+// FW_EPI_LDS: the node sums from an LDS stage per column tile (fw_epilogue_lds; overrides FW_EPI_RT)
+#ifndef FW_EPI_LDS
+#define FW_EPI_LDS 1
+#endif
 // FW_STAMP (A/B builds): s_memtime sums per wave into g_pk_stamps: [0] K loops, [1] epilogues,
 // [2] first step pair of each tile (the tile-start wait), [3] tiles, [4] waves, [5] whole walk
 #ifndef FW_STAMP
 #define FW_STAMP 0
 #endif
 // FW_ABL (A/B builds, timing ablations, results invalid): Args::rtabl bits (NT_FK_RTABL) -- 1 gathers
-// read row 0, 4 no H_out / S_out stores, 8 residual rows read row 0, 32 no aggregation scan
+// read row 0, 4 no H_out / S_out stores, 8 residual rows read row 0, 32 no aggregation scan, 64 no
+// epilogue at all, 128 no MFMA, 256 no split, 512 no per-step barrier, 2 W reads block 0, 1024 no W
+// loads in the K loop, 2048 no gathers in the K loop
 #ifndef FW_ABL
 #define FW_ABL 0
 #endif
@@ -67,7 +77,15 @@ constexpr int kMaxNT = 20;            // fp32: h <= 320
 constexpr int kMaxNTb = 32;           // bf16: h <= 512
 // PREC 0: fp32 storage, two fp16 parts per k-slice; 1: bf16 storage, one bf16 part
 constexpr int buf_bytes(int PREC) { return PREC ? kPartB : 2 * kPartB; }
-constexpr int lds_bytes(int PREC) { return 2 * buf_bytes(PREC) + kEmapB + kBiasB; }
+// FW_EPI_LDS: per-wave stage of one column tile (128 rows x 16 columns, pitch 20 floats: conflict-free
+// 16-B row writes) for the node reduction, and the tile's node list (start rows, count)
+constexpr int kStagePitch = 20;
+constexpr int kStageB = kRows * kStagePitch * 4;  // 10 KiB per wave
+constexpr int kNodeListN = kRows + 4;             // start rows [0, ns], ns at [kRows + 2]
+constexpr int kNodeListB = kNodeListN * 4;
+constexpr int lds_bytes(int PREC) {
+  return 2 * buf_bytes(PREC) + kEmapB + kBiasB + (FW_EPI_LDS ? 4 * (kStageB + kNodeListB) : 0);
+}
 
 template <int NCT, int PREC>
 struct St {
@@ -79,10 +97,13 @@ struct St {
   int gso[2], gqo[2];          // their row sources (16-B piece offsets, -1: none)
   float mxH, mxS;
   int lane, wave, fr, g16, grow, q, hv, hc, NT;
+  int rtabl;  // FW_ABL builds: Args::rtabl
   float sA, sAW, inv;
   char* abuf;
   int4* emap;
   float* lbias;
+  float* stage;  // FW_EPI_LDS: this wave's column-tile stage
+  int* nlist;    // FW_EPI_LDS: this wave's copy of the tile's node list
   __amdgpu_buffer_rsrc_t wrsrc;
 };
 
@@ -167,7 +188,10 @@ __device__ __forceinline__ void fw_load_w(St<NCT, PREC>& st, int s) {
   for (int j = J0; j < J1; ++j) {
     const int ct = st.wave + 4 * j;
     // fp32: two parts per block behind the scale header; bf16: the plain bf16 image (one part)
-    const int blk = PREC ? (s * st.NT + ct) * 1024 : fk::kImgHdr + ((s * st.NT + ct) * 2) * 1024;
+    int blk = PREC ? (s * st.NT + ct) * 1024 : fk::kImgHdr + ((s * st.NT + ct) * 2) * 1024;
+#if FW_ABL
+    if (st.rtabl & 2) blk = PREC ? 0 : fk::kImgHdr;
+#endif
     const int soff = __builtin_amdgcn_readfirstlane(blk);
     st.wb[P][j][0] = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff, 0));
     if constexpr (PREC == 0)
@@ -208,21 +232,42 @@ __device__ __forceinline__ void fw_step(St<NCT, PREC>& st, const Args& a, int s_
       n0 = *reinterpret_cast<const f16x8*>(bb + (rt + 1) * 1024);
       if constexpr (PREC == 0) n1 = *reinterpret_cast<const f16x8*>(bb + kPartB + (rt + 1) * 1024);
     }
+#if FW_ABL
+    if (!(a.rtabl & 128))
+#endif
     if (rt < 6 || rt < nrt) {
 #pragma unroll
       for (int j = 0; j < NCT; ++j)
         st.acc[rt][j] = fk::fk_mac<PREC>(st.wb[P][j][0], st.wb[P][j][PREC ? 0 : 1], a0, a1, st.acc[rt][j]);
     }
     // side work of this row tile
+#if FW_ABL
+    if (!(a.rtabl & 1024)) {
+#endif
     if constexpr (rt == 0) fw_load_w<NCT, PREC, 1 - P, 0, (NCT + 1) / 2>(st, s_w1);
     if constexpr (rt == 1) fw_load_w<NCT, PREC, 1 - P, (NCT + 1) / 2, NCT>(st, s_w1);
+#if FW_ABL
+    }
+#endif
+#if FW_ABL
+    if (!(a.rtabl & 256)) {
+#endif
     if constexpr (rt == 2) fw_split<NCT, PREC, ACT, 1 - P, 1 - P>(st, a, s_split, 0);
     if constexpr (rt == 3) fw_split<NCT, PREC, ACT, 1 - P, 1 - P>(st, a, s_split, 1);
+#if FW_ABL
+    }
+#endif
+#if FW_ABL
+    if (!(a.rtabl & 2048))
+#endif
     if constexpr (rt == 4) fw_gather<NCT, PREC, 1 - P>(st, a, g_soff, g_qoff, s_g);
     a0 = n0;
     a1 = n1;
     __builtin_amdgcn_sched_barrier(0);
   });
+#if FW_ABL
+  if (a.rtabl & 512) return;  // no barrier (results invalid)
+#endif
   __syncthreads();
 }
 
@@ -329,6 +374,269 @@ __device__ __forceinline__ void fw_epi_col(St<NCT, PREC>& st, const Args& a, con
   if constexpr (J + 1 < NCT) fw_epi_col<J + 1, NCT, PREC, AACT, MAXL>(st, a, em, n, resid, load_next, i_next, rr0, rr1);
 }
 
+// Row-tile-outer epilogue (FW_EPI_RT): per row tile, its row entry (read once, the next one in
+// flight), then the NCT column tiles of the wave as independent units (their scans interleave, the
+// node carries of all column tiles live across row tiles), H_out / S_out at one row address per row
+// tile plus immediate column offsets, and then the next tile's residual rows of this row tile into
+// its dead accumulators (fp32) -- the loads spread over the epilogue.  Same values as fw_epi_col.
+template <int NCT, int PREC, int AACT, int MAXL>
+__device__ __forceinline__ void fw_epilogue_rt(St<NCT, PREC>& st, const Args& a, const int4* em, int n, bool resid,
+                                               bool load_next, const int4* em_next) {
+  const int hc = st.hc;
+  f32x4 carry[NCT], bj[NCT];
+  bool pok[NCT];
+  const int pc0 = 4 * st.wave + st.g16;  // column tile J: piece pc0 + 16 J
+#pragma unroll
+  for (int J = 0; J < NCT; ++J) {
+    carry[J] = f32x4{0.f, 0.f, 0.f, 0.f};
+    pok[J] = pc0 + 16 * J < hc;
+    bj[J] = (a.bias && pok[J]) ? *reinterpret_cast<const f32x4*>(st.lbias + 4 * (pc0 + 16 * J)) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  int4 ri_n = em[st.fr];
+  int en_n = load_next ? em_next[st.fr].x : 0;
+  uint2 rr[NCT], rr_n[NCT];
+  if constexpr (PREC == 1) {
+#pragma unroll
+    for (int J = 0; J < NCT; ++J) {
+      const int pc = pok[J] ? pc0 + 16 * J : 0;
+      rr_n[J] = resid ? reinterpret_cast<const uint2*>(a.H)[(int64_t)(ri_n.x >= 0 ? ri_n.x : 0) * hc + pc] : uint2{0u, 0u};
+    }
+  }
+  fk::sfor<kRT>([&](auto RTc) {
+    constexpr int rt = decltype(RTc)::value;
+    const int4 ri = ri_n;
+    const int en = en_n;
+    if constexpr (rt + 1 < kRT) {
+      ri_n = em[16 * (rt + 1) + st.fr];
+      en_n = load_next ? em_next[16 * (rt + 1) + st.fr].x : 0;
+    }
+    if constexpr (PREC == 1) {
+#pragma unroll
+      for (int J = 0; J < NCT; ++J) rr[J] = rr_n[J];
+      if constexpr (rt + 1 < kRT) {  // the next row tile's residual pieces, in flight across this one
+#pragma unroll
+        for (int J = 0; J < NCT; ++J) {
+          const int pc = pok[J] ? pc0 + 16 * J : 0;
+          rr_n[J] = resid ? reinterpret_cast<const uint2*>(a.H)[(int64_t)(ri_n.x >= 0 ? ri_n.x : 0) * hc + pc]
+                          : uint2{0u, 0u};
+        }
+      }
+    }
+    if (16 * rt < n) {
+      const bool rowok = ri.x >= 0;
+      bool endok = (ri.z & fk::kFlagEnd) && rowok;
+#if FW_ABL
+      const bool st_ok = !(a.rtabl & 4);
+#else
+      constexpr bool st_ok = true;
+#endif
+      const bool start = (ri.z & fk::kFlagStart) != 0;
+      const int64_t obase = (int64_t)(rowok ? ri.x : 0) * hc + pc0;
+      const int64_t sbase = (int64_t)(ri.y >= 0 ? ri.y : 0) * hc + pc0;
+#pragma unroll
+      for (int J = 0; J < NCT; ++J) {
+        f32x4 o;
+        uint2 ob = uint2{0u, 0u};
+        if constexpr (PREC == 1) {
+          const float4 r = fk::bf4_widen(uint4{rr[J].x, rr[J].y, 0u, 0u});
+          ob = fk::bf4_pack((st.acc[rt][J][0] + bj[J][0]) + r.x, (st.acc[rt][J][1] + bj[J][1]) + r.y,
+                            (st.acc[rt][J][2] + bj[J][2]) + r.z, (st.acc[rt][J][3] + bj[J][3]) + r.w);
+          const float4 w = fk::bf4_widen(uint4{ob.x, ob.y, 0u, 0u});
+          o = f32x4{w.x, w.y, w.z, w.w};
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[rt][J][q], st.inv, bj[J][q]);
+        }
+        if (rowok && pok[J] && st_ok) {
+          if constexpr (PREC == 1) {
+            reinterpret_cast<uint2*>(a.O)[obase + 16 * J] = ob;
+          } else {
+            reinterpret_cast<f32x4*>(a.O)[obase + 16 * J] = o;
+            st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+          }
+        }
+        f32x4 m;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[q] = act_t<AACT>(o[q], a.aact, a.aalpha);
+        f32x4 x = m, cin;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) cin[q] = fk::dpp_ror1(carry[J][q]);
+#if FW_ABL
+        if (!(a.rtabl & 32))
+#endif
+#pragma unroll
+          for (int it = 0; it < MAXL; ++it) {
+            f32x4 y;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) y[q] = fk::dpp_shr1(cin[q], x[q]);
+            x = start ? m : y + m;
+          }
+        if (endok && pok[J] && st_ok) {
+          if constexpr (PREC == 1) {
+            reinterpret_cast<uint2*>(a.SO)[sbase + 16 * J] = fk::bf4_pack(x[0], x[1], x[2], x[3]);
+          } else {
+            reinterpret_cast<f32x4*>(a.SO)[sbase + 16 * J] = x;
+            st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+          }
+        }
+        carry[J] = x;
+      }
+    }
+    // row tile rt is stored: fp32 -- its accumulators take the next tile's residual rows; bf16 --
+    // they restart at zero
+    if constexpr (PREC == 0) {
+      if (load_next) {
+        int e = en;
+#if FW_ABL
+        if (a.rtabl & 8) e = 0;
+#endif
+        const int64_t rb = (int64_t)(e >= 0 ? e : 0) * hc;
+#pragma unroll
+        for (int J = 0; J < NCT; ++J)
+          st.acc[rt][J] = reinterpret_cast<const f32x4*>(a.H)[rb + (pok[J] ? pc0 + 16 * J : 0)];
+      } else {
+#pragma unroll
+        for (int J = 0; J < NCT; ++J) st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    } else {
+#pragma unroll
+      for (int J = 0; J < NCT; ++J) st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  });
+}
+
+// LDS-staged epilogue (FW_EPI_LDS).  Per column tile J of the wave: every row tile's unit computes
+// H_out (stored as a 16-B row piece) and writes aact(H_out) into the wave's stage (128 rows x 16
+// columns); then lanes take (node, 4-column piece) items -- 16 nodes x 4 pieces per round -- and sum
+// the node's consecutive rows left to right from the stage (the order of CPU scatter_add_, so the
+// same bits as the scan), S_out as 16-B pieces (4 lanes: one 64-B segment of the node row).  No
+// cross-wave sync: each wave owns its stage and its copy of the tile's node list.  Per unit this is
+// ~12 VALU + one ds_write instead of the scan's ~40 VALU.
+template <int NCT, int PREC, int AACT>
+__device__ __forceinline__ void fw_epilogue_lds(St<NCT, PREC>& st, const Args& a, const int4* em, int n, bool resid,
+                                                bool load_next, const int4* em_next) {
+  const int hc = st.hc;
+  const int pc0 = 4 * st.wave + st.g16;  // column tile J: piece pc0 + 16 J
+  // the tile's node list: start rows of its nodes (ascending), ns = count, start[ns] = n
+  {
+    const int l = st.lane;
+    const bool s0 = l < n && (em[l].z & fk::kFlagStart), s1 = l + 64 < n && (em[l + 64].z & fk::kFlagStart);
+    const unsigned long long m0 = __ballot(s0), m1 = __ballot(s1);
+    const unsigned long long below = (1ull << l) - 1ull;
+    const int c0 = __popcll(m0);
+    if (s0) st.nlist[__popcll(m0 & below)] = l;
+    if (s1) st.nlist[c0 + __popcll(m1 & below)] = l + 64;
+    if (l == 0) {
+      const int ns = c0 + __popcll(m1);
+      st.nlist[ns] = n;
+      st.nlist[kRows + 2] = ns;
+    }
+  }
+  // the rows' edges (this tile) and the next tile's, one per row tile
+  int e_row[kRT], e_nxt[kRT];
+#pragma unroll
+  for (int rt = 0; rt < kRT; ++rt) {
+    e_row[rt] = em[16 * rt + st.fr].x;
+    e_nxt[rt] = load_next ? em_next[16 * rt + st.fr].x : 0;
+  }
+  uint2 rr[kRT], rr_n[kRT];
+  if constexpr (PREC == 1) {
+#pragma unroll
+    for (int rt = 0; rt < kRT; ++rt)
+      rr_n[rt] = resid ? reinterpret_cast<const uint2*>(a.H)[(int64_t)(e_row[rt] >= 0 ? e_row[rt] : 0) * hc + pc0]
+                       : uint2{0u, 0u};
+  }
+  const int ns = st.nlist[kRows + 2];
+  fk::sfor<NCT>([&](auto Jc) {
+    constexpr int J = decltype(Jc)::value;
+    const int pc = pc0 + 16 * J;
+    const bool pok = pc < hc;
+    const f32x4 bj = (a.bias && pok) ? *reinterpret_cast<const f32x4*>(st.lbias + 4 * pc) : f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (PREC == 1) {
+#pragma unroll
+      for (int rt = 0; rt < kRT; ++rt) rr[rt] = rr_n[rt];
+      if constexpr (J + 1 < NCT) {  // the next column tile's residual pieces, in flight across this one
+        const int pn = pc + 16 < hc ? pc + 16 : 0;
+#pragma unroll
+        for (int rt = 0; rt < kRT; ++rt)
+          rr_n[rt] = resid ? reinterpret_cast<const uint2*>(a.H)[(int64_t)(e_row[rt] >= 0 ? e_row[rt] : 0) * hc + pn]
+                           : uint2{0u, 0u};
+      }
+    }
+#if FW_ABL
+    const bool st_ok = !(a.rtabl & 4);
+#else
+    constexpr bool st_ok = true;
+#endif
+    // (1) units: H_out, aact(H_out) into the stage
+#pragma unroll
+    for (int rt = 0; rt < kRT; ++rt) {
+      if (16 * rt < n) {
+        f32x4 o;
+        uint2 ob = uint2{0u, 0u};
+        if constexpr (PREC == 1) {
+          const float4 r = fk::bf4_widen(uint4{rr[rt].x, rr[rt].y, 0u, 0u});
+          ob = fk::bf4_pack((st.acc[rt][J][0] + bj[0]) + r.x, (st.acc[rt][J][1] + bj[1]) + r.y,
+                            (st.acc[rt][J][2] + bj[2]) + r.z, (st.acc[rt][J][3] + bj[3]) + r.w);
+          const float4 w = fk::bf4_widen(uint4{ob.x, ob.y, 0u, 0u});
+          o = f32x4{w.x, w.y, w.z, w.w};
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[rt][J][q], st.inv, bj[q]);
+        }
+        const int e = e_row[rt];
+        if (e >= 0 && pok && st_ok) {
+          if constexpr (PREC == 1) {
+            reinterpret_cast<uint2*>(a.O)[(int64_t)e * hc + pc] = ob;
+          } else {
+            reinterpret_cast<f32x4*>(a.O)[(int64_t)e * hc + pc] = o;
+            st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+          }
+        }
+        f32x4 m;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[q] = act_t<AACT>(o[q], a.aact, a.aalpha);
+        *reinterpret_cast<f32x4*>(st.stage + (16 * rt + st.fr) * kStagePitch + 4 * st.g16) = m;
+      }
+      // row tile rt of column tile J is out: fp32 -- the accumulators take the next tile's residual
+      // rows; bf16 -- they restart at zero
+      if constexpr (PREC == 0) {
+        if (load_next) {
+          int en = e_nxt[rt];
+#if FW_ABL
+          if (a.rtabl & 8) en = 0;
+#endif
+          st.acc[rt][J] = reinterpret_cast<const f32x4*>(a.H)[(int64_t)(en >= 0 ? en : 0) * hc + (pok ? pc : 0)];
+        } else {
+          st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+      } else {
+        st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    // (2) nodes: lane = (node 16 r + (lane >> 2), piece lane & 3), rows summed left to right (the
+    // stage rows were written by other lanes of this wave: LDS keeps a wave's operations in order)
+    __builtin_amdgcn_wave_barrier();
+    const int p4 = st.lane & 3;
+    const int pcn = 4 * (st.wave + 4 * J) + p4;  // the item's 4-column piece of the row
+    for (int k = st.lane >> 2; k < ns; k += 16) {
+      const int r0 = st.nlist[k], r1 = st.nlist[k + 1];
+      f32x4 x = *reinterpret_cast<const f32x4*>(st.stage + r0 * kStagePitch + 4 * p4);
+      for (int r = r0 + 1; r < r1; ++r) x = x + *reinterpret_cast<const f32x4*>(st.stage + r * kStagePitch + 4 * p4);
+      const int4 re = em[r1 - 1];  // the node's last row: its id and end flag (hub rows carry none)
+      if ((re.z & fk::kFlagEnd) && re.x >= 0 && pcn < hc && st_ok) {
+        if constexpr (PREC == 1) {
+          reinterpret_cast<uint2*>(a.SO)[(int64_t)re.y * hc + pcn] = fk::bf4_pack(x[0], x[1], x[2], x[3]);
+        } else {
+          reinterpret_cast<f32x4*>(a.SO)[(int64_t)re.y * hc + pcn] = x;
+          st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next column tile rewrites the stage
+  });
+}
+
 template <int NCT, int PREC, int ACT, int AACT, int MAXL>
 __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int tstride, int ntl) {
   auto tile = [&](int i) __attribute__((always_inline)) { return t0 + (i < ntl ? i : ntl - 1) * tstride; };
@@ -343,9 +651,12 @@ __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int ts
   st.hv = a.hv;
   st.hc = a.h / 4;
   st.NT = a.NT;
+  st.rtabl = a.rtabl;
   st.abuf = smem;
   st.emap = reinterpret_cast<int4*>(smem + 2 * buf_bytes(PREC));
   st.lbias = reinterpret_cast<float*>(smem + 2 * buf_bytes(PREC) + kEmapB);
+  st.stage = reinterpret_cast<float*>(smem + 2 * buf_bytes(PREC) + kEmapB + kBiasB + st.wave * kStageB);
+  st.nlist = reinterpret_cast<int*>(smem + 2 * buf_bytes(PREC) + kEmapB + kBiasB + 4 * kStageB) + st.wave * kNodeListN;
   for (int c = tid; c < a.h; c += kThreads) {
     float b = 0.f;
     if (a.bias) {
@@ -452,8 +763,22 @@ __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int ts
 #endif
     const bool more = i + 1 < ntl;
     const int4* em = st.emap + (i % kEmaps) * kRows;
+#if FW_ABL
+    if (a.rtabl & 64) {  // no epilogue: the K loops alone (accumulators restart at zero)
+#pragma unroll
+      for (int rt = 0; rt < kRT; ++rt)
+#pragma unroll
+        for (int j = 0; j < NCT; ++j) st.acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    } else
+#endif
+#if FW_EPI_LDS
+    fw_epilogue_lds<NCT, PREC, AACT>(st, a, em, n_cur, resid, resid && more, st.emap + ((i + 1) % kEmaps) * kRows);
+#elif FW_EPI_RT
+    fw_epilogue_rt<NCT, PREC, AACT, MAXL>(st, a, em, n_cur, resid, resid && more, st.emap + ((i + 1) % kEmaps) * kRows);
+#else
     if (PREC == 1 && resid) fw_resid_bf(st, a, em, 0, rr0);
     fw_epi_col<0, NCT, PREC, AACT, MAXL>(st, a, em, n_cur, resid, resid && more, i + 1, rr0, rr1);
+#endif
 #if FW_STAMP
     ts_e += __builtin_amdgcn_s_memtime() - ts_1;
 #endif
