@@ -71,6 +71,12 @@
 #ifndef FK_STAMP
 #define FK_STAMP 0
 #endif
+// FK_EPI4 (A/B): the node sums of the two-workgroup 64-row walk from a per-wave LDS stage
+// (fk_epilogue4) instead of the DPP scan -- bit-identical, measured slower (124.0 vs 118.3 us at
+// config 2: the node pass diverges and the scan's VALU is not what binds this walk)
+#ifndef FK_EPI4
+#define FK_EPI4 0
+#endif
 // FK_GATHER2 (A/B builds): 1 = 64-B contiguous row reads per gather instruction (fp32, 128-row tiles)
 #ifndef FK_GATHER2
 #define FK_GATHER2 0
@@ -259,9 +265,11 @@ struct State {
   float sA, sAW, inv;
   int rtabl;  // FK_RTABL builds: Args::rtabl
   char* abuf;
-  float* stage;  // FK_EPI3: 128-row x 128-column output staging (pitch kSP floats)
+  float* stage;  // FK_EPI3: 128-row x 128-column output staging (pitch kSP floats); FK_EPI4: this wave's
+                 // column-tile stage (RT x 16 rows x 16 columns, pitch kSP4)
   float* lbias;  // FK_EPI3: the bias in fp32 (h floats), loaded once
-  int* nlist;    // FK_EPI3: node segments of the current tile (start rows, count at [kNlistN])
+  int* nlist;    // FK_EPI3: node segments of the current tile (start rows, count at [kNlistN]); FK_EPI4:
+                 // this wave's copy
   int4* emap;
   __amdgpu_buffer_rsrc_t wrsrc;
 };
@@ -875,6 +883,97 @@ __device__ __forceinline__ void fk_epilogue3(State<RT, CT, GD, PREC, NW>& st, co
   fk_epi3_group<0, RT, CT, AACT, GD, PREC>(st, a, em, c, n, resid, rr);
 }
 
+// --------------------------------------------------------------------------- LDS node reduction
+// FK_EPI4 (the two-workgroup 64-row walk, sum aggregation): per column tile J of the wave, the row
+// tiles' units store H_out and write aact(H_out) into the wave's own stage; then lanes take (node,
+// 4-column piece) items, 16 nodes x 4 pieces per round, and sum each node's consecutive rows left to
+// right (CPU scatter_add_ order: the same bits as the DPP scan), S_out as 16-B pieces.  No barrier:
+// each wave owns its stage and its copy of the tile's node list.  ~12 VALU + one ds_write per unit
+// against the scan's ~40 VALU.
+constexpr int kSP4 = 20;  // stage pitch (floats): conflict-free 16-B row writes
+constexpr int kNl4 = 68;  // node list ints per wave: start rows [0, ns], ns at [66]
+
+template <int J, int RT, int CT, int AACT, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_epi4_col(State<RT, CT, GD, PREC, NW>& st, const Args& a, const int4* em, int c,
+                                            int n, int ns, bool load_next, int i_next, int c_next) {
+  const int ct = c * st.CTC + st.wave + NW * J;
+  const int hc = st.hc;
+  if (ct < st.NT) {
+    const int pc = 4 * ct + st.g16;
+    const bool pok = pc < hc;
+    const f32x4 bj = (a.bias && pok) ? *reinterpret_cast<const f32x4*>(st.lbias + 4 * pc) : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) {
+      if (16 * rt < n) {
+        f32x4 o;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[rt][J][q], st.inv, bj[q]);
+        const int e = em[16 * rt + st.fr].x;
+        if (e >= 0 && pok) {
+          reinterpret_cast<f32x4*>(a.O)[(int64_t)e * hc + pc] = o;
+          st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
+        }
+        f32x4 m;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) m[q] = act_t<AACT>(o[q], a.aact, a.aalpha);
+        *reinterpret_cast<f32x4*>(st.stage + (16 * rt + st.fr) * kSP4 + 4 * st.g16) = m;
+      }
+    }
+  }
+  // column tile J is out: its accumulators take the next (tile, chunk)'s residual rows, in flight
+  // across the node pass below
+  if (load_next) {
+    fk_resid_load(st, a, i_next, c_next, J);
+  } else {
+#pragma unroll
+    for (int rt = 0; rt < RT; ++rt) st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  if (ct < st.NT) {
+    __builtin_amdgcn_wave_barrier();  // the stage rows come from other lanes of this wave (LDS keeps order)
+    const int p4 = st.lane & 3;
+    const int pcn = 4 * ct + p4;
+    for (int k = st.lane >> 2; k < ns; k += 16) {
+      const int r0 = st.nlist[k], r1 = st.nlist[k + 1];
+      f32x4 x = *reinterpret_cast<const f32x4*>(st.stage + r0 * kSP4 + 4 * p4);
+      for (int r = r0 + 1; r < r1; ++r) x = x + *reinterpret_cast<const f32x4*>(st.stage + r * kSP4 + 4 * p4);
+      const int4 re = em[r1 - 1];  // the node's last row: its id and end flag (hub rows carry none)
+      if ((re.z & kFlagEnd) && re.x >= 0 && pcn < hc) {
+        reinterpret_cast<f32x4*>(a.SO)[(int64_t)re.y * hc + pcn] = x;
+        st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next column tile rewrites the stage
+  }
+  if constexpr (J + 1 < CT)
+    fk_epi4_col<J + 1, RT, CT, AACT, GD, PREC, NW>(st, a, em, c, n, ns, load_next, i_next, c_next);
+}
+
+template <int RT, int CT, int AACT, int GD, int PREC, int NW>
+__device__ __forceinline__ void fk_epilogue4(State<RT, CT, GD, PREC, NW>& st, const Args& a, int i, int c, int n,
+                                             bool load_next, int i_next, int c_next) {
+  static_assert(RT * 16 <= 64, "FK_EPI4: tiles of at most 64 rows (one ballot)");
+  using St = State<RT, CT, GD, PREC, NW>;
+  const int4* em = st.emap + (i % kEmaps) * St::ROWS;
+  // the wave's stage and node list behind the bias (wave-uniform addresses)
+  char* e4 = st.abuf + 2 * St::kBufB + kEmaps * St::ROWS * 16 + kLbiasB;
+  st.stage = reinterpret_cast<float*>(e4 + st.wave * (16 * RT * kSP4 * 4));
+  st.nlist = reinterpret_cast<int*>(e4 + NW * (16 * RT * kSP4 * 4)) + st.wave * kNl4;
+  {  // the tile's node list: start rows of its nodes (ascending), ns = count, start[ns] = n
+    const int l = st.lane;
+    const bool s0 = l < n && (em[l].z & kFlagStart);
+    const unsigned long long m0 = __ballot(s0);
+    if (s0) st.nlist[__popcll(m0 & ((1ull << l) - 1ull))] = l;
+    if (l == 0) {
+      const int ns = __popcll(m0);
+      st.nlist[ns] = n;
+      st.nlist[66] = ns;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  const int ns = st.nlist[66];
+  fk_epi4_col<0, RT, CT, AACT, GD, PREC, NW>(st, a, em, c, n, ns, load_next, i_next, c_next);
+}
+
 __device__ __forceinline__ void fk_barrier() {
   // LDS writes of this step retired, then the workgroup barrier (vector-memory loads stay in flight)
   __syncthreads();
@@ -895,8 +994,11 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   constexpr int kEmapB = kEmaps * ROWS * 16;
   static_assert(RT == NW || (RT == 4 && NW == 8), "row tiles per wave mapping");
   constexpr bool EPI3 = FK_EPI3 && RT == 8 && NW == 8;
+  // FK_EPI4: the LDS node reduction on the two-workgroup 64-row walk (fp32, sum)
+  constexpr bool EPI4 = FK_EPI4 && NW == 4 && RT == 4 && PREC == 0 && SUMONLY && MAXL > 1;
   constexpr bool LB = fk_lds_bias(NW, RT, PREC);
-  constexpr int kExtraB = EPI3 ? kStageB + kLbiasB + kNlistB : (LB ? kLbiasB : 0);
+  constexpr int kEpi4B = EPI4 ? NW * (16 * RT * kSP4 * 4 + kNl4 * 4) : 0;
+  constexpr int kExtraB = (EPI3 ? kStageB + kLbiasB + kNlistB : (LB ? kLbiasB : 0)) + kEpi4B;
   __shared__ __attribute__((aligned(16))) uint4 smem[(2 * St::kBufB + kEmapB + kExtraB) / 16];
 
   // XCD-aware persistent walk (blocks b and b + nxcd share an L2): each XCD one contiguous chunk
@@ -943,6 +1045,7 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   st.stage = reinterpret_cast<float*>(st.abuf + 2 * St::kBufB + kEmapB);
   st.lbias = st.stage + (EPI3 ? kStageB / 4 : 0);
   st.nlist = reinterpret_cast<int*>(st.lbias + (EPI3 ? kLbiasB / 4 : 0));
+
   if constexpr (EPI3 || LB) {  // the bias in fp32, once (h <= 512)
     for (int q = tid; q < a.h; q += 64 * NW) {
       float b = 0.f;
@@ -1140,6 +1243,7 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
     const int i_next = last_c ? (i + 1 < ntl ? i + 1 : i) : i, c_next = last_c ? 0 : c + 1;
     if constexpr ((ABL & 8) == 0) {
       if constexpr (EPI3) fk_epilogue3<RT, CT, AACT, GD>(st, a, i, c, n_cur, resid);
+      else if constexpr (EPI4) fk_epilogue4<RT, CT, AACT, GD>(st, a, i, c, n_cur, resid, i_next, c_next);
       else fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
       stamp(4);
     }
