@@ -67,6 +67,9 @@ __global__ void __launch_bounds__(256) segment_reduce_scalar(
 }
 
 // ---------------- fused init + first aggregation ----------------
+#ifndef NT_INIT_MASK
+#define NT_INIT_MASK 1  // A/B: 0 = every lane loads every pass (pieces past the row read piece 0)
+#endif
 
 template <int R, int ACT>
 __global__ void __launch_bounds__(256) init_aggregate_vec4(
@@ -133,8 +136,12 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int q = 0; q < PPL; ++q) {
-            a[u][q] = Xv[sv[u] * hv + cc[q]];
-            x[u][q] = Xe[ed[u] * hv + cc[q]];
+            if (q == 0 || ok[q] || !NT_INIT_MASK) {  // pieces past the row: no load (exec-masked)
+              a[u][q] = Xv[sv[u] * hv + cc[q]];
+              x[u][q] = Xe[ed[u] * hv + cc[q]];
+            } else {
+              a[u][q] = x[u][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
           }
 #pragma unroll
         for (int u = 0; u < 4; ++u)

@@ -49,6 +49,10 @@ from notorch_amd._lib import NT_ACT_IDENTITY
 from notorch_amd.data.models.graph import DeviceLayout
 
 _IDENTITY = (NT_ACT_IDENTITY, 0.0)
+_RELU = (_lib.NT_ACT_RELU, 0.0)
+# backward: dA and dS = sum_src dA in one fused launch (dA_plan); NT_FUSED_DA=0 keeps dense_matmul +
+# segment_reduce (A/B)
+_FUSED_DA = os.environ.get("NT_FUSED_DA", "1") != "0"
 # fp32 weight gradient: "kernel" (nt_dmpnn_weight_grad_fk for h <= 320, else nt_dmpnn_weight_grad),
 # "kernel6" (nt_dmpnn_weight_grad, bf16x6) or "library" (message + split-K library GEMM)
 _WGRAD_DEFAULT = "kernel"
@@ -648,6 +652,32 @@ class LayerwiseBlockFunction(torch.autograd.Function):
         return (*res_inputs, None, None, None, None, None, None, None, None, None, *res_params)
 
 
+def dA_plan(lay: DeviceLayout, src: Tensor, V: int, E: int, src_ptr: Tensor, src_perm: Tensor):
+    """The backward's fused dA + dS launch plan (fp32): node-aligned 64-row tiles over the src-sorted
+    edge order (the transpose of the forward's dst plan) and its row table {edge, e, -1, src node}:
+    A[e] = G[e] (the "src" row of the gather is the edge itself, nothing subtracted), so the layer
+    kernel's fused mode computes dA = G W and dS[v] = sum_{e: src[e] = v} dA[e] in ascending edge order
+    (the bits of segment_reduce(dA, src CSR)).  None when some node has more than
+    MAX_FUSED_IN_DEGREE out-edges (then dense_matmul + segment_reduce).  Cached on the layout."""
+    key = (src.data_ptr(), src.numel(), V)
+    hit = getattr(lay, "da_plan", None)
+    if hit is None or hit[0] != key:
+        plan = None
+        if E > 0 and V > 0:
+            outdeg = src_ptr[1:] - src_ptr[:-1]
+            dmax, dmin = int(outdeg.max()), int(outdeg.min())
+            if dmax <= MAX_FUSED_IN_DEGREE:
+                tile_ptr, ntiles, dsts = K.tile_plan(src_ptr, E, dmax, rows=64, ncu=K.PLAN_NCU)
+                ident = torch.arange(E, dtype=torch.int64, device=src.device)
+                none = torch.full((E,), -1, dtype=torch.int64, device=src.device)
+                # the gathered operand is G (E rows): the row table's bound on the "src" index is E
+                rt = K.dmpnn_row_table(src_perm, dsts, ident, none, E)
+                plan = ((tile_ptr, ntiles, dsts), dmax, dmin == 0, ident, none, rt)
+        hit = (key, plan)
+        lay.da_plan = hit
+    return hit[1]
+
+
 def backward_layout(lay: DeviceLayout, src: Tensor, rev: Tensor, V: int, E: int) -> tuple:
     """(src_ptr, src_perm, rev_ptr, rev_perm): the CSRs of the two gathers' transposes (scatter by
     src into nodes, scatter by rev_index into edges), built once per graph and cached on its layout."""
@@ -746,14 +776,28 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             dWs[l] = _weight_grad(Gu, A)
             dbs[l] = Gu.sum(0)
             del A
-        if fk_dense:
-            dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous(), fk_only=True), amax=gmax)
-        elif bf16_kernels and os.environ.get("NT_BF16_DA", "kernel") == "kernel":  # the bf16 layer kernel
-            dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous()))  # without gathers
+        dap = dA_plan(lay, src, V, E, src_ptr, src_perm) if (fk_dense and _FUSED_DA) else None
+        if dap is not None:
+            # dA = G W and dS = sum_src dA in one launch of the layer kernel's fused mode over the
+            # src-sorted plan (A[e] = G[e]: rev = -1 everywhere, so act and H are never applied)
+            plan3, dmax, zf, ident, none, rt = dap
+            # gmax = (0, max|G|): [0] is never written (the bound of the H term, absent here), so the
+            # split scale is dense_matmul's
+            amx = gmax
+            dS = (torch.zeros if zf else torch.empty)(V, h, dtype=Gu.dtype, device=Gu.device)
+            dA, dS = K.dmpnn_update_fused(Gu, Gu, ident, none, K.pack_weights(W.t().contiguous(), fk_only=True), None,
+                                          residual=False, act=_RELU, plan=plan3, tile_rows=64, max_in_degree=dmax,
+                                          perm=src_perm, reduce="sum", agg_act=_IDENTITY, amax_in=amx,
+                                          row_table=rt, S_out=dS)
         else:
-            dA = torch.mm(Gu, W)
+            if fk_dense:
+                dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous(), fk_only=True), amax=gmax)
+            elif bf16_kernels and os.environ.get("NT_BF16_DA", "kernel") == "kernel":  # the bf16 layer kernel
+                dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous()))  # without gathers
+            else:
+                dA = torch.mm(Gu, W)
+            dS = K.segment_reduce(dA, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY)
         del Gu
-        dS = K.segment_reduce(dA, src_ptr, src_perm, V, reduce="sum", act=_IDENTITY)
         gmax_cur = gbuf[l - 1] if fp32 and l > 0 else None
         g1 = None if gmax_cur is None else gmax_cur[1:2]
         if maxmin:  # chemprop.py:39 with scatter_max / scatter_min: the arg of act(H_l) per node

@@ -37,6 +37,7 @@ def main():
     p.add_argument("--rounds", type=int, default=5)
     p.add_argument("--rows", type=int, default=128)
     p.add_argument("--agg", default="relu")
+    p.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     a = p.parse_args()
     lib = _lib.load()
     setfw = getattr(lib, "nt_debug_set_fw")
@@ -45,17 +46,20 @@ def main():
     V, E, h = G.num_nodes, G.num_edges, a.h
     lay = G._nt_layout
     gen = torch.Generator(device="cuda").manual_seed(0)
-    H = torch.randn(E, h, device="cuda", generator=gen)
-    S = torch.randn(V, h, device="cuda", generator=gen)
-    W = torch.randn(h, h, device="cuda", generator=gen) / 17
-    b = torch.randn(h, device="cuda", generator=gen)
+    dt = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+    H = torch.randn(E, h, device="cuda", generator=gen).to(dt)
+    S = torch.randn(V, h, device="cuda", generator=gen).to(dt)
+    W = (torch.randn(h, h, device="cuda", generator=gen) / 17).to(dt)
+    b = torch.randn(h, device="cuda", generator=gen).to(dt)
     Wp = K.pack_weights(W)
     src, rev = G.edge_index[0].contiguous(), G.rev_index
     relu = K.act_code(torch.nn.ReLU())
     agg = relu if a.agg == "relu" else K.act_code(torch.nn.Identity())
-    amax = torch.zeros(2, device="cuda")
-    K.absmax(H, amax[0:1])
-    K.absmax(S, amax[1:2])
+    amax = None
+    if dt == torch.float32:
+        amax = torch.zeros(2, device="cuda")
+        K.absmax(H, amax[0:1])
+        K.absmax(S, amax[1:2])
     deg = int((lay.dst_ptr[1:] - lay.dst_ptr[:-1]).max().item())
     plan = K.tile_plan(lay.dst_ptr, E, deg, rows=a.rows, ncu=K.PLAN_NCU)
     rt = K.dmpnn_row_table(lay.dst_perm, plan[2], src, rev, V)
@@ -64,7 +68,8 @@ def main():
     outs = {}
 
     def run(v, out, S2, am):
-        pl, rtab, rows = (plan64, rt64, 64) if v == 2 else (plan, rt, a.rows)
+        # bf16: the default bf16 kernel takes 64-row plans only, so v = 0 is the 64-row walk too
+        pl, rtab, rows = (plan64, rt64, 64) if (v == 2 or (v == 0 and dt != torch.float32)) else (plan, rt, a.rows)
 
         def f():
             setfw(1 if v == 1 else 0)
@@ -75,7 +80,8 @@ def main():
 
     fns = {}
     for v in (0, 1, 2):
-        out, S2, am = torch.full_like(H, float("nan")), torch.full_like(S, float("nan")), torch.zeros(2, device="cuda")
+        out, S2 = torch.full_like(H, float("nan")), torch.full_like(S, float("nan"))
+        am = torch.zeros(2, device="cuda") if dt == torch.float32 else None
         outs[v] = (out, S2, am)
         fns[v] = run(v, out, S2, am)
         fns[v]()
@@ -83,7 +89,9 @@ def main():
     st = K.device_status() if hasattr(K, "device_status") else None
     print(f"{a.kind}-{a.mols} rev={a.rev} V={V} E={E} h={h} deg={deg} tiles={plan[1]} status={st}")
     (o0, s0, m0), (o1, s1, m1) = outs[0], outs[1]
-    eqH, eqS, eqM = torch.equal(o0, o1), torch.equal(s0, s1), torch.equal(m0, m1)
+    eqH, eqS = torch.equal(o0, o1), torch.equal(s0, s1)
+    eqM = m0 is None or torch.equal(m0, m1)
+    o0, o1, s0, s1 = o0.float(), o1.float(), s0.float(), s1.float()
     dH = (o0 - o1).abs().max().item() / o0.abs().max().item()
     dS = (s0 - s1).abs().max().item() / s0.abs().max().item()
     print(f"bit-exact H {eqH} S {eqS} amax {eqM}  (norm max diff H {dH:.3e} S {dS:.3e}; nan {o1.isnan().sum().item()})")
@@ -107,7 +115,9 @@ def main():
         c0 = diff[r0].nonzero().flatten()[:4].tolist()
         print(f"  row {r0}: fk {o0[r0, c0].tolist()} fw {o1[r0, c0].tolist()}")
     o2, s2, m2 = outs[2]
-    print(f"fk 64-row walk bit-exact vs 128-row: H {torch.equal(o0, o2)} S {torch.equal(s0, s2)}")
+    print(f"fk 64-row walk bit-exact vs 128-row: H {torch.equal(o0, o2.float())} S {torch.equal(s0, s2.float())}; "
+          f"fw vs 64-row: H {torch.equal(o1, o2.float())} S {torch.equal(s1, s2.float())} "
+          f"(norm max diff H {(o1 - o2.float()).abs().max().item() / o2.float().abs().max().item():.3e})")
     res = {0: [], 1: [], 2: []}
     for _ in range(a.rounds):
         for v in (0, 1, 2):
