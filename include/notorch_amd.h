@@ -213,6 +213,15 @@ NT_API int nt_dmpnn_pack_weight(const void* W, int64_t nlayers, int64_t h, int d
 NT_API int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h, void* Wp, void* stream);
 
 /*
+ * nt_dmpnn_pack_weight_fk for nlayers (<= 16) separate h x h weights in one launch pair: W, Wp (and
+ * WpT) are HOST arrays of nlayers device pointers; WpT may be NULL, else WpT[l] receives the fk
+ * image of W[l]^T (the backward's dA = G W, chemprop.py:41 under autograd) read from W[l] directly.
+ * Same bytes as nt_dmpnn_pack_weight_fk of W[l] and of W[l].t().contiguous().
+ */
+NT_API int nt_dmpnn_pack_weights_fk(const void* const* W, int64_t nlayers, int64_t h, void* const* Wp,
+                                    void* const* WpT, void* stream);
+
+/*
  * One fused D-MPNN layer (ChempropLayer.forward, chemprop.py:28-43, wrapped by Residual,
  * residual.py:27-28), for every directed edge e:
  *   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b

@@ -53,6 +53,9 @@ int fk_tile_rows(int64_t h, int act, int reduce, int aact, bool fused);
 int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in, float* amax_out,
                      const int32_t* tile_ptr, int64_t ntiles, int tile_rows, int max_in_degree,
                      const void* row_table, int reduce, int aact, float aalpha, float* S_out);
+// fk images of nlayers separate weights (<= 16) and optionally of their transposes, one launch pair
+int fk_pack_multi(const float* const* W, int64_t nlayers, int64_t h, char* const* img, char* const* imgT,
+                  hipStream_t stream);
 int fk_row_table(const int32_t* perm, const int32_t* dsts, const int64_t* src, const int64_t* rev, int64_t V,
                  int64_t E, void* out, hipStream_t stream);
 int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_t img_stride, void* img,

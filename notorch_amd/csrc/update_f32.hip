@@ -615,6 +615,27 @@ extern "C" int nt_dmpnn_pack_weight_fk(const void* W, int64_t nlayers, int64_t h
                  as_stream(stream_));
 }
 
+extern "C" int nt_dmpnn_pack_weights_fk(const void* const* W, int64_t nlayers, int64_t h, void* const* Wp,
+                                        void* const* WpT, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(nlayers >= 0 && nlayers <= 16 && h > 0 && h <= 8192, NT_EINVAL, "bad sizes (nlayers <= 16, h <= 8192)");
+  if (nlayers == 0) return NT_OK;
+  NT_REQUIRE(W && Wp, NT_EINVAL, "NULL pointer array");
+  NT_REQUIRE(has_fk_image(h), NT_EUNSUPPORTED, "the fk image needs h % 4 == 0 (or h > 512)");
+  const float* w[16];
+  char* img[16];
+  char* imgT[16];
+  for (int64_t l = 0; l < nlayers; ++l) {
+    NT_REQUIRE(W[l] && Wp[l] && aligned16(Wp[l]) && (WpT == nullptr || (WpT[l] && aligned16(WpT[l]))), NT_EINVAL,
+               "NULL or misaligned pointer");
+    w[l] = (const float*)W[l];
+    img[l] = (char*)Wp[l] + fk_offset(h);
+    imgT[l] = WpT ? (char*)WpT[l] + fk_offset(h) : nullptr;
+  }
+  return fk_pack_multi(w, nlayers, h, img, WpT ? imgT : nullptr, as_stream(stream_));
+}
+
 extern "C" int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, int agg_act) {
   if (h <= 0) return 0;
   if (dtype == NT_BF16) {

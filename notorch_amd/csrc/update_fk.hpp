@@ -1366,6 +1366,75 @@ __global__ void __launch_bounds__(256) pack_fk_kernel(const float* __restrict__ 
   *reinterpret_cast<f16x8*>(out + kImgHdr + q * 16) = v;
 }
 
+// Multi-layer pack: the fk images of up to kPackMax layer weights (separate tensors) and, optionally,
+// the images of their transposes (the backward's dA = G W), in one launch pair: the scale partials
+// of layer l (max|W| = max|W^T|) go into both headers; a fragment slot of the W^T image reads W
+// transposed (no transposed copy of W).  Same values as pack_fk_{scale_,}kernel on W and on
+// W.t().contiguous().
+constexpr int kPackMax = 16;
+struct PackPtrs {
+  const float* W[kPackMax];
+  char* img[kPackMax];
+  char* imgT[kPackMax];  // may be NULL
+};
+
+__global__ void __launch_bounds__(256) pack_fk_scale_multi(PackPtrs p, int64_t h) {
+  const float* Wl = p.W[blockIdx.y];
+  const int64_t n = h * h, per = (n + kScaleParts - 1) / kScaleParts;
+  const int64_t lo = blockIdx.x * per, hi = lo + per < n ? lo + per : n;
+  __shared__ float red[4];
+  float m = 0.f;
+  for (int64_t q = lo + threadIdx.x; q < hi; q += 256) m = fmaxf(m, fabsf(Wl[q]));
+  m = wave_max(m);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const float r = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+    reinterpret_cast<float*>(p.img[blockIdx.y])[1 + blockIdx.x] = r;
+    if (p.imgT[blockIdx.y]) reinterpret_cast<float*>(p.imgT[blockIdx.y])[1 + blockIdx.x] = r;
+  }
+}
+
+__global__ void __launch_bounds__(256) pack_fk_multi(PackPtrs p, int64_t h, int KS, int NT) {
+  const int layer = blockIdx.y;
+  const float* Wl = p.W[layer];
+  char* out = p.img[layer];
+  char* outT = p.imgT[layer];
+  float mw = 0.f;
+#pragma unroll
+  for (int i = 1; i <= kScaleParts; ++i) mw = fmaxf(mw, reinterpret_cast<const float*>(out)[i]);
+  const float sW = ldexpf(1.f, scale_exp(mw));
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    *reinterpret_cast<float*>(out) = sW;
+    if (outT) *reinterpret_cast<float*>(outT) = sW;
+  }
+  const int64_t slots = (int64_t)KS * NT * 2 * 64;
+  const int64_t q = blockIdx.x * 256LL + threadIdx.x;
+  if (q >= slots) return;
+  const int l = (int)(q & 63);
+  const int64_t blk = q >> 6;
+  const int part = (int)(blk & 1);
+  const int64_t sc = blk >> 1;
+  const int ct = (int)(sc % NT), s = (int)(sc / NT);
+  const int col = 16 * ct + (l & 15);
+  f16x8 v, vt;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int k = 32 * s + 8 * (l >> 4) + j;
+    const bool in = col < h && k < h;
+    const float w = in ? Wl[(int64_t)col * h + k] * sW : 0.f;
+    const _Float16 w0 = (_Float16)w;
+    v[j] = part == 0 ? w0 : (_Float16)(w - (float)w0);
+    if (outT) {  // W^T[col][k] = W[k][col]
+      const float wt = in ? Wl[(int64_t)k * h + col] * sW : 0.f;
+      const _Float16 t0 = (_Float16)wt;
+      vt[j] = part == 0 ? t0 : (_Float16)(wt - (float)t0);
+    }
+  }
+  *reinterpret_cast<f16x8*>(out + kImgHdr + q * 16) = v;
+  if (outT) *reinterpret_cast<f16x8*>(outT + kImgHdr + q * 16) = vt;
+}
+
 // atomically max |X| over n elements into *out (non-negative float bit order)
 __global__ void __launch_bounds__(256) absmax_kernel(const float* __restrict__ X, int64_t n,
                                                      float* __restrict__ out) {

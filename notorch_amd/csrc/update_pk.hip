@@ -1185,6 +1185,23 @@ int fk_pack(const float* W, int64_t nlayers, int64_t h, int64_t w_stride, int64_
   return NT_OK;
 }
 
+int fk_pack_multi(const float* const* W, int64_t nlayers, int64_t h, char* const* img, char* const* imgT,
+                  hipStream_t stream) {
+  const int KS = fk::ks_for(h), NT = fk::nt_for(h);
+  const int64_t slots = (int64_t)KS * NT * 2 * 64;
+  fk::PackPtrs p;
+  for (int l = 0; l < fk::kPackMax; ++l) {
+    p.W[l] = l < nlayers ? W[l] : nullptr;
+    p.img[l] = l < nlayers ? img[l] : nullptr;
+    p.imgT[l] = (l < nlayers && imgT) ? imgT[l] : nullptr;
+  }
+  fk::pack_fk_scale_multi<<<dim3(fk::kScaleParts, (unsigned)nlayers), 256, 0, stream>>>(p, h);
+  NT_LAUNCH_CHECK();
+  fk::pack_fk_multi<<<dim3((unsigned)((slots + 255) / 256), (unsigned)nlayers), 256, 0, stream>>>(p, h, KS, NT);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
 int fk_row_table(const int32_t* perm, const int32_t* dsts, const int64_t* src, const int64_t* rev, int64_t V,
                  int64_t E, void* out, hipStream_t stream) {
   if (E <= 0) return NT_OK;

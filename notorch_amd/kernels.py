@@ -7,6 +7,8 @@ Each wrapper validates device / dtype / shape / contiguity up front (raising ``T
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 from torch import Tensor
 
@@ -384,6 +386,31 @@ def pack_weights(W: Tensor, *, fk_only: bool = False) -> Tensor:
     else:
         _run(dev, lib.nt_dmpnn_pack_weight, _ptr(W3), L, h, code, _ptr(Wp), _stream(dev))
     return Wp[0] if W.dim() == 2 else Wp
+
+
+def pack_weights_fk_multi(Ws: Sequence[Tensor], with_t: bool = False) -> tuple[list[Tensor], list[Tensor] | None]:
+    """fp32: the fk images (nt_dmpnn_pack_weight_fk's part of pack_weights) of up to 16 separate h x h
+    weights and, with ``with_t``, of their transposes (the backward's dA image), in one launch pair
+    (nt_dmpnn_pack_weights_fk).  Bytes equal pack_weights(W, fk_only=True) and
+    pack_weights(W.t().contiguous(), fk_only=True)."""
+    if not Ws:
+        return [], ([] if with_t else None)
+    dev = _require_device(*Ws)
+    h = Ws[0].shape[0]
+    for W in Ws:
+        _require_f32("weight", W)
+        if W.shape != (h, h) or not W.is_contiguous():
+            raise ValueError("pack_weights_fk_multi: contiguous h x h weights of one hidden size")
+    if len(Ws) > 16:
+        raise ValueError("pack_weights_fk_multi: at most 16 weights per call")
+    n = packed_weight_numel(h, torch.float32)
+    imgs = [torch.empty(n, dtype=torch.float32, device=dev) for _ in Ws]
+    imgsT = [torch.empty(n, dtype=torch.float32, device=dev) for _ in Ws] if with_t else None
+    arr = ctypes.c_void_p * len(Ws)
+    _run(dev, _lib.load().nt_dmpnn_pack_weights_fk, arr(*[W.data_ptr() for W in Ws]), len(Ws), h,
+         arr(*[t.data_ptr() for t in imgs]), None if imgsT is None else arr(*[t.data_ptr() for t in imgsT]),
+         _stream(dev))
+    return imgs, imgsT
 
 
 def dmpnn_update(

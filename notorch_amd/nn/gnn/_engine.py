@@ -188,6 +188,28 @@ def hub_info(lay: DeviceLayout):
     return lay.hubs or None
 
 
+def zero_rows_needed(lay: DeviceLayout, src: Tensor, V: int) -> tuple[bool, bool, bool]:
+    """Which node-row outputs need a zero fill because no row of a plan writes them: (out, mid, bwd) =
+    some node has in-degree 0 (the final node output: torch_scatter's empty segment is 0), some node
+    has in-degree 0 and out-degree > 0 (an intermediate S row that a later S[src] gather reads), some
+    node has out-degree 0 and in-degree > 0 (a dS row that the edge backward's dS[dst] reads).  Bond
+    graphs have in-degree = out-degree, so only `out` can hold (isolated atoms).  Cached; the first
+    call syncs once unless the in-degrees alone decide it."""
+    key = (src.data_ptr(), src.numel(), V)
+    hit = getattr(lay, "zero_rows", None)
+    if hit is None or hit[0] != key:
+        zf_out = V > 0 and _degree_range(lay)[1] == 0
+        mid = bwd = False
+        if zf_out or (V > 0 and src.numel() > 0):
+            indeg = (lay.dst_ptr[1:] - lay.dst_ptr[:-1])
+            outdeg = torch.bincount(src, minlength=V)[:V]
+            t = torch.stack([((indeg == 0) & (outdeg > 0)).any(), ((outdeg == 0) & (indeg > 0)).any()]).cpu()
+            mid, bwd = bool(t[0]), bool(t[1])
+        hit = (key, (zf_out, mid, bwd))
+        lay.zero_rows = hit
+    return hit[1]
+
+
 def fused_plan(lay: DeviceLayout, V: int, E: int, rows: int = 64, dtype: torch.dtype = torch.float32):
     """Tile plan of the fused update for this layout with tiles of at most ``rows`` (64 or 128) rows,
     balanced to whole rounds over PLAN_NCU CUs, as (tile_ptr, ntiles, dst_sorted, zero_fill), cached on
@@ -260,19 +282,60 @@ def _fused_enabled() -> bool:
 _PACKED: dict[int, tuple] = {}
 
 
-def pack_layer_weights(weights: Sequence[Tensor]) -> list[Tensor]:
-    """One packed MFMA image per layer; shared layers (same tensor) are packed once."""
-    out = []
-    for W in weights:
+def _multi_packable(W: Tensor) -> bool:
+    """fp32 weights whose image is the fk image alone (shipping library, h % 4 == 0): packed in one
+    launch pair for all layers (nt_dmpnn_pack_weights_fk), with the backward's W^T image alongside."""
+    return (W.dtype == torch.float32 and W.dim() == 2 and W.shape[0] % 4 == 0 and W.is_contiguous()
+            and not _lib.DIAG)
+
+
+def pack_layer_weights(weights: Sequence[Tensor], with_t: bool = False) -> list[Tensor]:
+    """One packed MFMA image per layer; shared layers (same tensor) are packed once.  with_t (a
+    training forward, fp32): the images of W^T too (packed_transpose), from the same launch pair."""
+    out: list = [None] * len(weights)
+    stale = []  # (index, W) needing a pack
+    for i, W in enumerate(weights):
         key = (W.data_ptr(), W._version, tuple(W.shape), W.device)
         hit = _PACKED.get(id(W))
-        if hit is None or hit[0]() is not W or hit[1] != key:
-            wid = id(W)
-            ref = weakref.ref(W, lambda _r, wid=wid: _PACKED.pop(wid, None))
-            hit = (ref, key, K.pack_weights(W.detach()))
-            _PACKED[wid] = hit
-        out.append(hit[2])
+        if hit is None or hit[0]() is not W or hit[1] != key or (with_t and hit[3] is None):
+            stale.append((i, W))
+        else:
+            out[i] = hit[2]
+    multi = [(i, W) for i, W in stale if _multi_packable(W)]
+    uniq: dict = {}
+    for i, W in multi:
+        uniq.setdefault(id(W), W)
+    groups: dict = {}
+    for W in uniq.values():
+        groups.setdefault((W.shape[0], W.device), []).append(W)
+    for ws in groups.values():
+        for c in range(0, len(ws), 16):
+            chunk = ws[c:c + 16]
+            imgs, imgsT = K.pack_weights_fk_multi([W.detach() for W in chunk], with_t=with_t)
+            for j, W in enumerate(chunk):
+                _remember(W, imgs[j], None if imgsT is None else imgsT[j])
+    for i, W in stale:
+        if not _multi_packable(W):
+            _remember(W, K.pack_weights(W.detach()), None)
+        out[i] = _PACKED[id(W)][2]
     return out
+
+
+def _remember(W: Tensor, Wp: Tensor, WpT: Optional[Tensor]) -> None:
+    key = (W.data_ptr(), W._version, tuple(W.shape), W.device)
+    wid = id(W)
+    ref = weakref.ref(W, lambda _r, wid=wid: _PACKED.pop(wid, None))
+    _PACKED[wid] = (ref, key, Wp, WpT)
+
+
+def packed_transpose(W: Tensor) -> Tensor:
+    """The fk image of W^T (the backward's dA = G W): the one the training forward packed beside W's
+    if W is unchanged since, else packed now."""
+    key = (W.data_ptr(), W._version, tuple(W.shape), W.device)
+    hit = _PACKED.get(id(W))
+    if hit is not None and hit[0]() is W and hit[1] == key and hit[3] is not None:
+        return hit[3]
+    return K.pack_weights(W.detach().t().contiguous(), fk_only=True)
 
 
 def block_forward(
@@ -406,7 +469,8 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
     if d == 0:
         node = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, _IDENTITY, chunks)
         return node, H, []
-    Wps = pack_layer_weights(weights)
+    # a training forward (states kept for the kernel backward) packs the dA images of W^T alongside
+    Wps = pack_layer_weights(weights, with_t=keep_states and H.dtype == torch.float32)
     E, h = H.shape
     fp32 = H.dtype == torch.float32
     if fp32 and amax is None:
@@ -480,6 +544,9 @@ def row_table(lay: DeviceLayout, dsts: Tensor, src: Tensor, rev: Tensor, V: int)
 
 def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, residual, keep_states, amax):
     tile_ptr, ntiles, dsts, zero_fill = plan
+    # zero fills only where a row is read or returned (zero_rows_needed): the last layer's node output;
+    # an intermediate S only if some source node has no in-edge
+    zf_out, zf_mid, _ = zero_rows_needed(lay, src, S.shape[0]) if zero_fill else (False, False, False)
     d = len(Wps)
     rt = row_table(lay, dsts, src, rev, S.shape[0])
     states = []
@@ -498,7 +565,8 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
         Hn, Sn = K.dmpnn_update_fused(
             H, S, src, rev, Wps[l], None if biases[l] is None else biases[l].detach(),
             residual=residual, act=act, plan=(tile_ptr, ntiles, dsts), tile_rows=rows, max_in_degree=maxdeg,
-            perm=lay.dst_perm, reduce=reduce, agg_act=_IDENTITY if last else act, zero_fill=zero_fill,
+            perm=lay.dst_perm, reduce=reduce, agg_act=_IDENTITY if last else act,
+            zero_fill=zf_out if last else zf_mid,
             amax_in=None if amax is None else amax[l],
             amax_out=None if (amax is None or last) else amax[l + 1],  # row d has no reader
             row_table=rt, out=spare_H, S_out=None if last else spare_S,
@@ -672,7 +740,9 @@ def dA_plan(lay: DeviceLayout, src: Tensor, V: int, E: int, src_ptr: Tensor, src
                 none = torch.full((E,), -1, dtype=torch.int64, device=src.device)
                 # the gathered operand is G (E rows): the row table's bound on the "src" index is E
                 rt = K.dmpnn_row_table(src_perm, dsts, ident, none, E)
-                plan = ((tile_ptr, ntiles, dsts), dmax, dmin == 0, ident, none, rt)
+                # dS rows no tile writes (out-degree 0) need zeros only if an edge's dS[dst] reads them
+                zf = dmin == 0 and zero_rows_needed(lay, src, V)[2]
+                plan = ((tile_ptr, ntiles, dsts), dmax, zf, ident, none, rt)
         hit = (key, plan)
         lay.da_plan = hit
     return hit[1]
@@ -785,13 +855,13 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             # split scale is dense_matmul's
             amx = gmax
             dS = (torch.zeros if zf else torch.empty)(V, h, dtype=Gu.dtype, device=Gu.device)
-            dA, dS = K.dmpnn_update_fused(Gu, Gu, ident, none, K.pack_weights(W.t().contiguous(), fk_only=True), None,
+            dA, dS = K.dmpnn_update_fused(Gu, Gu, ident, none, packed_transpose(weights[l]), None,
                                           residual=False, act=_RELU, plan=plan3, tile_rows=64, max_in_degree=dmax,
                                           perm=src_perm, reduce="sum", agg_act=_IDENTITY, amax_in=amx,
                                           row_table=rt, S_out=dS)
         else:
             if fk_dense:
-                dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous(), fk_only=True), amax=gmax)
+                dA = K.dense_matmul(Gu, packed_transpose(weights[l]), amax=gmax)
             elif bf16_kernels and os.environ.get("NT_BF16_DA", "kernel") == "kernel":  # the bf16 layer kernel
                 dA = K.dense_matmul(Gu, K.pack_weights(W.t().contiguous()))  # without gathers
             else:

@@ -20,7 +20,7 @@ def test_header_declares_the_boundary():
     assert set(names) == {
         "nt_abi_version", "nt_last_error", "nt_last_kernel", "nt_csr_workspace_bytes", "nt_csr_build", "nt_dropout_residual",
         "nt_dmpnn_init", "nt_segment_reduce", "nt_dmpnn_packed_weight_bytes",
-        "nt_dmpnn_pack_weight", "nt_dmpnn_update", "nt_dmpnn_tile_count", "nt_dmpnn_tile_plan",
+        "nt_dmpnn_pack_weight", "nt_dmpnn_pack_weights_fk", "nt_dmpnn_update", "nt_dmpnn_tile_count", "nt_dmpnn_tile_plan",
         "nt_dmpnn_update_fused", "nt_dmpnn_message", "nt_dmpnn_edge_backward", "nt_gather_rows",
         "nt_embed_bag", "nt_dmpnn_init_embed", "nt_node_scores", "nt_softmax_pool",
         "nt_collate_graphs", "nt_segment_reduce_chunked", "nt_device_status", "nt_device_status_reset",

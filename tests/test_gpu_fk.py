@@ -286,6 +286,24 @@ def test_pack_fk_only_matches_full_pack():
         assert_parity(a, X.double() @ W.double().t(), FP32_NORM_TOL, f"dense h={h}")
 
 
+@pytest.mark.parametrize("h", [300, 36, 640])
+def test_multi_pack_with_transposes_matches_single_packs(h):
+    """nt_dmpnn_pack_weights_fk (all layers and their transposes in one launch pair, the training
+    forward's pack) gives the bytes of the fk image of each W and of W.t().contiguous()."""
+    K = _K()
+    g = torch.Generator().manual_seed(h)
+    Ws = [(torch.randn(h, h, generator=g) * 0.05).to(DEV) for _ in range(3)]
+    imgs, imgsT = K.pack_weights_fk_multi(Ws, with_t=True)
+    n = K.packed_weight_numel(h, torch.float32)
+    for W, a, at in zip(Ws, imgs, imgsT):
+        ref, refT = K.pack_weights(W, fk_only=True), K.pack_weights(W.t().contiguous(), fk_only=True)
+        X = torch.randn(129, h, generator=g).to(DEV)
+        assert torch.equal(K.dense_matmul(X, a), K.dense_matmul(X, ref)), h
+        assert torch.equal(K.dense_matmul(X, at), K.dense_matmul(X, refT)), h
+    only, none = K.pack_weights_fk_multi(Ws[:1])
+    assert none is None and only[0].numel() == n
+
+
 @pytest.mark.parametrize("h", [300, 128, 600])
 @pytest.mark.parametrize("reduce", ["sum", "max"])
 def test_fused_init_exact_on_skewed_degrees(h, reduce):
