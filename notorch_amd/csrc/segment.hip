@@ -18,6 +18,9 @@
 namespace nt {
 
 // ---------------- segment reduce ----------------
+#ifndef NT_SEG_WAVE
+#define NT_SEG_WAVE 1  // A/B: 0 = the thread-per-piece kernel for every row width
+#endif
 template <int R, int ACT>
 __global__ void __launch_bounds__(256) segment_reduce_vec4(
     const float4* __restrict__ X, const int32_t* __restrict__ seg_ptr,
@@ -43,6 +46,58 @@ __global__ void __launch_bounds__(256) segment_reduce_vec4(
       r.push(act4_t<ACT>(X[row * hv + c], act, alpha));
     }
     out[t] = r.result();
+  }
+}
+
+// One wave per segment (rows of >= 32 pieces): the segment bounds and the row indices are
+// wave-uniform scalar loads, lane l takes row pieces l + 64 q (q < PPL), four rows in flight, pushed
+// in ascending order -- the same bits as segment_reduce_vec4.  Pieces past the row load nothing.
+template <int R, int ACT, int PPL>
+__global__ void __launch_bounds__(256) segment_reduce_wave(
+    const float4* __restrict__ X, const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm,
+    int64_t nseg, int64_t hv, int act, float alpha, float4* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t s = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+       s < nseg; s += nwaves) {
+    const int32_t b = seg_ptr[s], e = seg_ptr[s + 1];
+    for (int64_t c0 = 0; c0 < hv; c0 += 64 * PPL) {
+      int64_t cc[PPL];
+      bool ok[PPL];
+      Reducer4<R> r[PPL];
+#pragma unroll
+      for (int q = 0; q < PPL; ++q) {
+        const int64_t c = c0 + lane + 64 * q;
+        ok[q] = c < hv;
+        cc[q] = ok[q] ? c : 0;
+        r[q].init();
+      }
+      int32_t j = b;
+      for (; j + 4 <= e; j += 4) {
+        int64_t row[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) row[u] = perm ? (int64_t)perm[j + u] : (int64_t)(j + u);
+        float4 x[4][PPL];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < PPL; ++q)
+            x[u][q] = ok[q] ? X[row[u] * hv + cc[q]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < PPL; ++q) r[q].push(act4_t<ACT>(x[u][q], act, alpha));
+      }
+      for (; j < e; ++j) {
+        const int64_t row = perm ? (int64_t)perm[j] : (int64_t)j;
+#pragma unroll
+        for (int q = 0; q < PPL; ++q)
+          r[q].push(act4_t<ACT>(ok[q] ? X[row * hv + cc[q]] : make_float4(0.f, 0.f, 0.f, 0.f), act, alpha));
+      }
+#pragma unroll
+      for (int q = 0; q < PPL; ++q)
+        if (ok[q]) out[s * hv + cc[q]] = r[q].result();
+    }
   }
 }
 
@@ -272,7 +327,19 @@ extern "C" int nt_segment_reduce(const void* X, const int32_t* seg_ptr, const in
   if (dtype == NT_BF16)
     return launch_segment_reduce_bf16(X, seg_ptr, perm, nseg, h, reduce, act, act_alpha, out, stream);
   const bool vec = (h % 4 == 0) && aligned16(X) && aligned16(out);
-  if (vec) {
+  if (vec && h / 4 >= 32 && NT_SEG_WAVE) {  // rows of >= 32 pieces: a wave per segment
+    const int64_t hv = h / 4;
+    const int grid = grid_for(nseg * 64, 256, 256 * 8);
+    if (hv <= 64) {
+      NT_DISPATCH_RA(reduce, act,
+                     (segment_reduce_wave<R_, A_, 1><<<grid, 256, 0, stream>>>(
+                         (const float4*)X, seg_ptr, perm, nseg, hv, act, act_alpha, (float4*)out)));
+    } else {
+      NT_DISPATCH_RA(reduce, act,
+                     (segment_reduce_wave<R_, A_, 2><<<grid, 256, 0, stream>>>(
+                         (const float4*)X, seg_ptr, perm, nseg, hv, act, act_alpha, (float4*)out)));
+    }
+  } else if (vec) {
     const int64_t hv = h / 4;
     const int grid = grid_for(nseg * hv, 256, 256 * 32);
     NT_DISPATCH_RA(reduce, act,
