@@ -3,7 +3,7 @@ HIPCC   ?= /opt/rocm/bin/hipcc
 ARCH    ?= gfx950
 SRC_DIR := notorch_amd/csrc
 SRCS    := $(wildcard $(SRC_DIR)/*.hip)
-HDRS    := $(wildcard $(SRC_DIR)/*.hpp) include/notorch_amd.h
+HDRS    := $(wildcard $(SRC_DIR)/*.hpp) $(wildcard $(SRC_DIR)/diag/*.hpp) include/notorch_amd.h
 FLAGS   := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result \
            -fvisibility=hidden -DNT_BUILD
 # DIAG=1: the diagnostic library (A/B kernel variants, ablation and stamp builds selected by NT_*
@@ -15,6 +15,8 @@ ifeq ($(DIAG),1)
 OUT     := notorch_amd/lib/libnotorch_amd_diag.so
 BDIR    := build_diag
 FLAGS   += -DNT_DIAG
+# csrc/diag/: kernels of the diagnostic library only (A/B variants superseded in the shipping one)
+SRCS    += $(wildcard $(SRC_DIR)/diag/*.hip)
 else ifneq ($(VARIANT),)
 OUT     := notorch_amd/lib/libnotorch_amd_$(VARIANT).so
 BDIR    := build_$(VARIANT)
@@ -23,11 +25,12 @@ OUT     := notorch_amd/lib/libnotorch_amd.so
 BDIR    := build
 endif
 OBJS    := $(patsubst $(SRC_DIR)/%.hip,$(BDIR)/%.o,$(SRCS))
+DIAG_OBJS := $(filter $(BDIR)/diag/%,$(OBJS))
 
 all: $(OUT)
 
 $(BDIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
-	@mkdir -p $(BDIR)
+	@mkdir -p $(dir $@)
 	$(HIPCC) $(FLAGS) -c $< -o $@
 
 $(OUT): $(OBJS)

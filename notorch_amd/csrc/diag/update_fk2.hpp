@@ -27,7 +27,7 @@
 // after the K loop (x = (acc / (s_A s_W) + b) + H[e]) instead of in the accumulator.
 #pragma once
 
-#include "update_fk.hpp"
+#include "../update_fk.hpp"
 
 namespace nt {
 namespace fk {

@@ -29,7 +29,7 @@
 // lane l holds row l & 15 of a row tile, columns 4 (l >> 4) .. + 3 of a column tile.
 #pragma once
 
-#include "update_fk.hpp"
+#include "../update_fk.hpp"
 
 #ifndef FW_ONE_PATH
 #define FW_ONE_PATH 0

@@ -24,8 +24,8 @@
 
 #include <type_traits>
 
-#include "common.hpp"
-#include "update.hpp"
+#include "../common.hpp"
+#include "../update.hpp"
 
 #ifdef NT_DIAG  // A/B variant: superseded by update_fk_kernel in the shipping library
 namespace nt {

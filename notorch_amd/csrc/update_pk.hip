@@ -44,9 +44,9 @@ __device__ unsigned long long g_pk_stamps[10];
 // the fp16x3 layer kernel (shares g_pk_timeout: bit 1 = bounded wait gave up, bit 2 = a tile larger
 // than the fk kernel's row capacity)
 #include "update_fk.hpp"
-#include "update_fw.hpp"  // one wave per SIMD variant of the fused layer
 #ifdef NT_DIAG
-#include "update_fk2.hpp"  // A/B: LDS-staged output variant (NT_FK=2)
+#include "diag/update_fk2.hpp"  // A/B: LDS-staged output variant (NT_FK=2)
+#include "diag/update_fw.hpp"   // A/B: one-wave-per-SIMD walk of the fused layer (NT_FK_FW=1)
 #endif
 
 namespace nt {
@@ -885,6 +885,7 @@ int launch_fk_nw4(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
                      : launch_fk_nw4_t<NT_ACT_IDENTITY, 16>(a, grid, stream);
 }
 
+#ifdef NT_DIAG
 // A/B switch: NT_FK_FW=1 / 0 (read once per process) selects update_fw_kernel where it applies;
 // nt_debug_set_fw overrides it (tests and kernel benches switch within one process)
 int g_fw_override = -1;
@@ -932,6 +933,8 @@ int launch_fw(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
                      : launch_fw_t<NT_ACT_IDENTITY, 16>(a, grid, stream);
 }
 
+#endif  // NT_DIAG
+
 // 64-row tiles: every other combination (any reduce, any aggregation act) and h > 384
 template <int CT>
 int launch_fk_narrow(const fk::Args& a, int maxl, int grid, hipStream_t stream) {
@@ -966,10 +969,15 @@ int fk_tile_rows(int64_t h, int act, int reduce, int aact, bool fused) {
 // the one-wave-per-SIMD walk for this fused layer (A/B switch fw_selected): fp32 257 <= h <= 320,
 // bf16 449 <= h <= 512 (eight column tiles per wave), relu layers with a relu / identity sum
 bool fw_active(int64_t h, int dtype, int act, int reduce, int aact) {
+#ifdef NT_DIAG
   if (!fw_selected() || act != NT_ACT_RELU || reduce != NT_SUM || !(aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY))
     return false;
   const int nt = fk::nt_for(h);
   return dtype == NT_BF16 ? (h % 8 == 0 && nt > 28 && nt <= fw::kMaxNTb) : (nt > 16 && nt <= fw::kMaxNT);
+#else
+  (void)h, (void)dtype, (void)act, (void)reduce, (void)aact;
+  return false;  // the fw walk is an A/B of the diagnostic library only
+#endif
 }
 
 int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in, float* amax_out,
@@ -1040,10 +1048,12 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
     return launch_fk2(a, grid, u.stream);
   }
 #endif
+#ifdef NT_DIAG
   if (fused && fw_active(u.h, NT_F32, u.act, reduce, aact)) {
     a.nchunks = 1;
     return launch_fw(a, maxl, grid, u.stream);
   }
+#endif
   if (fused && tile_rows <= 64 && fk_nw4(u.h, true, u.act, reduce, aact)) {
     a.nchunks = 1;
     const int g4 = a.ntiles < 2 * cu_count() ? a.ntiles : 2 * cu_count();
@@ -1149,7 +1159,9 @@ int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* 
     return launch_fkb_t<-1, NT_ACT_IDENTITY, true, 1>(a, grid, u.stream);
   }
   const int maxl = max_in_degree - 1;
+#ifdef NT_DIAG
   if (fw_active(u.h, NT_BF16, u.act, reduce, aact)) return launch_fwb(a, maxl, grid, u.stream);
+#endif
   {
     if (bf16_kernel_env() == 2 && tile_rows <= 64 && relu && reduce == NT_SUM &&
         (aact == NT_ACT_RELU || aact == NT_ACT_IDENTITY)) {
@@ -1229,7 +1241,7 @@ int amax_fill(float* ws, const float* H, int64_t nh, const float* S, int64_t ns,
 
 }  // namespace nt
 
-#if FW_STAMP
+#if defined(NT_DIAG) && FW_STAMP
 // A/B builds only (FW_STAMP): read and reset the fw kernel's stamp sums (6 values)
 extern "C" __attribute__((visibility("default"))) int nt_debug_fw_stamps(unsigned long long* out6) {
   if (hipMemcpyFromSymbol(out6, HIP_SYMBOL(nt::g_pk_stamps), 6 * sizeof(unsigned long long), 0,
@@ -1251,12 +1263,14 @@ extern "C" __attribute__((visibility("default"))) int nt_debug_fk_stamps(unsigne
 }
 #endif
 
-// Debug-only (not part of include/notorch_amd.h): select the fp32 fused layer walk (-1: the default,
-// 0: update_fk_kernel, 1: update_fw_kernel where it applies)
+#ifdef NT_DIAG
+// Debug-only (diagnostic library, not part of include/notorch_amd.h): select the fp32 fused layer
+// walk (-1: the default, 0: update_fk_kernel, 1: update_fw_kernel where it applies)
 extern "C" __attribute__((visibility("default"))) int nt_debug_set_fw(int v) {
   nt::g_fw_override = v;
   return 0;
 }
+#endif
 
 extern "C" __attribute__((visibility("default"))) int nt_device_status(uint32_t* host_out,
                                                                       void* stream) {
