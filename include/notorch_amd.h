@@ -163,6 +163,16 @@ NT_API int nt_segment_reduce(const void* X, const int32_t* seg_ptr, const int32_
                       void* stream);
 
 /*
+ * The per-layer message aggregation under the name SURVEY §8(b) gives it (chemprop.py:36-39):
+ *   S_out[v] = reduce_{j in [row_ptr[v], row_ptr[v+1])} relu(H[perm[j]])
+ * over the dst CSR of nt_csr_build; = nt_segment_reduce(H, row_ptr, perm, V, h, reduce,
+ * NT_ACT_RELU, 0, dtype, S_out, stream).  The shipping forward fuses this into nt_dmpnn_init and
+ * nt_dmpnn_update_fused; this entry point serves callers that run the layer unfused.
+ */
+NT_API int nt_dmpnn_aggregate(const void* H, const int32_t* row_ptr, const int32_t* perm, int64_t V,
+                              int64_t h, int reduce, int dtype, void* S_out, void* stream);
+
+/*
  * nt_segment_reduce for segments of very different lengths (polymer hubs):
  * the CSR positions are cut into chunks [chunk_pos[k], chunk_pos[k+1]) of bounded length that never
  * straddle a segment; segment s owns chunks [chunk_ptr[s], chunk_ptr[s+1]) (none when empty).

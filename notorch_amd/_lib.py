@@ -74,6 +74,7 @@ SIGNATURES: dict[str, tuple] = {
         _c_int,
         [_vp, _vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp],
     ),
+    "nt_dmpnn_aggregate": (_c_int, [_vp, _vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _vp, _vp]),
     "nt_segment_reduce_chunked": (
         _c_int,
         [_vp, _vp, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp, _vp],

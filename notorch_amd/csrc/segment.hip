@@ -355,6 +355,11 @@ extern "C" int nt_segment_reduce(const void* X, const int32_t* seg_ptr, const in
   return NT_OK;
 }
 
+extern "C" int nt_dmpnn_aggregate(const void* H, const int32_t* row_ptr, const int32_t* perm, int64_t V,
+                                  int64_t h, int reduce, int dtype, void* S_out, void* stream) {
+  return nt_segment_reduce(H, row_ptr, perm, V, h, reduce, NT_ACT_RELU, 0.f, dtype, S_out, stream);
+}
+
 namespace nt {
 int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);  // update_pk.hip
 }

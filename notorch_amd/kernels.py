@@ -19,6 +19,7 @@ __all__ = [
     "csr_build",
     "dmpnn_init",
     "segment_reduce",
+    "dmpnn_aggregate",
     "chunk_plan",
     "pack_weights",
     "dmpnn_update",
@@ -262,6 +263,25 @@ def segment_reduce(
          _ptr(X), _ptr(seg_ptr), _ptr(perm), nseg, h, reduce_code(reduce), act[0], act[1], code,
          _ptr(out), _stream(dev))
     return out
+
+
+def dmpnn_aggregate(H: Tensor, row_ptr: Tensor, perm: Tensor, V: int, *, reduce: str = "sum") -> Tensor:
+    """S[v] = reduce over v's in-edges of relu(H[e]) (chemprop.py:36-39) through nt_dmpnn_aggregate
+    (the dst CSR of nt_csr_build: row_ptr int32[V+1], perm int32[E])."""
+    dev = _require_device(H, row_ptr, perm)
+    code = _require_feat("H", H)
+    if H.dim() != 2:
+        raise ValueError("H must be 2-D")
+    if row_ptr.dtype != torch.int32 or row_ptr.numel() != V + 1 or not row_ptr.is_contiguous():
+        raise ValueError("row_ptr must be contiguous int32 of length V + 1")
+    if perm.dtype != torch.int32 or perm.numel() != H.shape[0] or not perm.is_contiguous():
+        raise ValueError("perm must be contiguous int32 with one entry per row of H")
+    S = torch.empty(V, H.shape[1], dtype=H.dtype, device=dev)
+    if H.shape[0] == 0:
+        return S.zero_()
+    _run(dev, _lib.load().nt_dmpnn_aggregate,
+         _ptr(H), _ptr(row_ptr), _ptr(perm), V, H.shape[1], reduce_code(reduce), code, _ptr(S), _stream(dev))
+    return S
 
 
 CHUNK_ROWS = 32  # rows per chunk of the load-balanced segment reduce

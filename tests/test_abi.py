@@ -19,7 +19,7 @@ def test_header_declares_the_boundary():
     names = header_functions()
     assert set(names) == {
         "nt_abi_version", "nt_last_error", "nt_last_kernel", "nt_csr_workspace_bytes", "nt_csr_build", "nt_dropout_residual",
-        "nt_dmpnn_init", "nt_segment_reduce", "nt_dmpnn_packed_weight_bytes",
+        "nt_dmpnn_init", "nt_segment_reduce", "nt_dmpnn_aggregate", "nt_dmpnn_packed_weight_bytes",
         "nt_dmpnn_pack_weight", "nt_dmpnn_pack_weights_fk", "nt_dmpnn_update", "nt_dmpnn_tile_count", "nt_dmpnn_tile_plan",
         "nt_dmpnn_update_fused", "nt_dmpnn_message", "nt_dmpnn_edge_backward", "nt_gather_rows",
         "nt_embed_bag", "nt_dmpnn_init_embed", "nt_node_scores", "nt_softmax_pool",
@@ -68,6 +68,10 @@ def test_abi_version_and_errors_without_gpu():
     assert rc == 1 and b"NULL" in lib.nt_last_error()  # bf16 is implemented: validation reached
     rc = lib.nt_segment_reduce(None, None, None, 4, 8, 0, 0, 0.0, 7, None, None)
     assert rc == 3  # NT_EUNSUPPORTED: unknown dtype code
+    rc = lib.nt_dmpnn_aggregate(None, None, None, 4, 8, 9, 0, None, None)  # = nt_segment_reduce, act relu
+    assert rc == 1 and b"reduce" in lib.nt_last_error()
+    rc = lib.nt_dmpnn_aggregate(None, None, None, 4, 8, 0, 0, None, None)
+    assert rc == 1 and b"NULL" in lib.nt_last_error()
     assert lib.nt_dmpnn_packed_weight_bytes(512, 1) == 16 * 32 * 64 * 16  # bf16 image, h = 512
     rc = lib.nt_dmpnn_message(None, None, None, None, 4, 8, 16, 1, 0.0, 1, None, None)
     assert rc == 1 and b"NULL" in lib.nt_last_error()  # bf16 backward is implemented

@@ -83,6 +83,23 @@ def test_segment_reduce(reduce, h, act):
         assert torch.equal(out.cpu(), ref)
 
 
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
+@pytest.mark.parametrize("h", [300, 13])
+def test_dmpnn_aggregate(reduce, h):
+    """nt_dmpnn_aggregate (SURVEY §8(b)'s name): the layer's relu + scatter (chemprop.py:36-39)."""
+    K = _K()
+    G = _graph_tensors("qm9", 64, seed=2)
+    E, V = G.edge_index.shape[1], G.num_nodes
+    X = torch.randn(E, h)
+    dst = G.edge_index[1]
+    seg_ptr, perm = K.csr_build(dst.to(DEV), V)
+    out = K.dmpnn_aggregate(X.to(DEV), seg_ptr, perm, V, reduce=reduce)
+    ref = dmpnn_ref.scatter(torch.relu(X), dst, V, reduce)
+    assert_parity(out, ref, 1e-6, f"dmpnn_aggregate {reduce}")
+    if reduce in ("sum", "max", "min"):  # ascending-edge-order accumulation: bit-exact
+        assert torch.equal(out.cpu(), ref)
+
+
 def test_segment_reduce_empty_segments():
     K = _K()
     X = torch.randn(3, 8)

@@ -46,6 +46,7 @@ def main():
     Wp = K.pack_weights(W)
     src, rev = G.edge_index[0].contiguous(), G.rev_index
     out = torch.empty_like(H)
+    H2 = torch.randn(E, h, device="cuda", generator=gen)
     S2 = torch.empty_like(S)
     relu = K.act_code(torch.nn.ReLU())
     amax = torch.zeros(2, device="cuda")
@@ -95,6 +96,10 @@ def main():
         "fk_noamax": lambda: K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=plans[128][0], tile_rows=128,
                                                   max_in_degree=deg, perm=lay.dst_perm, agg_act=relu, amax_in=amax,
                                                   row_table=plans[128][1], out=out, S_out=S2),
+        "init_only": lambda: K.dmpnn_init(Xv, H, src, act=relu, amax=amax_out),
+        # bandwidth ceilings of the init's traffic: E-row copy (2 rows / edge), E-row add (3 rows / edge)
+        "copy": lambda: out.copy_(H),
+        "add": lambda: torch.add(H, H2, out=out),
         "absmax": lambda: K.absmax(H, amax_out[0:1]),
         "pack": lambda: K.pack_weights(W),
     }
@@ -117,8 +122,9 @@ def main():
         extra = ""
         if name.startswith("fk"):
             extra = f"  {2 * E * h * h / (med * 1e-6) / 1e12:.1f} TF/s fp32-equivalent"
-        elif name in ("init", "absmax"):
-            rows = {"init": 3 * E + V, "absmax": E}[name]
+        elif name in ("init", "init_noamax", "init_only", "copy", "add", "absmax"):
+            rows = {"init": 3 * E + V, "init_noamax": 3 * E + V, "init_only": 3 * E, "copy": 2 * E, "add": 3 * E,
+                    "absmax": E}[name]
             extra = f"  {rows * h * 4 / (med * 1e-6) / 1e9:.0f} GB/s alg"
         print(f"{name:12s} median {med:8.1f} us  min {mn:8.1f} us{extra}")
 
