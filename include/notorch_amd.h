@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define NT_ABI_VERSION 6
+#define NT_ABI_VERSION 7
 
 #if defined(NT_BUILD)
 #define NT_API __attribute__((visibility("default")))
@@ -177,28 +177,34 @@ NT_API int nt_dmpnn_aggregate(const void* H, const int32_t* row_ptr, const int32
  * the CSR positions are cut into chunks [chunk_pos[k], chunk_pos[k+1]) of bounded length that never
  * straddle a segment; segment s owns chunks [chunk_ptr[s], chunk_ptr[s+1]) (none when empty).
  * Pass 1 reduces every chunk into partial (nchunks x h fp32 workspace), pass 2 combines each
- * segment's partials in chunk order (mean divides by seg_ptr's count).  Same result as
+ * segment's partials in chunk order (mean divides by seg_ptr's count).  chunk_seg (int32[nchunks],
+ * may be NULL): s when chunk k is segment s's only chunk, else -1 — pass 1 then stores that segment's
+ * result directly and pass 2 runs only over the ncomb segments listed in comb_seg (int32[ncomb]: every
+ * segment with != 1 chunk); with chunk_seg NULL pass 2 runs over all nseg segments and comb_seg /
+ * ncomb are ignored.  (ABI 7)  Same result as
  * nt_segment_reduce up to fp32 reassociation at chunk boundaries; deterministic.  amax_out (fp32,
  * may be NULL; ignored for bf16): one zero-filled device float raised to max|out| (the first layer's
  * split scale on hub graphs).
  */
 NT_API int nt_segment_reduce_chunked(const void* X, const int32_t* perm, const int32_t* chunk_pos,
-                                     int64_t nchunks, const int32_t* chunk_ptr,
-                                     const int32_t* seg_ptr, int64_t nseg, int64_t h, int reduce,
-                                     int act, float act_alpha, int dtype, float* partial, void* out,
-                                     float* amax_out, void* stream);
+                                     int64_t nchunks, const int32_t* chunk_ptr, const int32_t* chunk_seg,
+                                     const int32_t* comb_seg, int64_t ncomb, const int32_t* seg_ptr,
+                                     int64_t nseg, int64_t h, int reduce, int act, float act_alpha,
+                                     int dtype, float* partial, void* out, float* amax_out, void* stream);
 
 /*
  * nt_dmpnn_init fused with layer 0's aggregation on hub graphs (fp32): the chunked reduction above with
  * the rows computed in pass 1 instead of read, H0[e] = Xv[src[e]] + Xe[e] (chemprop.py:82-83) stored
  * as it goes, then S[v] = reduce act(H0) over v's chunks (chemprop.py:37-39, layer 0), so H0 is
- * written once and never re-read.  (perm, chunk_pos, chunk_ptr, seg_ptr) as nt_segment_reduce_chunked
+ * written once and never re-read.  (perm, chunk_pos, chunk_ptr, chunk_seg, comb_seg, ncomb, seg_ptr) as
+ * nt_segment_reduce_chunked
  * on the dst CSR; H0 E x h, S V x h.  Same H0 as nt_dmpnn_init (bit-identical), same S as
  * nt_segment_reduce_chunked of that H0.  amax_out (may be NULL): 2 zero-filled device floats raised to
  * max|H0|, max|S|.
  */
 NT_API int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64_t* src, const int32_t* perm,
                                  const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
+                                 const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb,
                                  const int32_t* seg_ptr, int64_t V, int64_t E, int64_t h, int act,
                                  float act_alpha, int reduce, int dtype, float* partial, void* H0, void* S,
                                  float* amax_out, void* stream);

@@ -179,6 +179,11 @@ __global__ void __launch_bounds__(256) pack_bf16(const bf16_t* __restrict__ W, i
 }
 
 // ------------------------------------------------------------------------------ update
+// BF_ABL (variant builds only, tools/r5_bf16_abl.sh): 1 = gathers read row 0, 2 = W fragments of
+// k step 0 only, 4 = no H' / S' stores, 8 = no residual loads, 16 = no MFMA.  Results are wrong.
+#ifndef BF_ABL
+#define BF_ABL 0
+#endif
 constexpr int kM = 64;        // edges per tile
 constexpr int kThreads = 256;  // 4 waves
 constexpr int kNWMax = 8;     // column tiles per wave at h = 512 (NW = ceil(ceil(h/16) / 4))
@@ -330,7 +335,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
       uint4 sraw[kRG], qraw[kRG];
 #pragma unroll
       for (int u = 0; u < kRG; ++u) {
-        const int64_t so = soff[r0 + u], qo = qoff[r0 + u];
+        const int64_t so = (BF_ABL & 1) ? 0 : soff[r0 + u], qo = (BF_ABL & 1) ? 0 : qoff[r0 + u];
         sraw[u] = *reinterpret_cast<const uint4*>(S + (so >= 0 ? so : 0) + kc);
         qraw[u] = *reinterpret_cast<const uint4*>(H + (qo >= 0 ? qo : 0) + kc);
       }
@@ -392,7 +397,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
   const char* arow = lds + (lane & 15) * lda + 16 * (lane >> 4);
   for (int ks = 0; ks < KS; ++ks) {
     // next step's fragments (the last step re-reads its own: no branch, no drain)
-    const int64_t kn = (ks + 1 < KS ? ks + 1 : ks) * kstride;
+    const int64_t kn = (BF_ABL & 2) ? 0 : (ks + 1 < KS ? ks + 1 : ks) * kstride;
     uint4 bnext[NW];
 #pragma unroll
     for (int j = 0; j < NW; ++j) bnext[j] = Wp[kn + boff(j)];
@@ -404,8 +409,13 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     for (int j = 0; j < NW; ++j) {
       const bf16x8 b = __builtin_bit_cast(bf16x8, bcur[j]);
 #pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b, acc[mt][j], 0, 0, 0);
+      for (int mt = 0; mt < 4; ++mt) {
+        if constexpr ((BF_ABL & 16) != 0) {
+          acc[mt][j][0] += (float)a[mt][0] * (float)b[0];
+        } else {
+          acc[mt][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[mt], b, acc[mt][j], 0, 0, 0);
+        }
+      }
     }
 #pragma unroll
     for (int j = 0; j < NW; ++j) bcur[j] = bnext[j];
@@ -432,7 +442,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
     constexpr int kPre = kIt;
     auto load_res = [&](int it) {
       const int64_t e = erow[(tid >> 5) + 8 * it];
-      const bool ok = cok && e >= 0 && residual;
+      const bool ok = cok && e >= 0 && residual && (BF_ABL & 8) == 0;
       return *reinterpret_cast<const uint4*>(H + (ok ? e * h + n0 + cpiece : 0));
     };
     uint4 hres[kPre];
@@ -470,7 +480,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
             const unsigned hb = (q & 1) ? (hu[q >> 1] & 0xffff0000u) : (hu[q >> 1] << 16);
             y[q] = st[q] + bb[q] + (residual ? __uint_as_float(hb) : 0.f);
           }
-          store_chunk<8>(out + e * h + n0 + cpiece, y);
+          if constexpr ((BF_ABL & 4) == 0) store_chunk<8>(out + e * h + n0 + cpiece, y);
           if constexpr (AGG != 0) {  // the aggregation reads the stored (bf16) value, as unfused
 #pragma unroll
             for (int q = 0; q < 8; ++q) st[q] = AGG == 2 ? act_t<ACT>(rbf(y[q]), act, alpha) : rbf(y[q]);
@@ -488,7 +498,7 @@ __global__ void __launch_bounds__(kThreads, 2) update_bf16_kernel(
             case NT_MAX: reduce_rows<NT_MAX>(stage, nstart[k], nstart[k + 1], cpiece, y); break;
             default: reduce_rows<NT_MIN>(stage, nstart[k], nstart[k + 1], cpiece, y); break;
           }
-          store_chunk<8>(agg.S_out + (int64_t)nnode[k] * h + n0 + cpiece, y);
+          if constexpr ((BF_ABL & 4) == 0) store_chunk<8>(agg.S_out + (int64_t)nnode[k] * h + n0 + cpiece, y);
         }
       }
     } else {

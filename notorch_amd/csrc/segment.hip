@@ -447,23 +447,46 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
 // (segment, piece) kernel above walks a whole segment serially, so one hub sets the kernel time.
 // Here every segment is cut into chunks of at most kChunk rows (chunk_pos: monotone CSR positions,
 // segment boundaries included); pass 1 reduces each chunk (one lane per (chunk, piece), 4 rows in
-// flight), pass 2 combines a segment's chunk partials in chunk order.  Deterministic; sums differ
-// from the serial ascending order only by the regrouping (fp32 reassociation at chunk boundaries).
+// flight): a chunk that is its segment's only one (chunk_seg[k] = s) is the segment's result and is
+// stored to out[s] directly, the others go to the partial rows P[k]; pass 2 combines the chunk
+// partials of the remaining segments (comb_seg: more than one chunk, or none) in chunk order.
+// Deterministic; sums differ from the serial ascending order only by the regrouping (fp32
+// reassociation at chunk boundaries, and at the 8 sub-ranges pass 2 splits a segment's chunks into).
 #include "rows.hpp"
 
 namespace nt {
 namespace {
 
+// reduce R's finishing step for one segment result held in accumulator form (the mean divides by the
+// segment's row count n)
+template <int R, int N>
+__device__ __forceinline__ void seg_finish(float (&y)[N], int n) {
+  if constexpr (R == NT_MEAN) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) y[i] /= (float)(n > 1 ? n : 1);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ float absmax_n(float m, const float (&y)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) m = fmaxf(m, fabsf(y[i]));
+  return m;
+}
+
 template <typename T, bool VEC, int R, int ACT>
 __global__ void __launch_bounds__(256) seg_chunk_partial(const T* __restrict__ X,
                                                          const int32_t* __restrict__ perm,
                                                          const int32_t* __restrict__ chunk_pos,
+                                                         const int32_t* __restrict__ chunk_seg,
                                                          int64_t nchunks, int64_t h, int act,
-                                                         float alpha, float* __restrict__ P) {
+                                                         float alpha, float* __restrict__ P,
+                                                         T* __restrict__ out, float* __restrict__ amax) {
   constexpr int N = Piece<T, VEC>::N;
-  constexpr int RR = R == NT_MEAN ? NT_SUM : R;  // the mean divides in pass 2
+  constexpr int RR = R == NT_MEAN ? NT_SUM : R;  // the mean divides at the end
   const int64_t hw = h / N;
   const int64_t total = nchunks * hw;
+  float m = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = t / hw, c = (t - k * hw) * N;
@@ -485,28 +508,40 @@ __global__ void __launch_bounds__(256) seg_chunk_partial(const T* __restrict__ X
         for (int i = 0; i < N; ++i) r[i].push(act_t<ACT>(x[u][i], act, alpha));
       }
     }
+    const int32_t sk = chunk_seg ? chunk_seg[k] : -1;
+    float y[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) P[k * h + c + i] = r[i].acc;  // raw accumulator (chunk non-empty)
+    for (int i = 0; i < N; ++i) y[i] = r[i].acc;  // raw accumulator (chunk non-empty)
+    if (sk >= 0) {  // the segment's only chunk: its result
+      seg_finish<R>(y, e - b);
+      Piece<T, VEC>::store(out + (int64_t)sk * h + c, y);
+      m = absmax_n(m, y);
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) P[k * h + c + i] = y[i];
+    }
   }
+  if (amax) block_max_to(amax, m);  // fp32 callers: max|out| of the rows stored here
 }
 
 // The initial gather fused into pass 1 (hub graphs, fp32): the chunk's rows are computed, not read,
 // H0[e] = Xv[src[e]] + Xe[e] (stored: every dst-sorted position lies in exactly one chunk) and reduced
-// as act(H0) in the chunk's position order; amax[0] raised to max|H0|.  One lane per (chunk, piece),
-// 4 rows in flight.
+// as act(H0) in the chunk's position order; amax[0] raised to max|H0|, amax[1] to max|S| of the
+// segments finished here.  One lane per (chunk, piece), 4 rows in flight.
 template <bool VEC, int R, int ACT>
 __global__ void __launch_bounds__(256) init_chunk_partial(const float* __restrict__ Xv, const float* __restrict__ Xe,
                                                           const int64_t* __restrict__ src,
                                                           const int32_t* __restrict__ perm,
                                                           const int32_t* __restrict__ chunk_pos,
+                                                          const int32_t* __restrict__ chunk_seg,
                                                           int64_t nchunks, int64_t h, int act, float alpha,
                                                           float* __restrict__ H0, float* __restrict__ P,
-                                                          float* __restrict__ amax) {
+                                                          float* __restrict__ S, float* __restrict__ amax) {
   constexpr int N = Piece<float, VEC>::N;
-  constexpr int RR = R == NT_MEAN ? NT_SUM : R;  // the mean divides in the combine
+  constexpr int RR = R == NT_MEAN ? NT_SUM : R;  // the mean divides at the end
   const int64_t hw = h / N;
   const int64_t total = nchunks * hw;
-  float m = 0.f;
+  float m = 0.f, ms = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t k = t / hw, c = (t - k * hw) * N;
@@ -539,53 +574,122 @@ __global__ void __launch_bounds__(256) init_chunk_partial(const float* __restric
         Piece<float, VEC>::store(H0 + ed[u] * h + c, y);
       }
     }
+    const int32_t sk = chunk_seg ? chunk_seg[k] : -1;
+    float y[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) P[k * h + c + i] = r[i].acc;  // raw accumulator (chunk non-empty)
+    for (int i = 0; i < N; ++i) y[i] = r[i].acc;  // raw accumulator (chunk non-empty)
+    if (sk >= 0) {
+      seg_finish<R>(y, e - b);
+      Piece<float, VEC>::store(S + (int64_t)sk * h + c, y);
+      ms = absmax_n(ms, y);
+    } else {
+#pragma unroll
+      for (int i = 0; i < N; ++i) P[k * h + c + i] = y[i];
+    }
   }
-  if (amax) block_max_to(amax, m);
+  if (amax) block_max_to(amax, m, ms, true);
 }
 
+// Pass 2: one block per (listed segment, 32-piece slab); the segment's chunks split into 8
+// consecutive sub-ranges (one per 32-thread group), each summed in chunk order, then the 8 group
+// results combined in order by group 0 (empty segment -> 0 for every reduction).
+constexpr int kCombG = 8;
 template <typename T, bool VEC, int R>
 __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict__ P,
                                                          const int32_t* __restrict__ chunk_ptr,
                                                          const int32_t* __restrict__ seg_ptr,
-                                                         int64_t nseg, int64_t h,
+                                                         const int32_t* __restrict__ comb_seg,
+                                                         int64_t ncomb, int64_t h,
                                                          T* __restrict__ out, float* __restrict__ amax) {
   constexpr int N = Piece<T, VEC>::N;
-  const int64_t hw = h / N;
-  const int64_t total = nseg * hw;
+  __shared__ float red[kCombG][32][N];
+  const int64_t hw = h / N, nslab = (hw + 31) / 32;
+  const int g = threadIdx.x >> 5, cl = threadIdx.x & 31;
   float m = 0.f;
-  for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
-       t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t s = t / hw, c = (t - s * hw) * N;
-    const int32_t b = chunk_ptr[s], e = chunk_ptr[s + 1];
+  for (int64_t blk = blockIdx.x; blk < ncomb * nslab; blk += gridDim.x) {
+    const int64_t i = blk / nslab, pc = (blk - i * nslab) * 32 + cl;
+    const int32_t sg = comb_seg ? comb_seg[i] : (int32_t)i;
+    const int32_t b = chunk_ptr[sg], n = chunk_ptr[sg + 1] - b;
+    const bool ok = pc < hw;
+    const int64_t c = (ok ? pc : 0) * N;
+    const int32_t kb = b + (int32_t)((int64_t)n * g / kCombG), ke = b + (int32_t)((int64_t)n * (g + 1) / kCombG);
     float y[N];
 #pragma unroll
-    for (int i = 0; i < N; ++i) y[i] = 0.f;  // empty segment -> 0 for every reduction
-    for (int32_t k = b; k < e; ++k) {
+    for (int q = 0; q < N; ++q) y[q] = 0.f;
+    for (int32_t k = kb; k < ke; k += 4) {
+      float p[4][N];
 #pragma unroll
-      for (int i = 0; i < N; ++i) {
-        const float p = P[(int64_t)k * h + c + i];
-        if constexpr (R == NT_MAX) y[i] = k == b ? p : fmaxf(y[i], p);
-        else if constexpr (R == NT_MIN) y[i] = k == b ? p : fminf(y[i], p);
-        else y[i] += p;
+      for (int u = 0; u < 4; ++u) {
+        const int64_t kk = k + u < ke ? k + u : kb;
+#pragma unroll
+        for (int q = 0; q < N; ++q) p[u][q] = P[kk * h + c + q];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (k + u >= ke) break;
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+          if constexpr (R == NT_MAX) y[q] = k + u == kb ? p[u][q] : fmaxf(y[q], p[u][q]);
+          else if constexpr (R == NT_MIN) y[q] = k + u == kb ? p[u][q] : fminf(y[q], p[u][q]);
+          else y[q] += p[u][q];
+        }
       }
     }
-    if constexpr (R == NT_MEAN) {
-      const int n = seg_ptr[s + 1] - seg_ptr[s];
 #pragma unroll
-      for (int i = 0; i < N; ++i) y[i] /= (float)(n > 1 ? n : 1);
+    for (int q = 0; q < N; ++q) red[g][cl][q] = y[q];
+    __syncthreads();
+    if (g == 0 && ok) {
+      bool first = true;
+      for (int gg = 0; gg < kCombG; ++gg) {
+        const int32_t gb = (int32_t)((int64_t)n * gg / kCombG), ge = (int32_t)((int64_t)n * (gg + 1) / kCombG);
+        if (gb == ge) continue;  // an empty sub-range
+#pragma unroll
+        for (int q = 0; q < N; ++q) {
+          const float v = red[gg][cl][q];
+          if constexpr (R == NT_MAX) y[q] = first ? v : fmaxf(y[q], v);
+          else if constexpr (R == NT_MIN) y[q] = first ? v : fminf(y[q], v);
+          else y[q] = first ? v : y[q] + v;
+        }
+        first = false;
+      }
+      if (first) {  // no chunks: empty segment
+#pragma unroll
+        for (int q = 0; q < N; ++q) y[q] = 0.f;
+      }
+      seg_finish<R>(y, seg_ptr[sg + 1] - seg_ptr[sg]);
+      Piece<T, VEC>::store(out + (int64_t)sg * h + c, y);
+      m = absmax_n(m, y);
     }
-    Piece<T, VEC>::store(out + s * h + c, y);
-#pragma unroll
-    for (int i = 0; i < N; ++i) m = fmaxf(m, fabsf(y[i]));
+    __syncthreads();
   }
   if (amax) block_max_to(amax, m);  // fp32 callers: max|out| (the fp32 layer kernel's split scale)
 }
 
+template <typename T, bool VEC, int R>
+void launch_combine(const float* P, const int32_t* chunk_ptr, const int32_t* seg_ptr, const int32_t* comb_seg,
+                    int64_t ncomb, int64_t h, T* out, float* amax, hipStream_t stream) {
+  constexpr int N = Piece<T, VEC>::N;
+  const int64_t blocks = ncomb * ((h / N + 31) / 32);
+  if (blocks == 0) return;
+  const int g = (int)(blocks < 256 * 16 ? blocks : 256 * 16);
+  seg_chunk_combine<T, VEC, R><<<g, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax);
+}
+
+template <typename T, bool VEC>
+void launch_combine_r(int reduce, const float* P, const int32_t* chunk_ptr, const int32_t* seg_ptr,
+                      const int32_t* comb_seg, int64_t ncomb, int64_t h, T* out, float* amax, hipStream_t stream) {
+  switch (reduce) {
+    case NT_SUM: launch_combine<T, VEC, NT_SUM>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream); break;
+    case NT_MEAN: launch_combine<T, VEC, NT_MEAN>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream); break;
+    case NT_MAX: launch_combine<T, VEC, NT_MAX>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream); break;
+    default: launch_combine<T, VEC, NT_MIN>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream); break;
+  }
+}
+
 template <bool VEC>
 int launch_init_chunked(const float* Xv, const float* Xe, const int64_t* src, const int32_t* perm,
-                        const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr, const int32_t* seg_ptr,
+                        const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
+                        const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb, const int32_t* seg_ptr,
                         int64_t nseg, int64_t h, int reduce, int act, float alpha, float* P, float* H0, float* S,
                         float* amax, hipStream_t stream) {
   constexpr int N = Piece<float, VEC>::N;
@@ -593,40 +697,32 @@ int launch_init_chunked(const float* Xv, const float* Xe, const int64_t* src, co
     const int g1 = grid_for(nchunks * (h / N), 256, 256 * 32);
     NT_DISPATCH_RA(reduce, act,
                    (init_chunk_partial<VEC, R_, A_><<<g1, 256, 0, stream>>>(
-                       Xv, Xe, src, perm, chunk_pos, nchunks, h, act, alpha, H0, P, amax)));
+                       Xv, Xe, src, perm, chunk_pos, chunk_seg, nchunks, h, act, alpha, H0, P, S, amax)));
     NT_LAUNCH_CHECK();
   }
-  float* am1 = amax ? amax + 1 : nullptr;
-  const int g2 = grid_for(nseg * (h / N), 256, 256 * 32);
-  switch (reduce) {
-    case NT_SUM: seg_chunk_combine<float, VEC, NT_SUM><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, S, am1); break;
-    case NT_MEAN: seg_chunk_combine<float, VEC, NT_MEAN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, S, am1); break;
-    case NT_MAX: seg_chunk_combine<float, VEC, NT_MAX><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, S, am1); break;
-    default: seg_chunk_combine<float, VEC, NT_MIN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, S, am1); break;
-  }
+  if (chunk_seg == nullptr) ncomb = nseg;  // every segment through pass 2
+  launch_combine_r<float, VEC>(reduce, P, chunk_ptr, seg_ptr, chunk_seg ? comb_seg : nullptr, ncomb, h, S,
+                               amax ? amax + 1 : nullptr, stream);
   NT_LAUNCH_CHECK();
   return NT_OK;
 }
 
 template <typename T, bool VEC>
 int launch_chunked(const void* X, const int32_t* perm, const int32_t* chunk_pos, int64_t nchunks,
-                   const int32_t* chunk_ptr, const int32_t* seg_ptr, int64_t nseg, int64_t h,
-                   int reduce, int act, float alpha, float* P, void* out, float* amax, hipStream_t stream) {
+                   const int32_t* chunk_ptr, const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb,
+                   const int32_t* seg_ptr, int64_t nseg, int64_t h, int reduce, int act, float alpha, float* P,
+                   void* out, float* amax, hipStream_t stream) {
   constexpr int N = Piece<T, VEC>::N;
   if (nchunks > 0) {
     const int g1 = grid_for(nchunks * (h / N), 256, 256 * 32);
     NT_DISPATCH_RA(reduce, act,
                    (seg_chunk_partial<T, VEC, R_, A_><<<g1, 256, 0, stream>>>(
-                       (const T*)X, perm, chunk_pos, nchunks, h, act, alpha, P)));
+                       (const T*)X, perm, chunk_pos, chunk_seg, nchunks, h, act, alpha, P, (T*)out, amax)));
     NT_LAUNCH_CHECK();
   }
-  const int g2 = grid_for(nseg * (h / N), 256, 256 * 32);
-  switch (reduce) {
-    case NT_SUM: seg_chunk_combine<T, VEC, NT_SUM><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out, amax); break;
-    case NT_MEAN: seg_chunk_combine<T, VEC, NT_MEAN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out, amax); break;
-    case NT_MAX: seg_chunk_combine<T, VEC, NT_MAX><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out, amax); break;
-    default: seg_chunk_combine<T, VEC, NT_MIN><<<g2, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, nseg, h, (T*)out, amax); break;
-  }
+  if (chunk_seg == nullptr) ncomb = nseg;
+  launch_combine_r<T, VEC>(reduce, P, chunk_ptr, seg_ptr, chunk_seg ? comb_seg : nullptr, ncomb, h, (T*)out, amax,
+                           stream);
   NT_LAUNCH_CHECK();
   return NT_OK;
 }
@@ -635,35 +731,39 @@ int launch_chunked(const void* X, const int32_t* perm, const int32_t* chunk_pos,
 }  // namespace nt
 
 extern "C" int nt_segment_reduce_chunked(const void* X, const int32_t* perm, const int32_t* chunk_pos,
-                                         int64_t nchunks, const int32_t* chunk_ptr,
-                                         const int32_t* seg_ptr, int64_t nseg, int64_t h, int reduce,
-                                         int act, float act_alpha, int dtype, float* partial,
-                                         void* out, float* amax_out, void* stream_) {
+                                         int64_t nchunks, const int32_t* chunk_ptr, const int32_t* chunk_seg,
+                                         const int32_t* comb_seg, int64_t ncomb, const int32_t* seg_ptr,
+                                         int64_t nseg, int64_t h, int reduce, int act, float act_alpha, int dtype,
+                                         float* partial, void* out, float* amax_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
-  NT_REQUIRE(nseg >= 0 && nchunks >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(nseg >= 0 && nchunks >= 0 && h > 0 && ncomb >= 0 && ncomb <= nseg, NT_EINVAL, "bad sizes");
   if (nseg == 0) return NT_OK;
   NT_REQUIRE(chunk_ptr && seg_ptr && out && (nchunks == 0 || (X && chunk_pos && partial)), NT_EINVAL,
              "NULL pointer");
+  NT_REQUIRE(chunk_seg == nullptr || ncomb == 0 || comb_seg != nullptr, NT_EINVAL, "chunk_seg needs comb_seg");
   hipStream_t stream = as_stream(stream_);
   const bool al = aligned16(X) && aligned16(out) && aligned16(partial);
   if (dtype == NT_F32)
     return (h % 4 == 0 && al)
-               ? launch_chunked<float, true>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
-                                             reduce, act, act_alpha, partial, out, amax_out, stream)
-               : launch_chunked<float, false>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
-                                              reduce, act, act_alpha, partial, out, amax_out, stream);
+               ? launch_chunked<float, true>(X, perm, chunk_pos, nchunks, chunk_ptr, chunk_seg, comb_seg, ncomb,
+                                             seg_ptr, nseg, h, reduce, act, act_alpha, partial, out, amax_out, stream)
+               : launch_chunked<float, false>(X, perm, chunk_pos, nchunks, chunk_ptr, chunk_seg, comb_seg, ncomb,
+                                              seg_ptr, nseg, h, reduce, act, act_alpha, partial, out, amax_out,
+                                              stream);
   return (h % 8 == 0 && al)
-             ? launch_chunked<bf16_raw, true>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
-                                              reduce, act, act_alpha, partial, out, nullptr, stream)
-             : launch_chunked<bf16_raw, false>(X, perm, chunk_pos, nchunks, chunk_ptr, seg_ptr, nseg, h,
-                                               reduce, act, act_alpha, partial, out, nullptr, stream);
+             ? launch_chunked<bf16_raw, true>(X, perm, chunk_pos, nchunks, chunk_ptr, chunk_seg, comb_seg, ncomb,
+                                              seg_ptr, nseg, h, reduce, act, act_alpha, partial, out, nullptr, stream)
+             : launch_chunked<bf16_raw, false>(X, perm, chunk_pos, nchunks, chunk_ptr, chunk_seg, comb_seg, ncomb,
+                                               seg_ptr, nseg, h, reduce, act, act_alpha, partial, out, nullptr,
+                                               stream);
 }
 
 extern "C" int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64_t* src, const int32_t* perm,
                                      const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
+                                     const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb,
                                      const int32_t* seg_ptr, int64_t V, int64_t E, int64_t h, int act,
                                      float act_alpha, int reduce, int dtype, float* partial, void* H0, void* S,
                                      float* amax_out, void* stream_) {
@@ -671,17 +771,18 @@ extern "C" int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64
   clear_error();
   NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_init_chunked is fp32 only");
   NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
-  NT_REQUIRE(V >= 0 && E >= 0 && nchunks >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(V >= 0 && E >= 0 && nchunks >= 0 && h > 0 && ncomb >= 0 && ncomb <= V, NT_EINVAL, "bad sizes");
   if (V == 0) return NT_OK;
   NT_REQUIRE(chunk_ptr && seg_ptr && S && (nchunks == 0 || (Xv && Xe && src && perm && chunk_pos && partial && H0)),
              NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(chunk_seg == nullptr || ncomb == 0 || comb_seg != nullptr, NT_EINVAL, "chunk_seg needs comb_seg");
   hipStream_t stream = as_stream(stream_);
   const bool al = aligned16(Xv) && aligned16(Xe) && aligned16(H0) && aligned16(S) && aligned16(partial);
   return (h % 4 == 0 && al)
              ? launch_init_chunked<true>((const float*)Xv, (const float*)Xe, src, perm, chunk_pos, nchunks, chunk_ptr,
-                                         seg_ptr, V, h, reduce, act, act_alpha, partial, (float*)H0, (float*)S,
-                                         amax_out, stream)
+                                         chunk_seg, comb_seg, ncomb, seg_ptr, V, h, reduce, act, act_alpha, partial,
+                                         (float*)H0, (float*)S, amax_out, stream)
              : launch_init_chunked<false>((const float*)Xv, (const float*)Xe, src, perm, chunk_pos, nchunks,
-                                          chunk_ptr, seg_ptr, V, h, reduce, act, act_alpha, partial, (float*)H0,
-                                          (float*)S, amax_out, stream);
+                                          chunk_ptr, chunk_seg, comb_seg, ncomb, seg_ptr, V, h, reduce, act,
+                                          act_alpha, partial, (float*)H0, (float*)S, amax_out, stream);
 }

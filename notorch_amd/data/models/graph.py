@@ -577,7 +577,8 @@ def host_tile_plan(dst_ptr: np.ndarray, E: int, max_in_degree: int, rows: int = 
 
 
 def host_chunk_plan(seg_ptr: np.ndarray, chunk: int = CHUNK_ROWS):
-    """(chunk_pos[nchunks+1], nchunks, chunk_ptr[nseg+1]) exactly as kernels.chunk_plan builds them."""
+    """(chunk_pos[nchunks+1], nchunks, chunk_ptr[nseg+1], chunk_seg[nchunks], comb_seg[ncomb]) exactly
+    as kernels.chunk_plan builds them."""
     sp = seg_ptr.astype(np.int64)
     n = sp[1:] - sp[:-1]
     nch = (n + chunk - 1) // chunk
@@ -589,7 +590,11 @@ def host_chunk_plan(seg_ptr: np.ndarray, chunk: int = CHUNK_ROWS):
     chunk_pos = np.empty(nchunks + 1, dtype=np.int32)
     chunk_pos[:nchunks] = sp[seg_of] + k_in_seg * chunk
     chunk_pos[nchunks] = seg_ptr[-1]
-    return torch.from_numpy(chunk_pos), nchunks, torch.from_numpy(chunk_ptr.astype(np.int32))
+    multi = nch != 1
+    chunk_seg = np.where(multi[seg_of], -1, seg_of).astype(np.int32)
+    comb_seg = np.nonzero(multi)[0].astype(np.int32)
+    return (torch.from_numpy(chunk_pos), nchunks, torch.from_numpy(chunk_ptr.astype(np.int32)),
+            torch.from_numpy(chunk_seg), torch.from_numpy(comb_seg))
 
 
 def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional[np.ndarray],

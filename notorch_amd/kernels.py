@@ -287,23 +287,47 @@ def dmpnn_aggregate(H: Tensor, row_ptr: Tensor, perm: Tensor, V: int, *, reduce:
 CHUNK_ROWS = 32  # rows per chunk of the load-balanced segment reduce
 
 
-def chunk_plan(seg_ptr: Tensor, chunk: int = CHUNK_ROWS) -> tuple[Tensor, int, Tensor]:
-    """(chunk_pos[nchunks+1], nchunks, chunk_ptr[nseg+1]) for nt_segment_reduce_chunked: every segment
-    cut into chunks of at most ``chunk`` CSR positions.  Device ops; one host sync (the chunk count)."""
+def chunk_plan(seg_ptr: Tensor, chunk: int = CHUNK_ROWS) -> tuple:
+    """(chunk_pos[nchunks+1], nchunks, chunk_ptr[nseg+1], chunk_seg[nchunks], comb_seg[ncomb]) for
+    nt_segment_reduce_chunked: every segment cut into chunks of at most ``chunk`` CSR positions;
+    chunk_seg[k] = the segment of chunk k when it is that segment's only chunk (pass 1 stores its
+    result directly), else -1; comb_seg = the segments with != 1 chunk (pass 2's list).  Device ops;
+    one host sync (the two counts)."""
     _require_device(seg_ptr)
+    dev = seg_ptr.device
     sp = seg_ptr.to(torch.int64)
     n = sp[1:] - sp[:-1]
     nch = (n + chunk - 1) // chunk
-    chunk_ptr64 = torch.zeros(n.numel() + 1, dtype=torch.int64, device=seg_ptr.device)
+    chunk_ptr64 = torch.zeros(n.numel() + 1, dtype=torch.int64, device=dev)
     torch.cumsum(nch, 0, out=chunk_ptr64[1:])
-    nchunks = int(chunk_ptr64[-1])
-    seg_of = torch.repeat_interleave(torch.arange(n.numel(), device=seg_ptr.device), nch,
-                                     output_size=nchunks)
-    k_in_seg = torch.arange(nchunks, device=seg_ptr.device) - chunk_ptr64[seg_of]
-    chunk_pos = torch.empty(nchunks + 1, dtype=torch.int32, device=seg_ptr.device)
+    multi = nch != 1
+    nchunks, ncomb = (int(x) for x in torch.stack([chunk_ptr64[-1], multi.sum()]).tolist())
+    seg_of = torch.repeat_interleave(torch.arange(n.numel(), device=dev), nch, output_size=nchunks)
+    k_in_seg = torch.arange(nchunks, device=dev) - chunk_ptr64[seg_of]
+    chunk_pos = torch.empty(nchunks + 1, dtype=torch.int32, device=dev)
     chunk_pos[:nchunks] = (sp[seg_of] + k_in_seg * chunk).to(torch.int32)
     chunk_pos[nchunks] = seg_ptr[-1]
-    return chunk_pos, nchunks, chunk_ptr64.to(torch.int32)
+    chunk_seg = torch.where(multi[seg_of], -1, seg_of).to(torch.int32)
+    comb_seg = torch.nonzero(multi).flatten().to(torch.int32)
+    assert comb_seg.numel() == ncomb
+    return chunk_pos, nchunks, chunk_ptr64.to(torch.int32), chunk_seg, comb_seg
+
+
+def _chunk_args(plan, nseg: int):
+    """ctypes arguments (chunk_pos, nchunks, chunk_ptr, chunk_seg, comb_seg, ncomb) of a chunk plan."""
+    if len(plan) != 5:
+        raise ValueError("plan must be chunk_plan(seg_ptr): (chunk_pos, nchunks, chunk_ptr, chunk_seg, comb_seg)")
+    chunk_pos, nchunks, chunk_ptr, chunk_seg, comb_seg = plan
+    for name, t in (("chunk_pos", chunk_pos), ("chunk_ptr", chunk_ptr), ("chunk_seg", chunk_seg),
+                    ("comb_seg", comb_seg)):
+        if t.dtype != torch.int32:
+            raise TypeError(f"{name} must be int32")
+        if not t.is_contiguous():
+            raise ValueError(f"{name} must be contiguous")
+    if (chunk_pos.numel() != nchunks + 1 or chunk_ptr.numel() != nseg + 1 or chunk_seg.numel() != nchunks
+            or comb_seg.numel() > nseg):
+        raise ValueError("plan must be chunk_plan(seg_ptr) of this CSR")
+    return _ptr(chunk_pos), nchunks, _ptr(chunk_ptr), _ptr(chunk_seg), _ptr(comb_seg), comb_seg.numel()
 
 
 def segment_reduce_chunked(
@@ -324,7 +348,8 @@ def segment_reduce_chunked(
     code = _require_feat("X", X)
     if seg_ptr.dtype != torch.int32 or seg_ptr.numel() != nseg + 1:
         raise ValueError("seg_ptr must be int32 of length nseg + 1")
-    chunk_pos, nchunks, chunk_ptr = plan
+    cargs = _chunk_args(plan, nseg)
+    nchunks = plan[1]
     h = X.shape[1]
     if out is None:
         out = torch.empty(nseg, h, dtype=X.dtype, device=dev)
@@ -332,7 +357,7 @@ def segment_reduce_chunked(
         _require_feat("out", out, X.dtype)
     partial = torch.empty(max(nchunks, 1), h, dtype=torch.float32, device=dev)
     _run(dev, _lib.load().nt_segment_reduce_chunked,
-         _ptr(X), _ptr(perm), _ptr(chunk_pos), nchunks, _ptr(chunk_ptr), _ptr(seg_ptr), nseg, h,
+         _ptr(X), _ptr(perm), *cargs, _ptr(seg_ptr), nseg, h,
          reduce_code(reduce), act[0], act[1], code, _ptr(partial), _ptr(out), _ptr(amax), _stream(dev))
     return out
 
@@ -352,13 +377,13 @@ def dmpnn_init_chunked(
     """(H0, S) = dmpnn_init with layer 0's aggregation over the chunk plan of a hub graph (fp32,
     plan = chunk_plan(seg_ptr)): H0 written once, S combined from per-chunk partials.  amax (2
     zero-filled device floats, optional) raised to max|H0|, max|S|."""
-    chunk_pos, nchunks, chunk_ptr = plan
-    dev = _require_device(Xv, Xe, src, seg_ptr, perm, chunk_pos, chunk_ptr, amax)
+    nchunks = plan[1]
+    dev = _require_device(Xv, Xe, src, seg_ptr, perm, plan[0], plan[2], amax)
     if Xv.dtype != torch.float32 or Xe.dtype != torch.float32:
         raise ValueError("dmpnn_init_chunked is fp32 only")
     _require_amax(amax, Xv.dtype)
     _require_i64("src", src)
-    for name, t in (("seg_ptr", seg_ptr), ("perm", perm), ("chunk_pos", chunk_pos), ("chunk_ptr", chunk_ptr)):
+    for name, t in (("seg_ptr", seg_ptr), ("perm", perm)):
         if t.dtype != torch.int32:
             raise TypeError(f"{name} must be int32")
         if not t.is_contiguous():
@@ -367,14 +392,12 @@ def dmpnn_init_chunked(
     E = Xe.shape[0]
     if Xe.shape[1] != h or src.numel() != E or perm.numel() != E or seg_ptr.numel() != V + 1:
         raise ValueError("shape mismatch between Xv, Xe, src and the dst CSR")
-    if chunk_pos.numel() != nchunks + 1 or chunk_ptr.numel() != V + 1:
-        raise ValueError("plan must be chunk_plan(seg_ptr): chunk_pos[nchunks + 1], chunk_ptr[V + 1]")
+    cargs = _chunk_args(plan, V)
     H0 = torch.empty(E, h, dtype=torch.float32, device=dev)
     S = torch.empty(V, h, dtype=torch.float32, device=dev)
     partial = torch.empty(max(nchunks, 1), h, dtype=torch.float32, device=dev)
     _run(dev, _lib.load().nt_dmpnn_init_chunked,
-         _ptr(Xv.contiguous()), _ptr(Xe.contiguous()), _ptr(src), _ptr(perm), _ptr(chunk_pos), nchunks,
-         _ptr(chunk_ptr), _ptr(seg_ptr), V, E, h, act[0], act[1], reduce_code(reduce), _DTYPE_CODES[torch.float32],
+         _ptr(Xv.contiguous()), _ptr(Xe.contiguous()), _ptr(src), _ptr(perm), *cargs, _ptr(seg_ptr), V, E, h, act[0], act[1], reduce_code(reduce), _DTYPE_CODES[torch.float32],
          _ptr(partial), _ptr(H0), _ptr(S), _ptr(amax), _stream(dev))
     return H0, S
 

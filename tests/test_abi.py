@@ -48,7 +48,7 @@ def test_abi_version_and_errors_without_gpu():
     from notorch_amd import _lib
 
     lib = _lib.load()
-    assert lib.nt_abi_version() == _lib.ABI_VERSION == 6
+    assert lib.nt_abi_version() == _lib.ABI_VERSION == 7
     assert lib.nt_last_kernel() == b""  # no layer call yet on this thread
     assert lib.nt_dmpnn_packed_weight_bytes(300, 0) > 0
     assert lib.nt_dmpnn_packed_weight_bytes(0, 0) == 0

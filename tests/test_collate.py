@@ -162,9 +162,14 @@ def test_host_plans_ship_with_the_collate():
         assert np.diff(tp).max() <= rows and np.diff(tp).min() >= 0
         assert all(int(t) in starts or hub_pos[t] for t in tp)
         assert hub_pos[tp].any()  # some cut falls inside a hub
-    chunk_pos, nchunks, chunk_ptr = lay.dst_chunks
+    chunk_pos, nchunks, chunk_ptr, chunk_seg, comb_seg = lay.dst_chunks
     assert chunk_pos.numel() == nchunks + 1 and int(chunk_ptr[-1]) == nchunks
     assert (np.diff(chunk_pos.numpy()) <= 32).all()
+    nch = np.diff(chunk_ptr.numpy())
+    single = np.nonzero(nch == 1)[0]
+    assert np.array_equal(chunk_seg.numpy()[chunk_ptr.numpy()[single]], single)
+    assert (chunk_seg.numpy() >= 0).sum() == single.size
+    assert np.array_equal(comb_seg.numpy(), np.nonzero(nch != 1)[0])
 
 
 def test_all_zero_bond_batch_collates():

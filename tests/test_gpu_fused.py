@@ -270,6 +270,7 @@ def test_host_plans_equal_device_planners():
         dev = K.chunk_plan(seg_ptr.to(DEV))
         assert dev[1] == host[1]
         assert torch.equal(dev[0].cpu(), host[0]) and torch.equal(dev[2].cpu(), host[2])
+        assert torch.equal(dev[3].cpu(), host[3]) and torch.equal(dev[4].cpu(), host[4])
 
 
 def test_forward_on_a_non_current_device():

@@ -530,6 +530,33 @@ def test_segment_reduce_chunked_skewed(reduce, dtype):
         assert got[nseg - 1].abs().sum() == 0  # trailing empty segments read 0
 
 
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
+def test_segment_reduce_chunked_without_single_chunk_list(reduce):
+    """chunk_seg = NULL (ABI 7): every segment goes through pass 2, as before the single-chunk
+    segments were stored by pass 1; the results are the same values."""
+    from notorch_amd import _lib
+    from notorch_amd.kernels import _ptr, _stream, reduce_code
+
+    K = _K()
+    G = _graph_tensors("polymer", 2, seed=6)
+    E, V, h = G.edge_index.shape[1], G.num_nodes, 300
+    torch.manual_seed(1)
+    X = torch.randn(E, h, device=DEV)
+    seg_ptr, perm = K.csr_build(G.edge_index[1].to(DEV), V + 2)
+    plan = K.chunk_plan(seg_ptr)
+    relu = K.act_code(nn.ReLU())
+    got = K.segment_reduce_chunked(X, seg_ptr, perm, V + 2, plan, reduce=reduce, act=relu)
+    chunk_pos, nchunks, chunk_ptr = plan[:3]
+    out = torch.full_like(got, float("nan"))
+    partial = torch.empty(nchunks, h, device=DEV)
+    rc = _lib.load().nt_segment_reduce_chunked(
+        _ptr(X), _ptr(perm), _ptr(chunk_pos), nchunks, _ptr(chunk_ptr), None, None, 0, _ptr(seg_ptr), V + 2, h,
+        reduce_code(reduce), relu[0], relu[1], 0, _ptr(partial), _ptr(out), None, _stream(X.device))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, got)
+
+
 def test_batch_with_zero_bond_molecules():
     """Single-atom molecules (E_i = 0; the reference MolToGraph would crash on them)
     mixed into a batch: their nodes have no in-edge, so S and node rows are 0 (torch_scatter empty
