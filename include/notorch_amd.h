@@ -139,11 +139,13 @@ NT_API int nt_csr_build(const int64_t* idx, int64_t n, int64_t nseg, int32_t* se
  * src = edge_index[0] (int64, E); (seg_ptr, perm) = nt_csr_build(edge_index[1], E, V).
  * amax_out (fp32 only, may be NULL): 2 device floats, atomically raised to max|H0| and max|S| (S
  * only when S != NULL); the caller zero-fills them.  They are the amax_in of layer 0's
- * nt_dmpnn_update_fused.
+ * nt_dmpnn_update_fused.  ld_out (ABI 7): row pitch in elements of H0 and S (0 = h; > h: fp32 with
+ * h % 4 == 0 and ld_out % 4 == 0, the padded rows nt_dmpnn_update_fused's ld_in takes).
  */
 NT_API int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src, const int32_t* seg_ptr,
                   const int32_t* perm, int64_t V, int64_t E, int64_t h, int act, float act_alpha,
-                  int reduce, int dtype, void* H0, void* S, float* amax_out, void* stream);
+                  int reduce, int dtype, void* H0, void* S, float* amax_out, int64_t ld_out,
+                  void* stream);
 
 /*
  * max |X| over n fp32 elements, atomically max-ed into *out (device float; non-negative floats
@@ -327,6 +329,9 @@ NT_API int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, i
  * amax_out (may be NULL) = 2 zero-filled device floats raised to max|H_out|, max|S_out|.
  * bf16 (h % 8 == 0, h <= 512): bf16 MFMA, tile_rows <= 64, amax ignored.
  * 16-byte aligned feature pointers; S_out must not alias S.
+ * ld_in / ld_out (ABI 7): row pitch in elements of H and S / of H_out and S_out (0 = h; fp32: >= h and
+ * a multiple of 4, bf16: h).  Rows padded to a 32-byte multiple (h = 300 -> 304) keep every row's
+ * pieces on whole 32-B sectors: the intermediate layers of a forward run on padded rows.
  */
 NT_API int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* src, const int64_t* rev,
                                  const void* Wp, const void* b, int64_t V, int64_t E, int64_t h,
@@ -334,7 +339,8 @@ NT_API int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* sr
                                  int64_t ntiles, int tile_rows, int max_in_degree, const int32_t* perm,
                                  const int32_t* dst_sorted, const void* row_table, int reduce,
                                  int agg_act, float agg_alpha, int dtype, const float* amax_in,
-                                 float* amax_out, void* H_out, void* S_out, void* stream);
+                                 float* amax_out, void* H_out, void* S_out, int64_t ld_in,
+                                 int64_t ld_out, void* stream);
 
 /*
  * Row table of a fused plan for the fp32 layer kernel: one int32 x 4 entry per dst-sorted position p

@@ -67,7 +67,8 @@ SIGNATURES: dict[str, tuple] = {
     "nt_csr_build": (_c_int, [_vp, _c_i64, _c_i64, _vp, _vp, _vp, _c_size, _vp, _vp]),
     "nt_dmpnn_init": (
         _c_int,
-        [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp, _vp],
+        [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp, _c_i64,
+         _vp],
     ),
     "nt_absmax": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp]),
     "nt_segment_reduce": (
@@ -105,7 +106,8 @@ SIGNATURES: dict[str, tuple] = {
     "nt_dmpnn_update_fused": (
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _vp, _c_i64,
-         _c_int, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp, _vp, _vp],
+         _c_int, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp, _vp, _c_i64, _c_i64,
+         _vp],
     ),
     "nt_dmpnn_row_table": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp]),
     "nt_node_scores": (

@@ -130,7 +130,7 @@ template <int R, int ACT>
 __global__ void __launch_bounds__(256) init_aggregate_vec4(
     const float4* __restrict__ Xv, const float4* __restrict__ Xe, const int64_t* __restrict__ src,
     const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm, int64_t V, int64_t hv,
-    int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S) {
+    int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S, int64_t lo) {
   const int64_t total = V * hv;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
@@ -141,10 +141,10 @@ __global__ void __launch_bounds__(256) init_aggregate_vec4(
     for (int32_t j = b; j < e; ++j) {
       const int64_t ed = perm[j];
       const float4 x = Xv[src[ed] * hv + c] + Xe[ed * hv + c];
-      H0[ed * hv + c] = x;
+      H0[ed * lo + c] = x;
       r.push(act4_t<ACT>(x, act, alpha));
     }
-    S[t] = r.result();
+    S[v * lo + c] = r.result();
   }
 }
 
@@ -158,7 +158,8 @@ template <int R, int ACT, int PPL>
 __global__ void __launch_bounds__(256) init_aggregate_wave(
     const float4* __restrict__ Xv, const float4* __restrict__ Xe, const int64_t* __restrict__ src,
     const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm, int64_t V, int64_t hv,
-    int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S, float* __restrict__ amax) {
+    int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S, float* __restrict__ amax,
+    int64_t lo) {  // lo: output row pitch in 16-B pieces (H0, S)
   const int lane = threadIdx.x & 63;
   float mh = 0.f, ms = 0.f;  // max |H0|, max |S| of this lane (amax != NULL)
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -204,7 +205,7 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
           for (int q = 0; q < PPL; ++q) {
             const float4 h0 = a[u][q] + x[u][q];
             if (ok[q]) {
-              H0[ed[u] * hv + cc[q]] = h0;
+              H0[ed[u] * lo + cc[q]] = h0;
               mh = amax4(mh, h0);
             }
             r[q].push(act4_t<ACT>(h0, act, alpha));
@@ -216,7 +217,7 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
         for (int q = 0; q < PPL; ++q) {
           const float4 h0 = Xv[sv * hv + cc[q]] + Xe[ed * hv + cc[q]];
           if (ok[q]) {
-            H0[ed * hv + cc[q]] = h0;
+            H0[ed * lo + cc[q]] = h0;
             mh = amax4(mh, h0);
           }
           r[q].push(act4_t<ACT>(h0, act, alpha));
@@ -226,7 +227,7 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
       for (int q = 0; q < PPL; ++q) {
         if (ok[q]) {
           const float4 s4 = r[q].result();
-          S[v * hv + cc[q]] = s4;
+          S[v * lo + cc[q]] = s4;
           ms = amax4(ms, s4);
         }
       }
@@ -262,14 +263,14 @@ __global__ void __launch_bounds__(256) init_only_vec4(const float4* __restrict__
                                                       const float4* __restrict__ Xe,
                                                       const int64_t* __restrict__ src, int64_t E,
                                                       int64_t hv, float4* __restrict__ H0,
-                                                      float* __restrict__ amax) {
+                                                      float* __restrict__ amax, int64_t lo) {
   const int64_t total = E * hv;
   float m = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t e = t / hv, c = t - e * hv;
     const float4 y = Xv[src[e] * hv + c] + Xe[t];
-    H0[t] = y;
+    H0[e * lo + c] = y;
     m = fmaxf(m, fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
   }
   if (amax) block_max_to(amax, m);
@@ -367,12 +368,19 @@ int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);  // up
 extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
                              const int32_t* seg_ptr, const int32_t* perm, int64_t V, int64_t E,
                              int64_t h, int act, float act_alpha, int reduce, int dtype, void* H0,
-                             void* S, float* amax_out, void* stream_) {
+                             void* S, float* amax_out, int64_t ld_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
-  NT_REQUIRE(V >= 0 && E >= 0 && h > 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(V >= 0 && E >= 0 && h > 0 && ld_out >= 0, NT_EINVAL, "bad sizes");
+  if (ld_out == 0) ld_out = h;
+  // padded output rows: the fp32 kernels that take them (the wave-per-node init, h >= 128, and the
+  // plain init); every other variant writes dense rows
+  NT_REQUIRE(ld_out == h || (dtype == NT_F32 && h % 4 == 0 && ld_out % 4 == 0 && ld_out > h &&
+                             (S == nullptr || h >= 128)),
+             NT_EUNSUPPORTED, "ld_out != h needs fp32, h % 4 == 0, ld_out % 4 == 0 and h >= 128 (with S)");
+  const int64_t lo4 = ld_out / 4;
   hipStream_t stream = as_stream(stream_);
   if (dtype == NT_BF16) {
     NT_REQUIRE(amax_out == nullptr, NT_EINVAL, "amax_out is fp32 only");
@@ -380,6 +388,7 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
   }
   const bool vec = (h % 4 == 0) && aligned16(Xv) && aligned16(Xe) && aligned16(H0) &&
                    (S == nullptr || aligned16(S));
+  NT_REQUIRE(ld_out == h || vec, NT_EINVAL, "padded output rows need 16-byte aligned pointers");
   if (S != nullptr) {
     if (V == 0) return NT_OK;
     NT_REQUIRE(seg_ptr && (perm || E == 0), NT_EINVAL, "fused aggregation needs the dst CSR");
@@ -395,12 +404,12 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
           NT_DISPATCH_RA(reduce, act,
                          (init_aggregate_wave<R_, A_, 1><<<grid, 256, 0, stream>>>(
                              (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
-                             act_alpha, (float4*)H0, (float4*)S, amax_out)));
+                             act_alpha, (float4*)H0, (float4*)S, amax_out, lo4)));
         } else {
           NT_DISPATCH_RA(reduce, act,
                          (init_aggregate_wave<R_, A_, 2><<<grid, 256, 0, stream>>>(
                              (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
-                             act_alpha, (float4*)H0, (float4*)S, amax_out)));
+                             act_alpha, (float4*)H0, (float4*)S, amax_out, lo4)));
         }
         NT_LAUNCH_CHECK();
         return NT_OK;
@@ -409,7 +418,7 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
         NT_DISPATCH_RA(reduce, act,
                        (init_aggregate_vec4<R_, A_><<<grid, 256, 0, stream>>>(
                            (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
-                           act_alpha, (float4*)H0, (float4*)S)));
+                           act_alpha, (float4*)H0, (float4*)S, hv)));
       }
     } else {
       const int grid = grid_for(V * h, 256, 256 * 32);
@@ -431,7 +440,7 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
     if (vec) {
       const int64_t hv = h / 4;
       init_only_vec4<<<grid_for(E * hv, 256, 256 * 32), 256, 0, stream>>>(
-          (const float4*)Xv, (const float4*)Xe, src, E, hv, (float4*)H0, amax_out);
+          (const float4*)Xv, (const float4*)Xe, src, E, hv, (float4*)H0, amax_out, lo4);
     } else {
       init_only_scalar<<<grid_for(E * h, 256, 256 * 32), 256, 0, stream>>>(
           (const float*)Xv, (const float*)Xe, src, E, h, (float*)H0, amax_out);

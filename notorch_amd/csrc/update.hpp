@@ -20,6 +20,9 @@ struct UpdateArgs {
   float alpha;
   float* H_out;
   hipStream_t stream;
+  // row pitches in elements (0: dense rows of h): H and S inputs, H_out and S_out outputs (fp32 fused
+  // layer kernel only)
+  int64_t ldi = 0, ldo = 0;
 };
 
 // bf16x6 fp32-emulation kernel (update_x6.hip): h % 4 == 0 and 97 <= h <= 512.

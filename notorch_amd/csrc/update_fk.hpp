@@ -128,6 +128,9 @@ struct Args {
   float* amax_out;       // may be NULL: [0] max over H_out, [1] max over S_out (atomic max)
   int64_t V, E;
   int h, hv, KS, NT, nchunks;
+  // row pitches: ldiv = 16-B gather pieces per input row of H and S (fp32 ld / 4, bf16 ld / 8); ldic /
+  // ldoc = 4-column pieces per input (H residual) / output (H_out, S_out) row.  = hv, h / 4 for dense rows
+  int ldiv, ldic, ldoc;
   int residual, act;
   float alpha;
   const int* tile_ptr;  // NULL: fixed tiles of 16 RT rows in edge order (no aggregation)
@@ -236,7 +239,7 @@ __device__ __forceinline__ int4 row_raw(const Args& a, TileHead th, int row) {
 // float4 offsets of the S[src] and H[rev] rows (-1: none / row past the tile)
 __device__ __forceinline__ int2 row_offsets(const Args& a, int4 raw, bool valid) {
   const bool sok = valid && raw.y >= 0 && raw.y < a.V, qok = valid && raw.z >= 0 && raw.z < a.E;
-  return int2{sok ? raw.y * a.hv : -1, qok ? raw.z * a.hv : -1};
+  return int2{sok ? raw.y * a.ldiv : -1, qok ? raw.z * a.ldiv : -1};
 }
 
 // emap entry {edge (-1 past the tile), node, flags, 0}
@@ -262,6 +265,7 @@ struct State {
   // constants of the thread / launch
   int lane, wave, fr, g16, grt, grow, kp0, hv, hc, NT, CTC;  // hv: 16-B gather pieces per row,
                                                            // hc: 4-column output pieces per row
+  int li, lo;  // row pitches in 4-column pieces: input (residual H), output (H_out, S_out)
   float sA, sAW, inv;
   int rtabl;  // FK_RTABL builds: Args::rtabl
   char* abuf;
@@ -516,7 +520,7 @@ __device__ __forceinline__ void fk_resid_load(State<RT, CT, GD, PREC, NW>& st, c
 #if FK_RTABL
     if (st.rtabl & 8) e = 0;
 #endif
-    const int64_t r = (int64_t)(e >= 0 ? e : 0) * st.hc + pc;
+    const int64_t r = (int64_t)(e >= 0 ? e : 0) * st.li + pc;
     if constexpr (PREC == 1) {  // 4 bf16 (8 B), widened by fk_resid_scale once they have landed
       const uint2 v = reinterpret_cast<const uint2*>(a.H)[r];
       st.acc[rt][j] = __builtin_bit_cast(f32x4, uint4{v.x, v.y, 0u, 0u});
@@ -585,7 +589,7 @@ template <int RTI, int J, int RT, int CT, int AACT, bool SUMONLY, int MAXL, int 
 __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC, NW>& st, const Args& a, const EpiCtx& x0, int pc,
                                            bool pok, const f32x4& bj, f32x4& carry, float& ccnt) {
   if (16 * RTI < x0.n) {
-    const int hc = st.hc;
+    const int lo = st.lo;
     const int4 ri = x0.em[16 * RTI + st.fr];
     f32x4 o;
     uint2 ob = uint2{0u, 0u};  // bf16: the stored (rounded) H_out piece
@@ -605,9 +609,9 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC, NW>& st, cons
 #endif
     if (rok && (ABL & 64) == 0) {
       if constexpr (PREC == 1) {
-        reinterpret_cast<uint2*>(x0.O4)[(int64_t)ri.x * hc + pc] = ob;
+        reinterpret_cast<uint2*>(x0.O4)[(int64_t)ri.x * lo + pc] = ob;
       } else {
-        x0.O4[(int64_t)ri.x * hc + pc] = o;
+        x0.O4[(int64_t)ri.x * lo + pc] = o;
         st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
       }
     }
@@ -671,9 +675,9 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC, NW>& st, cons
         f32x4 r = x;
         if (!SUMONLY && a.reduce == NT_MEAN) r = x / cnt;
         if constexpr (PREC == 1) {
-          reinterpret_cast<uint2*>(x0.SO4)[(int64_t)ri.y * hc + pc] = bf4_pack(r[0], r[1], r[2], r[3]);
+          reinterpret_cast<uint2*>(x0.SO4)[(int64_t)ri.y * lo + pc] = bf4_pack(r[0], r[1], r[2], r[3]);
         } else {
-          x0.SO4[(int64_t)ri.y * hc + pc] = r;
+          x0.SO4[(int64_t)ri.y * lo + pc] = r;
           st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(r[0]), fabsf(r[1])), fmaxf(fabsf(r[2]), fabsf(r[3]))));
         }
       }
@@ -755,7 +759,7 @@ __device__ __forceinline__ void fk_epi3_resid(State<RT, CT, GD, PREC, NW>& st, c
 #pragma unroll
   for (int m = 0; m < RT; ++m) {
     const int e = em[rg + 16 * m].x;
-    const int64_t r = (int64_t)(e >= 0 ? e : 0) * st.hc + pc;
+    const int64_t r = (int64_t)(e >= 0 ? e : 0) * st.li + pc;
     if constexpr (PREC == 1) {
       const uint2 v = reinterpret_cast<const uint2*>(a.H)[r];
       rr[m] = __builtin_bit_cast(f32x4, uint4{v.x, v.y, 0u, 0u});
@@ -814,13 +818,13 @@ __device__ __forceinline__ void fk_epi3_group(State<RT, CT, GD, PREC, NW>& st, c
             const f32x4 h4 = resid ? f32x4{w.x, w.y, w.z, w.w} : f32x4{0.f, 0.f, 0.f, 0.f};
             const uint2 ob = bf4_pack((v[0] + b4[0]) + h4[0], (v[1] + b4[1]) + h4[1], (v[2] + b4[2]) + h4[2],
                                       (v[3] + b4[3]) + h4[3]);
-            reinterpret_cast<uint2*>(a.O)[(int64_t)e * st.hc + pc] = ob;
+            reinterpret_cast<uint2*>(a.O)[(int64_t)e * st.lo + pc] = ob;
             const float4 s4 = bf4_widen(uint4{ob.x, ob.y, 0u, 0u});
             o = f32x4{s4.x, s4.y, s4.z, s4.w};
           } else {
 #pragma unroll
             for (int q = 0; q < 4; ++q) o[q] = fmaf(v[q], st.inv, b4[q]) + (resid ? rr[m][q] : 0.f);
-            reinterpret_cast<f32x4*>(a.O)[(int64_t)e * st.hc + pc] = o;
+            reinterpret_cast<f32x4*>(a.O)[(int64_t)e * st.lo + pc] = o;
             st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
           }
           if (a.SO != nullptr) {
@@ -861,9 +865,9 @@ __device__ __forceinline__ void fk_epi3_group(State<RT, CT, GD, PREC, NW>& st, c
             }
             const int node = em[r0].y;
             if constexpr (PREC == 1) {
-              reinterpret_cast<uint2*>(a.SO)[(int64_t)node * st.hc + pc] = bf4_pack(x[0], x[1], x[2], x[3]);
+              reinterpret_cast<uint2*>(a.SO)[(int64_t)node * st.lo + pc] = bf4_pack(x[0], x[1], x[2], x[3]);
             } else {
-              reinterpret_cast<f32x4*>(a.SO)[(int64_t)node * st.hc + pc] = x;
+              reinterpret_cast<f32x4*>(a.SO)[(int64_t)node * st.lo + pc] = x;
               st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
             }
           }
@@ -910,7 +914,7 @@ __device__ __forceinline__ void fk_epi4_col(State<RT, CT, GD, PREC, NW>& st, con
         for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[rt][J][q], st.inv, bj[q]);
         const int e = em[16 * rt + st.fr].x;
         if (e >= 0 && pok) {
-          reinterpret_cast<f32x4*>(a.O)[(int64_t)e * hc + pc] = o;
+          reinterpret_cast<f32x4*>(a.O)[(int64_t)e * st.lo + pc] = o;
           st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
         }
         f32x4 m;
@@ -938,7 +942,7 @@ __device__ __forceinline__ void fk_epi4_col(State<RT, CT, GD, PREC, NW>& st, con
       for (int r = r0 + 1; r < r1; ++r) x = x + *reinterpret_cast<const f32x4*>(st.stage + r * kSP4 + 4 * p4);
       const int4 re = em[r1 - 1];  // the node's last row: its id and end flag (hub rows carry none)
       if ((re.z & kFlagEnd) && re.x >= 0 && pcn < hc) {
-        reinterpret_cast<f32x4*>(a.SO)[(int64_t)re.y * hc + pcn] = x;
+        reinterpret_cast<f32x4*>(a.SO)[(int64_t)re.y * st.lo + pcn] = x;
         st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
       }
     }
@@ -1037,6 +1041,8 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   st.kp0 = RT == NW ? 2 * st.g16 : 2 * st.g16 + (st.wave >> 2);
   st.hv = a.hv;       // fp32: h / 4 (16-B pieces of 4 floats); bf16: h / 8 (of 8 bf16)
   st.hc = a.h / 4;    // 4-column output pieces per row
+  st.li = a.ldic;
+  st.lo = a.ldoc;
   st.rtabl = a.rtabl;
   st.NT = a.NT;
   st.CTC = NW * CT;

@@ -1008,6 +1008,20 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   a.E = u.E;
   a.h = (int)u.h;
   a.hv = (int)(u.h / 4);
+  {
+    const int64_t ldi = u.ldi ? u.ldi : u.h, ldo = u.ldo ? u.ldo : u.h;
+    NT_REQUIRE(ldi >= u.h && ldo >= u.h && ldi % 4 == 0 && ldo % 4 == 0, NT_EINVAL,
+               "row pitches must be >= h and multiples of 4");
+    NT_REQUIRE((u.E * ldi) / 4 < (int64_t(1) << 31) && (u.V * ldi) / 4 < (int64_t(1) << 31) &&
+                   (u.E * ldo) / 4 < (int64_t(1) << 31) && (u.V * ldo) / 4 < (int64_t(1) << 31),
+               NT_EUNSUPPORTED, "fp32 update: E*ld and V*ld must stay below 2^33");
+    a.ldiv = a.ldic = (int)(ldi / 4);
+    a.ldoc = (int)(ldo / 4);
+#ifdef NT_DIAG
+    NT_REQUIRE((ldi == u.h && ldo == u.h) || !(fk2_selected(u.h) || fw_active(u.h, NT_F32, u.act, reduce, aact)),
+               NT_EUNSUPPORTED, "diagnostic walks take dense rows only");
+#endif
+  }
   // an even number of k-steps, at least four, per tile (update_fk_kernel runs two steps per inner
   // trip and gathers three steps ahead, within the next tile at most); a k-step past the image reads
   // zeros (buffer range) and masked-off pieces
@@ -1133,6 +1147,8 @@ int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* 
   a.E = u.E;
   a.h = (int)u.h;
   a.hv = (int)(u.h / 8);  // 16-B gather pieces of 8 bf16
+  a.ldiv = a.hv;
+  a.ldic = a.ldoc = (int)(u.h / 4);
   a.KS = fk::ks_for(u.h) < 4 ? 4 : (fk::ks_for(u.h) + 1) / 2 * 2;
   a.NT = fk::nt_for(u.h);
   a.nchunks = 1;

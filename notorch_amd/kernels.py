@@ -109,6 +109,28 @@ def _require_feat(name: str, t: Tensor, dtype: torch.dtype | None = None) -> int
     return _DTYPE_CODES[t.dtype]
 
 
+def _row_pitch(name: str, t: Tensor, dtype: torch.dtype | None = None) -> int:
+    """Row pitch (elements) of a 2-D feature tensor that is contiguous or a row-padded view
+    (X[:, :h] of an [n, ld] fp32 buffer: unit column stride, 16-byte row pitch)."""
+    if t.dim() != 2:
+        raise ValueError(f"{name} must be 2-D")
+    if t.is_contiguous():
+        _require_feat(name, t, dtype)
+        return t.shape[1]
+    if t.dtype != torch.float32 or t.stride(1) != 1 or t.stride(0) < t.shape[1] or t.stride(0) % 4:
+        raise ValueError(f"{name} must be contiguous (or an fp32 row-padded view with a pitch % 4 == 0)")
+    if dtype is not None and t.dtype != dtype:
+        raise TypeError(f"{name} is {t.dtype} but the other operands are {dtype}")
+    return t.stride(0)
+
+
+def padded_rows(n: int, h: int, pitch: int, dtype: torch.dtype, device) -> Tensor:
+    """An n x h tensor whose rows sit ``pitch`` elements apart (a view of an n x pitch buffer)."""
+    if pitch == h:
+        return torch.empty(n, h, dtype=dtype, device=device)
+    return torch.empty(max(n, 1), pitch, dtype=dtype, device=device)[:n, :h]
+
+
 def _require_i64(name: str, t: Tensor) -> None:
     if t.dtype != torch.int64:
         raise TypeError(f"{name} must be int64 (reference index dtype), got {t.dtype}")
@@ -186,9 +208,12 @@ def dmpnn_init(
     act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
     reduce: str = "sum",
     amax: Tensor | None = None,
+    pitch: int | None = None,
 ) -> tuple[Tensor, Tensor | None]:
     """H0 = Xv[src] + Xe, optionally fused with S = scatter(act(H0), dst) (needs the dst CSR).
-    amax (fp32, 2 zero-filled device floats): raised to max|H0|, max|S| (layer 0's amax_in)."""
+    amax (fp32, 2 zero-filled device floats): raised to max|H0|, max|S| (layer 0's amax_in).
+    pitch (fp32, h % 4 == 0, h >= 128 with the aggregation): H0 and S as row-padded views whose rows
+    sit ``pitch`` floats apart (nt_dmpnn_init's ld_out)."""
     dev = _require_device(Xv, Xe, src, seg_ptr, perm, amax)
     _require_amax(amax, Xv.dtype)
     code = _require_feat("node_feats", Xv)
@@ -202,14 +227,15 @@ def dmpnn_init(
     E = Xe.shape[0]
     if src.numel() != E:
         raise ValueError("src must have one entry per edge")
-    H0 = torch.empty(E, h, dtype=Xv.dtype, device=dev)
+    ld = h if pitch is None else int(pitch)
+    H0 = padded_rows(E, h, ld, Xv.dtype, dev)
     S = None
     if seg_ptr is not None:
-        S = torch.empty(V, h, dtype=Xv.dtype, device=dev)
+        S = padded_rows(V, h, ld, Xv.dtype, dev)
     lib = _lib.load()
     _run(dev, lib.nt_dmpnn_init,
          _ptr(Xv), _ptr(Xe), _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h, act[0], act[1],
-         reduce_code(reduce), code, _ptr(H0), _ptr(S), _ptr(amax), _stream(dev))
+         reduce_code(reduce), code, _ptr(H0), _ptr(S), _ptr(amax), 0 if ld == h else ld, _stream(dev))
     return H0, S
 
 
@@ -599,9 +625,13 @@ def dmpnn_update_fused(
     row_table: Tensor | None = None,
     out: Tensor | None = None,
     S_out: Tensor | None = None,
+    pitch_out: int | None = None,
 ) -> tuple[Tensor, Tensor | None]:
     """H_out = (residual ? H : 0) + (S[src] - act(H[rev])) @ W^T + b and, with a tile plan (tiles of at
     most ``tile_rows`` rows), S_out = scatter(agg_act(H_out), dst, reduce) in the same persistent launch.
+
+    fp32: H and S may be row-padded views with one common pitch (see dmpnn_init's ``pitch``); H_out /
+    S_out are allocated with rows ``pitch_out`` floats apart (default: dense), or given with one pitch.
 
     fp32: ``amax_in`` = (max|H|, max|S|) on the device (computed here with nt_absmax when not given);
     ``amax_out`` (2 zero-filled floats) receives max|H_out|, max|S_out| for the next layer.
@@ -609,8 +639,10 @@ def dmpnn_update_fused(
     when not given (cache it per graph).
     ``zero_fill`` must be True when some node has no in-edge (its S_out row is then 0)."""
     dev = _require_device(H, S, src, rev, Wp, bias, out, S_out, perm, amax_in, amax_out)
-    code = _require_feat("H", H)
-    _require_feat("S", S, H.dtype)
+    ld_in = _row_pitch("H", H)
+    code = _DTYPE_CODES[H.dtype]
+    if _row_pitch("S", S, H.dtype) != ld_in:
+        raise ValueError("H and S must share one row pitch")
     _require_i64("src", src)
     _require_i64("rev_index", rev)
     _require_amax(amax_in, H.dtype)
@@ -626,7 +658,8 @@ def dmpnn_update_fused(
         if bias.numel() != h:
             raise ValueError("bias must have h entries")
     if out is None:
-        out = torch.empty_like(H)
+        out = padded_rows(E, h, h if pitch_out is None else int(pitch_out), H.dtype, dev)
+    ld_out = _row_pitch("out", out, H.dtype)
     tile_ptr = dsts = None
     ntiles = 0
     if plan is not None:
@@ -634,9 +667,14 @@ def dmpnn_update_fused(
         if perm is None or perm.dtype != torch.int32 or perm.numel() != E:
             raise ValueError("fused aggregation needs the int32 dst CSR permutation")
         if S_out is None:
-            S_out = (torch.zeros if zero_fill else torch.empty)(V, h, dtype=H.dtype, device=dev)
-        elif zero_fill:
-            S_out.zero_()
+            S_out = padded_rows(V, h, ld_out, H.dtype, dev)
+            if zero_fill:
+                S_out.zero_()
+        else:
+            if _row_pitch("S_out", S_out, H.dtype) != ld_out:
+                raise ValueError("out and S_out must share one row pitch")
+            if zero_fill:
+                S_out.zero_()
     else:
         perm = None
         S_out = None
@@ -651,7 +689,7 @@ def dmpnn_update_fused(
          _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
          act[0], act[1], _ptr(tile_ptr), ntiles, int(tile_rows), int(max_in_degree), _ptr(perm), _ptr(dsts),
          _ptr(row_table), reduce_code(reduce), agg_act[0], agg_act[1], code, _ptr(amax_in), _ptr(amax_out),
-         _ptr(out), _ptr(S_out), _stream(dev))
+         _ptr(out), _ptr(S_out), 0 if ld_in == h else ld_in, 0 if ld_out == h else ld_out, _stream(dev))
     return out, S_out
 
 

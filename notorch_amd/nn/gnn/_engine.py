@@ -373,12 +373,26 @@ def block_forward(
         H, _ = K.dmpnn_init(Xv, Xe, src, amax=a0)
         S = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks, amax=None if a0 is None else a0[1:2])
     else:
-        H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce, amax=a0)
+        pitch = row_pitch(Xv.shape[1], Xv.dtype) if (not keep_states and drop is None) else None
+        H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce, amax=a0, pitch=pitch)
     return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop,
                            amax)
 
 
+def row_pitch(h: int, dtype: torch.dtype) -> Optional[int]:
+    """Row pitch of the intermediate H_l / S_l of an inference forward: fp32 rows of h % 8 != 0 floats
+    padded to a 32-byte multiple (h = 300 -> 304), so that no row shares a 32-B sector with its
+    neighbour: the dst-ordered row stores of the init and of the layer kernels then write whole
+    sectors, and every 16-B gather piece of a row lies in one sector (measured with tools/r5_pitch.sh:
+    the layer kernel at h = 304 runs 113.5 us against 121.1 at h = 300, the same MFMA work).  None:
+    dense rows (h % 8 == 0 already, bf16, h < 128, or NT_ROW_PAD=0)."""
+    if dtype != torch.float32 or h % 4 or h % 8 == 0 or h < 128 or not _ROW_PAD:
+        return None
+    return (h + 7) // 8 * 8
+
+
 _NO_AMAX = torch.empty(0)  # a state without a valid amax row (bf16, or a path that skips the chain)
+_ROW_PAD = os.environ.get("NT_ROW_PAD", "1") != "0"  # A/B: 0 = dense intermediate rows
 
 
 # fp32 relu / sum layers on graphs of at most this many edges take 64-row tiles walked by two 4-wave
@@ -488,6 +502,8 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
     if plan is not None:
         return _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, residual, keep_states,
                               amax)
+    if not H.is_contiguous():  # row-padded init output (row_pitch) on a graph the fused plan cannot take
+        H, S = H.contiguous(), S.contiguous()
     states = []
     spare: Optional[Tensor] = None  # ping-pong buffer when states are not kept
     # graphs the fused plan cannot take (in-degree > 32): fp32 still runs the persistent layer kernel,
@@ -562,6 +578,10 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
         if timer is not None:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
+        # intermediate layers keep the input's row pitch (row_pitch); the block's outputs are dense
+        pitch = H.shape[1] if (last or hubs is not None) else H.stride(0)
+        if spare_H is not None and spare_H.stride(0) != pitch:
+            spare_H = spare_S = None
         Hn, Sn = K.dmpnn_update_fused(
             H, S, src, rev, Wps[l], None if biases[l] is None else biases[l].detach(),
             residual=residual, act=act, plan=(tile_ptr, ntiles, dsts), tile_rows=rows, max_in_degree=maxdeg,
@@ -569,7 +589,7 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
             zero_fill=zf_out if last else zf_mid,
             amax_in=None if amax is None else amax[l],
             amax_out=None if (amax is None or last) else amax[l + 1],  # row d has no reader
-            row_table=rt, out=spare_H, S_out=None if last else spare_S,
+            row_table=rt, out=spare_H, S_out=None if last else spare_S, pitch_out=pitch,
         )
         if timer is not None:
             ev[1].record()

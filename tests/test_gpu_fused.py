@@ -454,3 +454,65 @@ def test_weight_grad_fk(h, E, act, gs, xs):
     assert_parity(db, Gr.double().sum(0), FP32_NORM_TOL, f"db h={h} E={E}")
     dW2, db2 = K.weight_grad(*args, act=K.act_code(mod), amax_G=amax_G, amax_HS=amax_HS)
     assert torch.equal(dW, dW2) and torch.equal(db, db2)
+
+
+@pytest.mark.parametrize("h,pitch", [(300, 304), (300, 320), (132, 136)])
+@pytest.mark.parametrize("rows", [64, 128])
+def test_row_padded_init_and_layer_bit_identical(h, pitch, rows):
+    """Row-padded H / S (ABI 7 ld_out of nt_dmpnn_init, ld_in / ld_out of nt_dmpnn_update_fused):
+    the same values, bit for bit, as the dense rows -- the pitch moves rows, not arithmetic -- for a
+    padded -> padded layer and a padded -> dense one (the block's last layer)."""
+    K = _K()
+    G = _graph("qm9", 200, seed=21)
+    V, E = G.num_nodes, G.num_edges
+    dst_ptr, perm, plan, zf = _plan(G)
+    deg = int((dst_ptr[1:] - dst_ptr[:-1]).max())
+    plan = K.tile_plan(dst_ptr, E, deg, rows=rows, ncu=K.PLAN_NCU)
+    torch.manual_seed(3)
+    Xv, Xe = torch.randn(V, h, device=DEV), torch.randn(E, h, device=DEV)
+    W, b = torch.randn(h, h, device=DEV) / h ** 0.5, torch.randn(h, device=DEV)
+    Wp = K.pack_weights(W)
+    src, rev = G.edge_index[0].contiguous().to(DEV), G.rev_index.to(DEV)
+    relu = K.act_code(nn.ReLU())
+    ident = K.act_code(nn.Identity())
+    outs = {}
+    for ld in (h, pitch):
+        am = torch.zeros(3, 2, device=DEV)
+        H0, S0 = K.dmpnn_init(Xv, Xe, src, dst_ptr, perm, act=relu, amax=am[0], pitch=ld)
+        assert H0.shape == (E, h) and H0.stride(0) == ld and S0.stride(0) == ld
+        rt = K.dmpnn_row_table(perm, plan[2], src, rev, V)
+        H1, S1 = K.dmpnn_update_fused(H0, S0, src, rev, Wp, b, act=relu, plan=plan, tile_rows=rows,
+                                      max_in_degree=deg, perm=perm, agg_act=relu, zero_fill=zf, amax_in=am[0],
+                                      amax_out=am[1], row_table=rt, pitch_out=ld)
+        assert H1.stride(0) == ld and S1.stride(0) == ld
+        H2, S2 = K.dmpnn_update_fused(H1, S1, src, rev, Wp, b, act=relu, plan=plan, tile_rows=rows,
+                                      max_in_degree=deg, perm=perm, agg_act=ident, zero_fill=zf, amax_in=am[1],
+                                      amax_out=am[2], row_table=rt)
+        assert H2.is_contiguous() and S2.is_contiguous()
+        outs[ld] = [t.contiguous() for t in (H0, S0, H1, S1, H2, S2)] + [am]
+    for name, a, c in zip(("H0", "S0", "H1", "S1", "H2", "S2", "amax"), outs[h], outs[pitch]):
+        assert torch.equal(a, c), name
+
+
+def test_block_forward_row_padding_is_invisible(monkeypatch):
+    """The inference forward runs its intermediate layers on row-padded buffers (h = 300 -> 304):
+    the block's outputs are dense tensors and equal, bit for bit, to the dense-row forward."""
+    from notorch_amd.nn import ChempropBlock
+    from notorch_amd.nn.gnn import _engine
+
+    G = _graph("qm9", 300, seed=22)
+    h = 300
+    torch.manual_seed(5)
+    Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)
+    blk = ChempropBlock(hidden_dim=h, depth=3).to(DEV).eval()
+    Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
+    res = {}
+    for pad in (True, False):
+        monkeypatch.setattr(_engine, "_ROW_PAD", pad)
+        with torch.no_grad():
+            out = blk(Gd)
+        assert out.node_feats.is_contiguous() and out.edge_feats.is_contiguous()
+        res[pad] = (out.node_feats.clone(), out.edge_feats.clone())
+    monkeypatch.setattr(_engine, "_ROW_PAD", True)
+    assert _engine.row_pitch(h, torch.float32) == 304
+    assert torch.equal(res[True][0], res[False][0]) and torch.equal(res[True][1], res[False][1])
