@@ -51,7 +51,7 @@ if fetch and write:
     kern = os.environ.get("NT_PROFILE_KERNEL", "")
     if not kern:  # the bench line's dominant kernel (e.g. update_fk_kernel -> update_fk)
         for b in sys.argv[3:]:
-            k = json.loads(open(b).read().strip().splitlines()[-1])["roofline"]["kernel"].split()[0]
+            k = json.loads(open(b).read().strip().splitlines()[-1])["roofline"]["kernel"].split()[0].rstrip(":")
             kern = k[: -len("_kernel")] if k.endswith("_kernel") else k
     kern = kern or "update"
     traffic = read_pmc_traffic(f"{fetch[0]},{write[0]}", kern)
