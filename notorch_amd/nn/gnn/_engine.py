@@ -807,7 +807,7 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
     scatter_min): H_last = the forward's H_d, for the final node scatter's arg.
     Returns (dXv, dXe, [dW_l], [db_l])."""
     maxmin = reduce in ("max", "min")
-    E, h = states[0][0].shape if states else dH.shape
+    E, h = states[0][0].shape if states else (dH.shape if dH is not None else (rev.numel(), dnode.shape[1]))
     src_ptr, src_perm, rev_ptr, rev_perm = backward_layout(lay, src, rev, V, E)
     mean_ptr = lay.dst_ptr if reduce == "mean" else None
     d = len(weights)
@@ -921,6 +921,9 @@ class ChempropBlockFunction(torch.autograd.Function):
         ctx.save_for_backward(Xv, Xe, edge_index, rev,
                               *[p if p is not None else torch.empty(0) for p in params], *flat)
         ctx.cfg = (act_mod, act, reduce, residual, nlayers, [p is None for p in params], lay, kernel_bwd, drop)
+        # an output the loss does not use arrives as None instead of an E x h zero tensor: the backward
+        # then writes G = dnode[dst] whole (no zero fill, no zero base read by the gather)
+        ctx.set_materialize_grads(False)
         return node, H
 
     @staticmethod

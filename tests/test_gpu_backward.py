@@ -269,3 +269,34 @@ def test_backward_does_not_route_through_torch_block_for_sum(monkeypatch):
 
     monkeypatch.setattr(_engine, "_torch_block", boom)
     _check(_graph("qm9", 8, seed=13), 32, depth=2)
+
+
+@pytest.mark.parametrize("uses", ["node", "edge"])
+def test_block_grads_one_output_unused(uses):
+    """A loss on one of the block's two outputs only: the other's gradient arrives as None (the
+    Function does not materialise zeros), and the backward starts from the used one alone."""
+    from notorch_amd.nn import ChempropBlock, Sum
+
+    G = _graph("qm9", 24, seed=7)
+    h = 64
+    Xv, Xe = _embed(G, h)
+    torch.manual_seed(2)
+    blk = ChempropBlock(h, depth=3)
+    Ws, bs = dmpnn_ref.block_params(blk)
+    Ws = [W.detach().double().requires_grad_(True) for W in Ws]
+    bs = [b.detach().double().requires_grad_(True) for b in bs]
+    Xv_r, Xe_r = Xv.double().requires_grad_(True), Xe.double().requires_grad_(True)
+    n, e = dmpnn_ref.chemprop_block(Xv_r, Xe_r, G.edge_index, G.rev_index, Ws, bs)
+    w = torch.linspace(-1, 1, h, dtype=torch.float64)
+    loss = dmpnn_ref.readout(n, G.batch_node_index, len(G), "sum").pow(2).sum() if uses == "node" \
+        else (e * w).sum()
+    loss.backward()
+    blk = blk.to(DEV).train()
+    Xv_d, Xe_d = Xv.to(DEV).requires_grad_(True), Xe.to(DEV).requires_grad_(True)
+    out = blk(G.update(node_feats=Xv_d, edge_feats=Xe_d).to(DEV))
+    dloss = Sum()(out).pow(2).sum() if uses == "node" else (out.edge_feats * w.float().to(DEV)).sum()
+    dloss.backward()
+    assert_parity(Xv_d.grad, Xv_r.grad, GRAD_TOL, "dXv")
+    assert_parity(Xe_d.grad, Xe_r.grad, GRAD_TOL, "dXe")
+    for l, (m, W) in enumerate(zip(blk._chemprop_layers(), Ws)):
+        assert_parity(m.linear.weight.grad, W.grad, GRAD_TOL, f"dW[{l}]")
