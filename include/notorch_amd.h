@@ -202,14 +202,15 @@ NT_API int nt_segment_reduce_chunked(const void* X, const int32_t* perm, const i
  * nt_segment_reduce_chunked
  * on the dst CSR; H0 E x h, S V x h.  Same H0 as nt_dmpnn_init (bit-identical), same S as
  * nt_segment_reduce_chunked of that H0.  amax_out (may be NULL): 2 zero-filled device floats raised to
- * max|H0|, max|S|.
+ * max|H0|, max|S|.  ld_out (ABI 7): row pitch in elements of H0 and S (0 = h; >= h, a multiple of 4;
+ * the partial rows stay dense).
  */
 NT_API int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64_t* src, const int32_t* perm,
                                  const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
                                  const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb,
                                  const int32_t* seg_ptr, int64_t V, int64_t E, int64_t h, int act,
                                  float act_alpha, int reduce, int dtype, float* partial, void* H0, void* S,
-                                 float* amax_out, void* stream);
+                                 float* amax_out, int64_t ld_out, void* stream);
 
 /* Bytes of the packed weight image for one h x h layer (see nt_dmpnn_pack_weight). */
 NT_API size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype);
@@ -299,11 +300,13 @@ NT_API int nt_dmpnn_mark_hub_rows(void* row_table, int64_t E, const int32_t* dst
  *   out[v] = reduce_{p in [seg_ptr[v], seg_ptr[v+1])} act(X[perm[p]])   for v in hubs[0 .. nhub)
  * (rows of other nodes untouched).  amax_out (may be NULL): one device float raised to max|out[v]|
  * (the fused layer's max|S_out| slot).  fp32, h % 4 == 0, 16-byte aligned X / out; deterministic
- * (16 contiguous row ranges per hub, combined in order).
+ * (16 contiguous row ranges per hub, combined in order).  ld (ABI 7): row pitch in elements of X and
+ * out (0 = h; >= h, a multiple of 4).
  */
 NT_API int nt_dmpnn_hub_aggregate(const void* X, const int32_t* perm, const int32_t* seg_ptr,
                                   const int32_t* hubs, int64_t nhub, int64_t h, int reduce, int act,
-                                  float act_alpha, int dtype, float* amax_out, void* out, void* stream);
+                                  float act_alpha, int dtype, float* amax_out, void* out, int64_t ld,
+                                  void* stream);
 
 /*
  * Row capacity of one nt_dmpnn_update_fused tile for a layer of hidden size h, activation act and

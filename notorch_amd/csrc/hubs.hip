@@ -44,7 +44,7 @@ template <int R, int ACT>
 __global__ void __launch_bounds__(kHubWaves * 64) hub_aggregate_kernel(
     const float4* __restrict__ X, const int32_t* __restrict__ perm, const int32_t* __restrict__ seg_ptr,
     const int32_t* __restrict__ hubs, int hv, int P, int act, float alpha, float4* __restrict__ out,
-    float* __restrict__ amax) {
+    float* __restrict__ amax, int ld) {  // ld: row pitch of X and out in 16-B pieces
   __shared__ float4 part[kHubWaves][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int s = hubs[blockIdx.x];
@@ -60,7 +60,7 @@ __global__ void __launch_bounds__(kHubWaves * 64) hub_aggregate_kernel(
 #pragma unroll
     for (int u = 0; u < kHubBatch; ++u) {
       const int32_t p = j + u < r1 ? j + u : r1 - 1;
-      v[u] = X[(int64_t)perm[p] * hv + cc];
+      v[u] = X[(int64_t)perm[p] * ld + cc];
     }
 #pragma unroll
     for (int u = 0; u < kHubBatch; ++u)
@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(kHubWaves * 64) hub_aggregate_kernel(
     }
     if (n == 0) r = make_float4(0.f, 0.f, 0.f, 0.f);
     if (ok) {
-      out[(int64_t)s * hv + c] = r;
+      out[(int64_t)s * ld + c] = r;
       m = fmaxf(fmaxf(fabsf(r.x), fabsf(r.y)), fmaxf(fabsf(r.z), fabsf(r.w)));
     }
   }
@@ -105,21 +105,21 @@ __global__ void __launch_bounds__(256) mark_hub_rows_kernel(int4* __restrict__ r
 
 template <int R>
 int launch_hub(const float4* X, const int32_t* perm, const int32_t* seg_ptr, const int32_t* hubs,
-               int64_t nhub, int hv, int act, float alpha, float4* out, float* amax, hipStream_t stream) {
+               int64_t nhub, int hv, int act, float alpha, float4* out, float* amax, int ld, hipStream_t stream) {
   const int nslab = (hv + 63) / 64, P = (hv + nslab - 1) / nslab;
   const dim3 grid((unsigned)nhub, (unsigned)nslab);
   switch (act) {
     case NT_ACT_IDENTITY:
       hub_aggregate_kernel<R, NT_ACT_IDENTITY><<<grid, kHubWaves * 64, 0, stream>>>(X, perm, seg_ptr, hubs, hv, P,
-                                                                                 act, alpha, out, amax);
+                                                                                 act, alpha, out, amax, ld);
       break;
     case NT_ACT_RELU:
       hub_aggregate_kernel<R, NT_ACT_RELU><<<grid, kHubWaves * 64, 0, stream>>>(X, perm, seg_ptr, hubs, hv, P, act,
-                                                                             alpha, out, amax);
+                                                                             alpha, out, amax, ld);
       break;
     default:
       hub_aggregate_kernel<R, -1><<<grid, kHubWaves * 64, 0, stream>>>(X, perm, seg_ptr, hubs, hv, P, act, alpha,
-                                                                    out, amax);
+                                                                    out, amax, ld);
   }
   NT_LAUNCH_CHECK();
   return NT_OK;
@@ -145,7 +145,8 @@ extern "C" int nt_dmpnn_mark_hub_rows(void* row_table, int64_t E, const int32_t*
 
 extern "C" int nt_dmpnn_hub_aggregate(const void* X, const int32_t* perm, const int32_t* seg_ptr,
                                       const int32_t* hubs, int64_t nhub, int64_t h, int reduce, int act,
-                                      float act_alpha, int dtype, float* amax_out, void* out, void* stream_) {
+                                      float act_alpha, int dtype, float* amax_out, void* out, int64_t ld,
+                                      void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_hub_aggregate: fp32 only");
@@ -156,14 +157,16 @@ extern "C" int nt_dmpnn_hub_aggregate(const void* X, const int32_t* perm, const 
   if (nhub == 0) return NT_OK;
   NT_REQUIRE(X && seg_ptr && hubs && out && perm, NT_EINVAL, "NULL pointer");
   NT_REQUIRE(aligned16(X) && aligned16(out), NT_EINVAL, "feature pointers must be 16-byte aligned");
-  const int hv = (int)(h / 4);
+  if (ld == 0) ld = h;
+  NT_REQUIRE(ld >= h && ld % 4 == 0, NT_EINVAL, "row pitch must be >= h and a multiple of 4");
+  const int hv = (int)(h / 4), ld4 = (int)(ld / 4);
   const float4* X4 = (const float4*)X;
   float4* O4 = (float4*)out;
   hipStream_t s = as_stream(stream_);
   switch (reduce) {
-    case NT_SUM: return launch_hub<NT_SUM>(X4, perm, seg_ptr, hubs, nhub, hv, act, act_alpha, O4, amax_out, s);
-    case NT_MEAN: return launch_hub<NT_MEAN>(X4, perm, seg_ptr, hubs, nhub, hv, act, act_alpha, O4, amax_out, s);
-    case NT_MAX: return launch_hub<NT_MAX>(X4, perm, seg_ptr, hubs, nhub, hv, act, act_alpha, O4, amax_out, s);
-    default: return launch_hub<NT_MIN>(X4, perm, seg_ptr, hubs, nhub, hv, act, act_alpha, O4, amax_out, s);
+    case NT_SUM: return launch_hub<NT_SUM>(X4, perm, seg_ptr, hubs, nhub, hv, act, act_alpha, O4, amax_out, ld4, s);
+    case NT_MEAN: return launch_hub<NT_MEAN>(X4, perm, seg_ptr, hubs, nhub, hv, act, act_alpha, O4, amax_out, ld4, s);
+    case NT_MAX: return launch_hub<NT_MAX>(X4, perm, seg_ptr, hubs, nhub, hv, act, act_alpha, O4, amax_out, ld4, s);
+    default: return launch_hub<NT_MIN>(X4, perm, seg_ptr, hubs, nhub, hv, act, act_alpha, O4, amax_out, ld4, s);
   }
 }

@@ -545,7 +545,8 @@ __global__ void __launch_bounds__(256) init_chunk_partial(const float* __restric
                                                           const int32_t* __restrict__ chunk_seg,
                                                           int64_t nchunks, int64_t h, int act, float alpha,
                                                           float* __restrict__ H0, float* __restrict__ P,
-                                                          float* __restrict__ S, float* __restrict__ amax) {
+                                                          float* __restrict__ S, float* __restrict__ amax,
+                                                          int64_t lo) {  // lo: row pitch of H0 and S
   constexpr int N = Piece<float, VEC>::N;
   constexpr int RR = R == NT_MEAN ? NT_SUM : R;  // the mean divides at the end
   const int64_t hw = h / N;
@@ -580,7 +581,7 @@ __global__ void __launch_bounds__(256) init_chunk_partial(const float* __restric
           m = fmaxf(m, fabsf(y[i]));
           r[i].push(act_t<ACT>(y[i], act, alpha));
         }
-        Piece<float, VEC>::store(H0 + ed[u] * h + c, y);
+        Piece<float, VEC>::store(H0 + ed[u] * lo + c, y);
       }
     }
     const int32_t sk = chunk_seg ? chunk_seg[k] : -1;
@@ -589,7 +590,7 @@ __global__ void __launch_bounds__(256) init_chunk_partial(const float* __restric
     for (int i = 0; i < N; ++i) y[i] = r[i].acc;  // raw accumulator (chunk non-empty)
     if (sk >= 0) {
       seg_finish<R>(y, e - b);
-      Piece<float, VEC>::store(S + (int64_t)sk * h + c, y);
+      Piece<float, VEC>::store(S + (int64_t)sk * lo + c, y);
       ms = absmax_n(ms, y);
     } else {
 #pragma unroll
@@ -609,7 +610,8 @@ __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict
                                                          const int32_t* __restrict__ seg_ptr,
                                                          const int32_t* __restrict__ comb_seg,
                                                          int64_t ncomb, int64_t h,
-                                                         T* __restrict__ out, float* __restrict__ amax) {
+                                                         T* __restrict__ out, float* __restrict__ amax,
+                                                         int64_t lo) {  // lo: row pitch of out
   constexpr int N = Piece<T, VEC>::N;
   __shared__ float red[kCombG][32][N];
   const int64_t hw = h / N, nslab = (hw + 31) / 32;
@@ -666,7 +668,7 @@ __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict
         for (int q = 0; q < N; ++q) y[q] = 0.f;
       }
       seg_finish<R>(y, seg_ptr[sg + 1] - seg_ptr[sg]);
-      Piece<T, VEC>::store(out + (int64_t)sg * h + c, y);
+      Piece<T, VEC>::store(out + (int64_t)sg * lo + c, y);
       m = absmax_n(m, y);
     }
     __syncthreads();
@@ -676,22 +678,24 @@ __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict
 
 template <typename T, bool VEC, int R>
 void launch_combine(const float* P, const int32_t* chunk_ptr, const int32_t* seg_ptr, const int32_t* comb_seg,
-                    int64_t ncomb, int64_t h, T* out, float* amax, hipStream_t stream) {
+                    int64_t ncomb, int64_t h, T* out, float* amax, hipStream_t stream, int64_t lo = 0) {
   constexpr int N = Piece<T, VEC>::N;
   const int64_t blocks = ncomb * ((h / N + 31) / 32);
   if (blocks == 0) return;
   const int g = (int)(blocks < 256 * 16 ? blocks : 256 * 16);
-  seg_chunk_combine<T, VEC, R><<<g, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax);
+  seg_chunk_combine<T, VEC, R><<<g, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax,
+                                                       lo ? lo : h);
 }
 
 template <typename T, bool VEC>
 void launch_combine_r(int reduce, const float* P, const int32_t* chunk_ptr, const int32_t* seg_ptr,
-                      const int32_t* comb_seg, int64_t ncomb, int64_t h, T* out, float* amax, hipStream_t stream) {
+                      const int32_t* comb_seg, int64_t ncomb, int64_t h, T* out, float* amax, hipStream_t stream,
+                      int64_t lo = 0) {
   switch (reduce) {
-    case NT_SUM: launch_combine<T, VEC, NT_SUM>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream); break;
-    case NT_MEAN: launch_combine<T, VEC, NT_MEAN>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream); break;
-    case NT_MAX: launch_combine<T, VEC, NT_MAX>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream); break;
-    default: launch_combine<T, VEC, NT_MIN>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream); break;
+    case NT_SUM: launch_combine<T, VEC, NT_SUM>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream, lo); break;
+    case NT_MEAN: launch_combine<T, VEC, NT_MEAN>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream, lo); break;
+    case NT_MAX: launch_combine<T, VEC, NT_MAX>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream, lo); break;
+    default: launch_combine<T, VEC, NT_MIN>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax, stream, lo); break;
   }
 }
 
@@ -700,18 +704,18 @@ int launch_init_chunked(const float* Xv, const float* Xe, const int64_t* src, co
                         const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
                         const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb, const int32_t* seg_ptr,
                         int64_t nseg, int64_t h, int reduce, int act, float alpha, float* P, float* H0, float* S,
-                        float* amax, hipStream_t stream) {
+                        float* amax, int64_t lo, hipStream_t stream) {
   constexpr int N = Piece<float, VEC>::N;
   if (nchunks > 0) {
     const int g1 = grid_for(nchunks * (h / N), 256, 256 * 32);
     NT_DISPATCH_RA(reduce, act,
                    (init_chunk_partial<VEC, R_, A_><<<g1, 256, 0, stream>>>(
-                       Xv, Xe, src, perm, chunk_pos, chunk_seg, nchunks, h, act, alpha, H0, P, S, amax)));
+                       Xv, Xe, src, perm, chunk_pos, chunk_seg, nchunks, h, act, alpha, H0, P, S, amax, lo)));
     NT_LAUNCH_CHECK();
   }
   if (chunk_seg == nullptr) ncomb = nseg;  // every segment through pass 2
   launch_combine_r<float, VEC>(reduce, P, chunk_ptr, seg_ptr, chunk_seg ? comb_seg : nullptr, ncomb, h, S,
-                               amax ? amax + 1 : nullptr, stream);
+                               amax ? amax + 1 : nullptr, stream, lo);
   NT_LAUNCH_CHECK();
   return NT_OK;
 }
@@ -775,7 +779,7 @@ extern "C" int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64
                                      const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb,
                                      const int32_t* seg_ptr, int64_t V, int64_t E, int64_t h, int act,
                                      float act_alpha, int reduce, int dtype, float* partial, void* H0, void* S,
-                                     float* amax_out, void* stream_) {
+                                     float* amax_out, int64_t ld_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_init_chunked is fp32 only");
@@ -787,11 +791,14 @@ extern "C" int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64
   NT_REQUIRE(chunk_seg == nullptr || ncomb == 0 || comb_seg != nullptr, NT_EINVAL, "chunk_seg needs comb_seg");
   hipStream_t stream = as_stream(stream_);
   const bool al = aligned16(Xv) && aligned16(Xe) && aligned16(H0) && aligned16(S) && aligned16(partial);
+  if (ld_out == 0) ld_out = h;
+  NT_REQUIRE(ld_out == h || (h % 4 == 0 && ld_out % 4 == 0 && ld_out > h && al), NT_EINVAL,
+             "padded rows need h % 4 == 0, ld_out % 4 == 0 and 16-byte aligned pointers");
   return (h % 4 == 0 && al)
              ? launch_init_chunked<true>((const float*)Xv, (const float*)Xe, src, perm, chunk_pos, nchunks, chunk_ptr,
                                          chunk_seg, comb_seg, ncomb, seg_ptr, V, h, reduce, act, act_alpha, partial,
-                                         (float*)H0, (float*)S, amax_out, stream)
+                                         (float*)H0, (float*)S, amax_out, ld_out, stream)
              : launch_init_chunked<false>((const float*)Xv, (const float*)Xe, src, perm, chunk_pos, nchunks,
                                           chunk_ptr, chunk_seg, comb_seg, ncomb, seg_ptr, V, h, reduce, act,
-                                          act_alpha, partial, (float*)H0, (float*)S, amax_out, stream);
+                                          act_alpha, partial, (float*)H0, (float*)S, amax_out, ld_out, stream);
 }

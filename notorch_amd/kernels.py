@@ -399,10 +399,12 @@ def dmpnn_init_chunked(
     act: tuple[int, float] = (_lib.NT_ACT_IDENTITY, 0.0),
     reduce: str = "sum",
     amax: Tensor | None = None,
+    pitch: int | None = None,
 ) -> tuple[Tensor, Tensor]:
     """(H0, S) = dmpnn_init with layer 0's aggregation over the chunk plan of a hub graph (fp32,
     plan = chunk_plan(seg_ptr)): H0 written once, S combined from per-chunk partials.  amax (2
-    zero-filled device floats, optional) raised to max|H0|, max|S|."""
+    zero-filled device floats, optional) raised to max|H0|, max|S|.  pitch: H0 and S as row-padded
+    views (as dmpnn_init's)."""
     nchunks = plan[1]
     dev = _require_device(Xv, Xe, src, seg_ptr, perm, plan[0], plan[2], amax)
     if Xv.dtype != torch.float32 or Xe.dtype != torch.float32:
@@ -419,12 +421,13 @@ def dmpnn_init_chunked(
     if Xe.shape[1] != h or src.numel() != E or perm.numel() != E or seg_ptr.numel() != V + 1:
         raise ValueError("shape mismatch between Xv, Xe, src and the dst CSR")
     cargs = _chunk_args(plan, V)
-    H0 = torch.empty(E, h, dtype=torch.float32, device=dev)
-    S = torch.empty(V, h, dtype=torch.float32, device=dev)
+    ld = h if pitch is None else int(pitch)
+    H0 = padded_rows(E, h, ld, torch.float32, dev)
+    S = padded_rows(V, h, ld, torch.float32, dev)
     partial = torch.empty(max(nchunks, 1), h, dtype=torch.float32, device=dev)
     _run(dev, _lib.load().nt_dmpnn_init_chunked,
          _ptr(Xv.contiguous()), _ptr(Xe.contiguous()), _ptr(src), _ptr(perm), *cargs, _ptr(seg_ptr), V, E, h, act[0], act[1], reduce_code(reduce), _DTYPE_CODES[torch.float32],
-         _ptr(partial), _ptr(H0), _ptr(S), _ptr(amax), _stream(dev))
+         _ptr(partial), _ptr(H0), _ptr(S), _ptr(amax), 0 if ld == h else ld, _stream(dev))
     return H0, S
 
 
@@ -590,16 +593,21 @@ def mark_hub_rows(row_table: Tensor, dst_ptr: Tensor, hub_degree: int) -> Tensor
 def hub_aggregate(X: Tensor, perm: Tensor, seg_ptr: Tensor, hubs: Tensor, out: Tensor, *, reduce: str = "sum",
                   act: tuple[int, float] = (_lib.NT_ACT_IDENTITY, 0.0), amax: Tensor | None = None) -> Tensor:
     """out[v] = reduce over the in-edges p of v of act(X[perm[p]]) for the nodes v in ``hubs`` (int32),
-    other rows of ``out`` untouched; amax (1 float, may be None) raised to max|out[hubs]|."""
+    other rows of ``out`` untouched; amax (1 float, may be None) raised to max|out[hubs]|.  X and out
+    may be row-padded views of one common pitch."""
     dev = _require_device(X, perm, seg_ptr, hubs, out, amax)
-    _require_f32("X", X)
-    _require_f32("out", out)
+    if X.dtype != torch.float32 or out.dtype != torch.float32:
+        raise TypeError("hub_aggregate is fp32 only")
+    ld = _row_pitch("X", X)
+    if _row_pitch("out", out) != ld:
+        raise ValueError("X and out must share one row pitch")
     if hubs.dtype != torch.int32 or seg_ptr.dtype != torch.int32 or perm.dtype != torch.int32:
         raise TypeError("hubs, seg_ptr and perm must be int32")
     if out.shape[1] != X.shape[1] or out.shape[0] != seg_ptr.numel() - 1:
         raise ValueError("out must be nseg x h")
     _run(dev, _lib.load().nt_dmpnn_hub_aggregate, _ptr(X), _ptr(perm), _ptr(seg_ptr), _ptr(hubs), hubs.numel(),
-         X.shape[1], reduce_code(reduce), act[0], act[1], NT_F32, _ptr(amax), _ptr(out), _stream(dev))
+         X.shape[1], reduce_code(reduce), act[0], act[1], NT_F32, _ptr(amax), _ptr(out),
+         0 if ld == X.shape[1] else ld, _stream(dev))
     return out
 
 

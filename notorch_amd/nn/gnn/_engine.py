@@ -365,15 +365,16 @@ def block_forward(
         return _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states,
                                drop)
     chunks = dst_chunks(lay)
+    pitch = row_pitch(Xv.shape[1], Xv.dtype) if (not keep_states and drop is None) else None
     if chunks is not None and Xv.dtype == torch.float32:
         # hubs: the initial gather inside pass 1 of the chunked reduce (the wave-per-node init would walk
         # a hub's in-edges on one wave), so H0 is written once and not re-read
-        H, S = K.dmpnn_init_chunked(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, chunks, act=act, reduce=reduce, amax=a0)
+        H, S = K.dmpnn_init_chunked(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, chunks, act=act, reduce=reduce, amax=a0,
+                                    pitch=pitch)
     elif chunks is not None:
         H, _ = K.dmpnn_init(Xv, Xe, src, amax=a0)
         S = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, act, chunks, amax=None if a0 is None else a0[1:2])
     else:
-        pitch = row_pitch(Xv.shape[1], Xv.dtype) if (not keep_states and drop is None) else None
         H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce, amax=a0, pitch=pitch)
     return _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states, drop,
                            amax)
@@ -579,7 +580,7 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
         # intermediate layers keep the input's row pitch (row_pitch); the block's outputs are dense
-        pitch = H.shape[1] if (last or hubs is not None) else H.stride(0)
+        pitch = H.shape[1] if last else H.stride(0)
         if spare_H is not None and spare_H.stride(0) != pitch:
             spare_H = spare_S = None
         Hn, Sn = K.dmpnn_update_fused(

@@ -494,13 +494,15 @@ def test_row_padded_init_and_layer_bit_identical(h, pitch, rows):
         assert torch.equal(a, c), name
 
 
-def test_block_forward_row_padding_is_invisible(monkeypatch):
-    """The inference forward runs its intermediate layers on row-padded buffers (h = 300 -> 304):
-    the block's outputs are dense tensors and equal, bit for bit, to the dense-row forward."""
+@pytest.mark.parametrize("kind,n", [("qm9", 300), ("polymer", 2)])
+def test_block_forward_row_padding_is_invisible(monkeypatch, kind, n):
+    """The inference forward runs its intermediate layers on row-padded buffers (h = 300 -> 304; hub
+    graphs too: the chunked init, the hub aggregation): the block's outputs are dense tensors and
+    equal, bit for bit, to the dense-row forward."""
     from notorch_amd.nn import ChempropBlock
     from notorch_amd.nn.gnn import _engine
 
-    G = _graph("qm9", 300, seed=22)
+    G = _graph(kind, n, seed=22)
     h = 300
     torch.manual_seed(5)
     Xv, Xe = torch.randn(G.num_nodes, h), torch.randn(G.num_edges, h)

@@ -192,3 +192,32 @@ def test_fused_chunked_init_matches_init_then_chunked_reduce(reduce):
         assert torch.equal(H0, rH)
         assert torch.equal(S, rS)
         assert am[0].item() == rH.abs().max().item() and am[1].item() == rS.abs().max().item()
+
+
+def test_padded_rows_chunked_init_and_hub_aggregate_bit_identical():
+    """ABI 7 row pitches on the hub-graph path: nt_dmpnn_init_chunked's ld_out and
+    nt_dmpnn_hub_aggregate's ld give the dense-row values bit for bit."""
+    from notorch_amd import kernels as K
+    from notorch_amd.data.synth import make_batch
+
+    G = make_batch("polymer", 2, seed=4).collate("nodes").to(DEV)
+    lay = G._nt_layout
+    V, E, h = G.num_nodes, G.num_edges, 300
+    torch.manual_seed(0)
+    Xv, Xe = torch.randn(V, h, device=DEV), torch.randn(E, h, device=DEV)
+    src = G.edge_index[0].contiguous()
+    chunks = K.chunk_plan(lay.dst_ptr)
+    relu = K.act_code(nn.ReLU())
+    deg = lay.dst_ptr[1:] - lay.dst_ptr[:-1]
+    hubs = torch.nonzero(deg > 32).flatten().to(torch.int32)
+    res = {}
+    for ld in (h, 304):
+        am = torch.zeros(2, device=DEV)
+        H0, S = K.dmpnn_init_chunked(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, chunks, act=relu, amax=am, pitch=ld)
+        assert H0.stride(0) == ld and S.stride(0) == ld
+        out = K.padded_rows(V, h, ld, torch.float32, DEV)
+        out.zero_()
+        K.hub_aggregate(H0, lay.dst_perm, lay.dst_ptr, hubs, out, act=relu)
+        res[ld] = (H0.contiguous(), S.contiguous(), am, out.contiguous())
+    for name, a, b in zip(("H0", "S", "amax", "hub out"), res[h], res[304]):
+        assert torch.equal(a, b), name
