@@ -400,7 +400,7 @@ _ROW_PAD = os.environ.get("NT_ROW_PAD", "1") != "0"  # A/B: 0 = dense intermedia
 # workgroups per CU (overlapping one's epilogue with the other's K loop); larger graphs keep the
 # 128-row walk.  Measured per launch (tools/r4_sweep.sh, tools/r4_nw4b.sh): 78k edges 115-117 vs
 # 125 us; 155k 243 vs 244; 310k 465 vs 462; 456k (polymer-16) 720 vs 691; 621k 904 vs 895.
-NW4_MAX_EDGES = 131072
+NW4_MAX_EDGES = int(os.environ.get("NT_NW4_MAX_EDGES", "131072"))  # A/B override
 
 # per (device, stream, depth): a ring of _AMAX_RING amax buffers for forwards that keep no states,
 # zeroed all at once every _AMAX_RING forwards instead of one fill kernel per forward
