@@ -87,14 +87,16 @@ NT_API int nt_embed_bag(const void* table, int64_t num_types, const int64_t* idx
  *   S[v]  = reduce_{e: dst e = v} act(H0[e])   if S != NULL (then seg_ptr / perm = dst CSR)
  * Bit-identical to nt_embed_bag twice followed by nt_dmpnn_init.
  * amax_out (fp32 only, may be NULL): 2 device floats, atomically raised to max|H0| and max|S| (the
- * caller zero-fills them); the fp32 layer kernel scales its fp16 split by them.
+ * caller zero-fills them); the fp32 layer kernel scales its fp16 split by them.  ld_out (ABI 7): row
+ * pitch in elements of H0 and S (0 = h; > h: fp32 with S, 7 + 2 type columns, as nt_dmpnn_init's).
  */
 NT_API int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_types,
                                const int64_t* node_types, int64_t kv, const void* edge_table,
                                int64_t num_edge_types, const int64_t* edge_types, int64_t ke,
                                const int64_t* src, const int32_t* seg_ptr, const int32_t* perm,
                                int64_t V, int64_t E, int64_t h, int act, float act_alpha, int reduce,
-                               int dtype, void* H0, void* S, float* amax_out, void* stream);
+                               int dtype, void* H0, void* S, float* amax_out, int64_t ld_out,
+                               void* stream);
 
 /*
  * Host-side collate of B per-molecule graphs (BatchedGraph.from_graphs, notorch/data/models/

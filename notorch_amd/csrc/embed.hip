@@ -128,7 +128,7 @@ template <typename T, bool VEC, int R, int ACT, int KV, int KE, bool LDS = false
 __global__ void __launch_bounds__(LDS ? kLdsThreads : 256, LDS ? 2 : 1) init_embed_aggregate_k(
     EmbedArgs a, const int64_t* __restrict__ src, const int32_t* __restrict__ seg_ptr,
     const int32_t* __restrict__ perm, int64_t V, int64_t h, int act, float alpha,
-    T* __restrict__ H0, T* __restrict__ S, float* __restrict__ amax) {
+    T* __restrict__ H0, T* __restrict__ S, float* __restrict__ amax, int64_t lo) {  // lo: H0 / S row pitch
   constexpr int N = Piece<T, VEC>::N;
   constexpr int U = LDS ? 2 : 4;  // LDS rows are cheap: fewer edges in flight, more waves
   float mh = 0.f, ms = 0.f;       // max |H0|, max |S| of this lane (amax != NULL)
@@ -200,7 +200,7 @@ __global__ void __launch_bounds__(LDS ? kLdsThreads : 256, LDS ? 2 : 1) init_emb
         float x[N];
 #pragma unroll
         for (int i = 0; i < N; ++i) x[i] = as_stored<T>(as_stored<T>(xv[i]) + as_stored<T>(xe[i]));
-        Piece<T, VEC>::store(H0 + e[u] * h + c, x);
+        Piece<T, VEC>::store(H0 + e[u] * lo + c, x);
 #pragma unroll
         for (int i = 0; i < N; ++i) {
           mh = fmaxf(mh, fabsf(x[i]));
@@ -214,7 +214,7 @@ __global__ void __launch_bounds__(LDS ? kLdsThreads : 256, LDS ? 2 : 1) init_emb
       y[i] = r[i].result();
       ms = fmaxf(ms, fabsf(y[i]));
     }
-    Piece<T, VEC>::store(S + v * h + c, y);
+    Piece<T, VEC>::store(S + v * lo + c, y);
   }
   if (amax) block_max_to(amax, mh, ms, true);  // one atomic max per block
 }
@@ -237,8 +237,10 @@ __global__ void __launch_bounds__(256) init_embed_only(EmbedArgs a, const int64_
 template <typename T, bool VEC>
 int launch_init_embed(const EmbedArgs& a, const int64_t* src, const int32_t* seg_ptr,
                       const int32_t* perm, int64_t V, int64_t E, int64_t h, int act, float alpha,
-                      int reduce, void* H0, void* S, float* amax, hipStream_t stream) {
+                      int reduce, void* H0, void* S, float* amax, int64_t lo, hipStream_t stream) {
   constexpr int N = Piece<T, VEC>::N;
+  NT_REQUIRE(lo == h || (S != nullptr && a.kv == 7 && a.ke == 2), NT_EUNSUPPORTED,
+             "padded rows: the fused 7 + 2 type-column init only");
   if (S == nullptr) {
     if (E == 0) return NT_OK;
     init_embed_only<T, VEC><<<grid_for(E * (h / N), 256, 256 * 32), 256, 0, stream>>>(
@@ -259,10 +261,10 @@ int launch_init_embed(const EmbedArgs& a, const int64_t* src, const int32_t* seg
   do {                                                                                           \
     if (lds)                                                                                     \
       init_embed_aggregate_k<T, VEC, R_, A_, 7, 2, true><<<grid_lds, kLdsThreads, 0, stream>>>(  \
-          a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S, amax);                         \
+          a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S, amax, lo);                     \
     else if (k72)                                                                                \
       init_embed_aggregate_k<T, VEC, R_, A_, 7, 2><<<grid, 256, 0, stream>>>(                    \
-          a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S, amax);                         \
+          a, src, seg_ptr, perm, V, h, act, alpha, (T*)H0, (T*)S, amax, lo);                     \
     else                                                                                         \
       init_embed_aggregate<T, VEC, R_, A_><<<grid, 256, 0, stream>>>(a, src, seg_ptr, perm, V, h, \
                                                                      act, alpha, (T*)H0, (T*)S);  \
@@ -328,7 +330,7 @@ extern "C" int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_type
                                    const int64_t* src, const int32_t* seg_ptr, const int32_t* perm,
                                    int64_t V, int64_t E, int64_t h, int act, float act_alpha,
                                    int reduce, int dtype, void* H0, void* S, float* amax_out,
-                                   void* stream_) {
+                                   int64_t ld_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
@@ -341,6 +343,9 @@ extern "C" int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_type
   NT_REQUIRE(E == 0 || (node_table && edge_table && src && H0 && (node_types || kv == 0) &&
                         (edge_types || ke == 0)),
              NT_EINVAL, "NULL pointer");
+  if (ld_out == 0) ld_out = h;
+  NT_REQUIRE(ld_out == h || (dtype == NT_F32 && h % 4 == 0 && ld_out % 4 == 0 && ld_out > h), NT_EINVAL,
+             "ld_out != h needs fp32, h % 4 == 0 and ld_out % 4 == 0");
   hipStream_t stream = as_stream(stream_);
   const EmbedArgs a{node_table, num_node_types, node_types, kv,
                     edge_table, num_edge_types, edge_types, ke};
@@ -349,14 +354,14 @@ extern "C" int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_type
   if (dtype == NT_F32) {
     if (h % 4 == 0 && al)
       return launch_init_embed<float, true>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S,
-                                            amax_out, stream);
+                                            amax_out, ld_out, stream);
     return launch_init_embed<float, false>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S,
-                                           amax_out, stream);
+                                           amax_out, ld_out, stream);
   }
   NT_REQUIRE(amax_out == nullptr, NT_EINVAL, "amax_out is fp32 only");
   if (h % 8 == 0 && al)
     return launch_init_embed<bf16_raw, true>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S,
-                                             nullptr, stream);
+                                             nullptr, ld_out, stream);
   return launch_init_embed<bf16_raw, false>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S,
-                                            nullptr, stream);
+                                            nullptr, ld_out, stream);
 }

@@ -976,6 +976,7 @@ def dmpnn_init_embed(
     reduce: str = "sum",
     validate: bool = True,
     amax: Tensor | None = None,
+    pitch: int | None = None,
 ) -> tuple[Tensor, Tensor | None]:
     """H0 = Xv[src] + Xe with Xv = EmbeddingBag(node_table)(node_types), Xe likewise, never
     materialised; optionally fused with S = scatter(act(H0), dst) (needs the dst CSR).
@@ -995,12 +996,14 @@ def dmpnn_init_embed(
     h = node_table.shape[1]
     if src.numel() != E:
         raise ValueError("src must have one entry per edge")
-    H0 = torch.empty(E, h, dtype=node_table.dtype, device=dev)
-    S = None if seg_ptr is None else torch.empty(V, h, dtype=node_table.dtype, device=dev)
+    ld = h if pitch is None else int(pitch)  # row-padded H0 / S views (as dmpnn_init's pitch)
+    H0 = padded_rows(E, h, ld, node_table.dtype, dev)
+    S = None if seg_ptr is None else padded_rows(V, h, ld, node_table.dtype, dev)
     _run(dev, _lib.load().nt_dmpnn_init_embed,
          _ptr(node_table), node_table.shape[0], _ptr(node_types), kv, _ptr(edge_table),
          edge_table.shape[0], _ptr(edge_types), ke, _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h,
-         act[0], act[1], reduce_code(reduce), code, _ptr(H0), _ptr(S), _ptr(amax), _stream(dev))
+         act[0], act[1], reduce_code(reduce), code, _ptr(H0), _ptr(S), _ptr(amax), 0 if ld == h else ld,
+         _stream(dev))
     return H0, S
 
 

@@ -465,9 +465,11 @@ def block_forward_embedded(
         node, H, _ = _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, False)
         return node, H
     amax = _amax_buffer(len(weights), node_table, reuse=True)
+    k72 = node_types.dim() == 2 and node_types.shape[1] == 7 and edge_types.dim() == 2 and edge_types.shape[1] == 2
+    pitch = row_pitch(node_table.shape[1], node_table.dtype) if k72 else None
     H, S = K.dmpnn_init_embed(node_table, node_types, edge_table, edge_types, src, lay.dst_ptr,
                               lay.dst_perm, act=act, reduce=reduce, validate=validate,
-                              amax=None if amax is None else amax[0])
+                              amax=None if amax is None else amax[0], pitch=pitch)
     node, H, _ = _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, False,
                                  amax=amax)
     return node, H

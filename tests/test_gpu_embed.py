@@ -73,6 +73,26 @@ def test_init_embed_bit_identical_to_unfused(dtype, h, n):
         assert torch.equal(H0, H0_ref) and torch.equal(S, S_ref), reduce
 
 
+@pytest.mark.parametrize("h", [300, 132])
+def test_init_embed_padded_rows_bit_identical(h):
+    """ABI 7 ld_out of nt_dmpnn_init_embed: H0 and S on padded rows hold the dense values bit for
+    bit (LDS-staged tables at both sizes), the amax chain too."""
+    from notorch_amd import kernels as K
+
+    G = _graph("qm9", 400, seed=5)
+    torch.manual_seed(2)
+    Tv, Te = torch.randn(42, h, device=DEV), torch.randn(13, h, device=DEV)
+    nt, et = G.node_feats.to(DEV), G.edge_feats.to(DEV)
+    src, dst = G.edge_index[0].to(DEV), G.edge_index[1].to(DEV)
+    seg_ptr, perm = K.csr_build(dst, G.num_nodes)
+    am0, am1 = torch.zeros(2, device=DEV), torch.zeros(2, device=DEV)
+    H0, S = K.dmpnn_init_embed(Tv, nt, Te, et, src, seg_ptr, perm, amax=am0)
+    pitch = (h + 7) // 8 * 8 + 8
+    H0p, Sp = K.dmpnn_init_embed(Tv, nt, Te, et, src, seg_ptr, perm, amax=am1, pitch=pitch)
+    assert H0p.stride(0) == pitch and Sp.stride(0) == pitch
+    assert torch.equal(H0p, H0) and torch.equal(Sp, S) and torch.equal(am0, am1)
+
+
 def _modules(h, depth, dtype=torch.float32, **opts):
     from notorch_amd.nn import ChempropBlock, EmbeddedChempropBlock, GraphEmbedding
 
