@@ -76,6 +76,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=50)
     p.add_argument("--warmup", type=int, default=10)
+    p.add_argument("--prewarm-s", type=float, default=1.0,
+                   help="untimed steps for at least this long before the W warm-up steps: the GPU "
+                        "reaches its sustained clock only after ~1 s of load (measured: the layer "
+                        "kernel runs 115 us right after a cold start, 106-109 us at steady state)")
     p.add_argument("--workload", default="qm9-4096", choices=sorted(WORKLOADS))
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="CPU baseline budget per thread count")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -169,6 +173,19 @@ def make_jobs(name, rank, world, dev, embedding):
     G = batch.collate("nodes")
     jobs.append(Job(batch, G, embed_on_device(embedding, G, dev), h, depth, bf16))
     return jobs, batch, None
+
+
+def prewarm(step, seconds, dev):
+    """Untimed steps until `seconds` of wall time have passed (synchronised in rounds of 8 steps):
+    the clock-settling phase before the counted warm-up steps; returns the steps it ran."""
+    n = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(8):
+            step()
+        n += 8
+        torch.cuda.synchronize(dev)
+    return n
 
 
 def timed_steps(step, steps, warmup, env, dev):
@@ -380,18 +397,21 @@ def run_workload(name, args, env, dev, headline):
     torch.cuda.synchronize(dev)
 
     events = []
-    every = max(1, args.event_every)
+    # at least two sampled steps, at most one in `event_every`, none at the region's edges
+    every = max(1, args.event_every, args.steps // 2)
+    offset = max(0, min(every // 2, args.steps - 1))
     count = [0]
 
     def step():
-        # the per-launch roofline events ride on every `every`-th step (the first of the timed region
-        # included); the others run exactly as a user's forward does
-        _engine.UPDATE_EVENTS = events if count[0] % every == 0 else None
+        # the per-launch roofline events ride on the steps i = offset mod every of the timed region;
+        # the others run exactly as a user's forward does
+        _engine.UPDATE_EVENTS = events if count[0] % every == offset else None
         count[0] += 1
         for j in jobs:
             readout(block(j.Gd))
 
     with torch.no_grad():
+        prewarm(step, args.prewarm_s, dev)
         for _ in range(args.warmup):
             step()
     events.clear()
@@ -402,7 +422,7 @@ def run_workload(name, args, env, dev, headline):
     E_rank = sum(j.E for j in jobs)
     units, secs, rate = aggregate_throughput(E_rank * depth * args.steps, elapsed, device=BOOK_DEV)
     res = {"jobs": jobs, "embedding": embedding, "block": block, "readout": readout, "events": events,
-           "event_every": every,
+           "event_every": every, "event_offset": offset,
            "info": info, "units": units, "secs": secs, "rate": rate, "batch": batch, "ranges": ranges,
            "name": name, "kind": kind, "h": h, "depth": depth, "bf16": bf16, "n_mols": n_mols,
            "steps": args.steps}
@@ -572,8 +592,9 @@ def summary(res, args, env, pmc_csv=None):
     else:
         traffic, tsrc = committed_traffic(res["name"], kern)
     roof = launch_roofline(jobs, res["events"], info, traffic, tsrc)
-    roof["launch_sampling"] = (f"HIP events on the launch stream around every layer launch of every "
-                               f"{res['event_every']}-th step of the timed region ({len(res['events'])} launches)")
+    roof["launch_sampling"] = (f"HIP events on the launch stream around every layer launch of the steps "
+                               f"i = {res['event_offset']} mod {res['event_every']} of the timed region "
+                               f"({len(res['events'])} launches)")
     t_step = res["secs"] / args.steps
     V = sum(j.V for j in jobs)
     E = sum(j.E for j in jobs)
@@ -675,6 +696,7 @@ def main():
             "n_gpus": env.world_size,
             "steps": args.steps,
             "warmup": args.warmup,
+            "prewarm_s": args.prewarm_s,
             "ms_per_step": res["secs"] / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong" if sharded else "weak",
