@@ -483,6 +483,11 @@ __device__ __forceinline__ float absmax_n(float m, const float (&y)[N]) {
   return m;
 }
 
+#ifndef NT_SEG_PU
+#define NT_SEG_PU 8
+#endif
+constexpr int kSegPU = NT_SEG_PU;  // rows in flight per lane in seg_chunk_partial (a chunk: <= 32 rows)
+
 template <typename T, bool VEC, int R, int ACT>
 __global__ void __launch_bounds__(256) seg_chunk_partial(const T* __restrict__ X,
                                                          const int32_t* __restrict__ perm,
@@ -503,15 +508,15 @@ __global__ void __launch_bounds__(256) seg_chunk_partial(const T* __restrict__ X
     Reducer<RR> r[N];
 #pragma unroll
     for (int i = 0; i < N; ++i) r[i].init();
-    for (int32_t j = b; j < e; j += 4) {
-      float x[4][N];
-      int64_t row[4];
+    for (int32_t j = b; j < e; j += kSegPU) {
+      float x[kSegPU][N];
+      int64_t row[kSegPU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) row[u] = j + u < e ? (perm ? perm[j + u] : j + u) : (perm ? perm[b] : b);
+      for (int u = 0; u < kSegPU; ++u) row[u] = j + u < e ? (perm ? perm[j + u] : j + u) : (perm ? perm[b] : b);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) Piece<T, VEC>::load(X + row[u] * h + c, x[u]);
+      for (int u = 0; u < kSegPU; ++u) Piece<T, VEC>::load(X + row[u] * h + c, x[u]);
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
+      for (int u = 0; u < kSegPU; ++u) {
         if (j + u >= e) break;
 #pragma unroll
         for (int i = 0; i < N; ++i) r[i].push(act_t<ACT>(x[u][i], act, alpha));
@@ -600,12 +605,14 @@ __global__ void __launch_bounds__(256) init_chunk_partial(const float* __restric
   if (amax) block_max_to(amax, m, ms, true);
 }
 
-// Pass 2: one block per (listed segment, 32-piece slab); the segment's chunks split into 8
-// consecutive sub-ranges (one per 32-thread group), each summed in chunk order, then the 8 group
-// results combined in order by group 0 (empty segment -> 0 for every reduction).
-constexpr int kCombG = 8;
-template <typename T, bool VEC, int R>
-__global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict__ P,
+// Pass 2: one block per (listed segment, 32-piece slab); the segment's chunks split into 32
+// consecutive sub-ranges, each summed in chunk order (4 per 32-thread group in 256-thread blocks, 1
+// in the 1024-thread blocks launched when the listed segments are few), then the sub-range results
+// combined in order by group 0 (empty segment -> 0 for every reduction); the same bits at either
+// block size.
+constexpr int kCombSub = 32;  // a segment's chunks in 32 consecutive sub-ranges, whatever the block size
+template <typename T, bool VEC, int R, int kCombG>
+__global__ void __launch_bounds__(32 * kCombG) seg_chunk_combine(const float* __restrict__ P,
                                                          const int32_t* __restrict__ chunk_ptr,
                                                          const int32_t* __restrict__ seg_ptr,
                                                          const int32_t* __restrict__ comb_seg,
@@ -613,7 +620,8 @@ __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict
                                                          T* __restrict__ out, float* __restrict__ amax,
                                                          int64_t lo) {  // lo: row pitch of out
   constexpr int N = Piece<T, VEC>::N;
-  __shared__ float red[kCombG][32][N];
+  constexpr int SPG = kCombSub / kCombG;  // sub-ranges per 32-thread group
+  __shared__ float red[kCombSub][32][N];
   const int64_t hw = h / N, nslab = (hw + 31) / 32;
   const int g = threadIdx.x >> 5, cl = threadIdx.x & 31;
   float m = 0.f;
@@ -623,40 +631,43 @@ __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict
     const int32_t b = chunk_ptr[sg], n = chunk_ptr[sg + 1] - b;
     const bool ok = pc < hw;
     const int64_t c = (ok ? pc : 0) * N;
-    const int32_t kb = b + (int32_t)((int64_t)n * g / kCombG), ke = b + (int32_t)((int64_t)n * (g + 1) / kCombG);
-    float y[N];
+    for (int sr = g * SPG; sr < (g + 1) * SPG; ++sr) {
+      const int32_t kb = b + (int32_t)((int64_t)n * sr / kCombSub), ke = b + (int32_t)((int64_t)n * (sr + 1) / kCombSub);
+      float y[N];
 #pragma unroll
-    for (int q = 0; q < N; ++q) y[q] = 0.f;
-    for (int32_t k = kb; k < ke; k += 4) {
-      float p[4][N];
+      for (int q = 0; q < N; ++q) y[q] = 0.f;
+      for (int32_t k = kb; k < ke; k += 4) {
+        float p[4][N];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int64_t kk = k + u < ke ? k + u : kb;
+        for (int u = 0; u < 4; ++u) {
+          const int64_t kk = k + u < ke ? k + u : kb;
 #pragma unroll
-        for (int q = 0; q < N; ++q) p[u][q] = P[kk * h + c + q];
-      }
+          for (int q = 0; q < N; ++q) p[u][q] = P[kk * h + c + q];
+        }
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (k + u >= ke) break;
+        for (int u = 0; u < 4; ++u) {
+          if (k + u >= ke) break;
 #pragma unroll
-        for (int q = 0; q < N; ++q) {
-          if constexpr (R == NT_MAX) y[q] = k + u == kb ? p[u][q] : fmaxf(y[q], p[u][q]);
-          else if constexpr (R == NT_MIN) y[q] = k + u == kb ? p[u][q] : fminf(y[q], p[u][q]);
-          else y[q] += p[u][q];
+          for (int q = 0; q < N; ++q) {
+            if constexpr (R == NT_MAX) y[q] = k + u == kb ? p[u][q] : fmaxf(y[q], p[u][q]);
+            else if constexpr (R == NT_MIN) y[q] = k + u == kb ? p[u][q] : fminf(y[q], p[u][q]);
+            else y[q] += p[u][q];
+          }
         }
       }
-    }
 #pragma unroll
-    for (int q = 0; q < N; ++q) red[g][cl][q] = y[q];
+      for (int q = 0; q < N; ++q) red[sr][cl][q] = y[q];
+    }
     __syncthreads();
     if (g == 0 && ok) {
+      float y[N];
       bool first = true;
-      for (int gg = 0; gg < kCombG; ++gg) {
-        const int32_t gb = (int32_t)((int64_t)n * gg / kCombG), ge = (int32_t)((int64_t)n * (gg + 1) / kCombG);
+      for (int sr = 0; sr < kCombSub; ++sr) {
+        const int32_t gb = (int32_t)((int64_t)n * sr / kCombSub), ge = (int32_t)((int64_t)n * (sr + 1) / kCombSub);
         if (gb == ge) continue;  // an empty sub-range
 #pragma unroll
         for (int q = 0; q < N; ++q) {
-          const float v = red[gg][cl][q];
+          const float v = red[sr][cl][q];
           if constexpr (R == NT_MAX) y[q] = first ? v : fmaxf(y[q], v);
           else if constexpr (R == NT_MIN) y[q] = first ? v : fminf(y[q], v);
           else y[q] = first ? v : y[q] + v;
@@ -676,6 +687,9 @@ __global__ void __launch_bounds__(256) seg_chunk_combine(const float* __restrict
   if (amax) block_max_to(amax, m);  // fp32 callers: max|out| (the fp32 layer kernel's split scale)
 }
 
+#ifndef NT_COMB_WIDE
+#define NT_COMB_WIDE 1
+#endif
 template <typename T, bool VEC, int R>
 void launch_combine(const float* P, const int32_t* chunk_ptr, const int32_t* seg_ptr, const int32_t* comb_seg,
                     int64_t ncomb, int64_t h, T* out, float* amax, hipStream_t stream, int64_t lo = 0) {
@@ -683,8 +697,13 @@ void launch_combine(const float* P, const int32_t* chunk_ptr, const int32_t* seg
   const int64_t blocks = ncomb * ((h / N + 31) / 32);
   if (blocks == 0) return;
   const int g = (int)(blocks < 256 * 16 ? blocks : 256 * 16);
-  seg_chunk_combine<T, VEC, R><<<g, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax,
-                                                       lo ? lo : h);
+  if (NT_COMB_WIDE && blocks < 1024) {  // few long segments (a readout over polymers): 32 sub-ranges
+    seg_chunk_combine<T, VEC, R, 32><<<g, 1024, 0, stream>>>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax,
+                                                            lo ? lo : h);
+    return;
+  }
+  seg_chunk_combine<T, VEC, R, 8><<<g, 256, 0, stream>>>(P, chunk_ptr, seg_ptr, comb_seg, ncomb, h, out, amax,
+                                                         lo ? lo : h);
 }
 
 template <typename T, bool VEC>
