@@ -305,6 +305,20 @@ NT_API int nt_dmpnn_mark_hub_rows(void* row_table, int64_t E, const int32_t* dst
  * (16 contiguous row ranges per hub, combined in order).  ld (ABI 7): row pitch in elements of X and
  * out (0 = h; >= h, a multiple of 4).
  */
+/*
+ * The fused layer's hub partials combined (ABI 7): with S_part given to nt_dmpnn_update_fused and a
+ * row table whose hub rows are sub-runs (entries -((slot << 2) | start | end << 1) - 1: runs of one
+ * hub's consecutive in-edges within a tile, at most max_in_degree rows each), the layer stores each
+ * sub-run's reduce of agg_act(H_out) as partial row `slot` (fp32, h wide, dense); then for v in hubs
+ *   out[v] = reduce_{k in [slot_ptr[v], slot_ptr[v+1])} partial[k]   (mean: / in-degree from seg_ptr)
+ * slot_ptr (int32[V+1]): slots before node v's rows.  Combined as nt_segment_reduce_chunked's pass 2
+ * (32 consecutive sub-ranges in order; deterministic).  amax_out (may be NULL): one device float
+ * raised to max|out[hubs]|.  fp32, h % 4 == 0; ld = row pitch in elements of out (0 = h).
+ */
+NT_API int nt_dmpnn_hub_combine(const void* partial, const int32_t* hubs, const int32_t* slot_ptr, int64_t nhub,
+                                const int32_t* seg_ptr, int64_t V, int64_t h, int reduce, int dtype,
+                                float* amax_out, void* out, int64_t ld, void* stream);
+
 NT_API int nt_dmpnn_hub_aggregate(const void* X, const int32_t* perm, const int32_t* seg_ptr,
                                   const int32_t* hubs, int64_t nhub, int64_t h, int reduce, int act,
                                   float act_alpha, int dtype, float* amax_out, void* out, int64_t ld,
@@ -334,6 +348,8 @@ NT_API int nt_dmpnn_fused_tile_rows(int64_t h, int dtype, int act, int reduce, i
  * amax_out (may be NULL) = 2 zero-filled device floats raised to max|H_out|, max|S_out|.
  * bf16 (h % 8 == 0, h <= 512): bf16 MFMA, tile_rows <= 64, amax ignored.
  * 16-byte aligned feature pointers; S_out must not alias S.
+ * S_part (ABI 7, fp32, may be NULL): the hub partial rows (nt_dmpnn_hub_combine) when the row table
+ * marks hub sub-runs.
  * ld_in / ld_out (ABI 7): row pitch in elements of H and S / of H_out and S_out (0 = h; fp32: >= h and
  * a multiple of 4, bf16: h).  Rows padded to a 32-byte multiple (h = 300 -> 304) keep every row's
  * pieces on whole 32-B sectors: the intermediate layers of a forward run on padded rows.
@@ -344,7 +360,7 @@ NT_API int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t* sr
                                  int64_t ntiles, int tile_rows, int max_in_degree, const int32_t* perm,
                                  const int32_t* dst_sorted, const void* row_table, int reduce,
                                  int agg_act, float agg_alpha, int dtype, const float* amax_in,
-                                 float* amax_out, void* H_out, void* S_out, int64_t ld_in,
+                                 float* amax_out, void* H_out, void* S_out, void* S_part, int64_t ld_in,
                                  int64_t ld_out, void* stream);
 
 /*

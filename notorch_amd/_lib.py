@@ -106,8 +106,11 @@ SIGNATURES: dict[str, tuple] = {
     "nt_dmpnn_update_fused": (
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_int, _c_f32, _vp, _c_i64,
-         _c_int, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp, _vp, _c_i64, _c_i64,
-         _vp],
+         _c_int, _c_int, _vp, _vp, _vp, _c_int, _c_int, _c_f32, _c_int, _vp, _vp, _vp, _vp, _vp, _c_i64,
+         _c_i64, _vp],
+    ),
+    "nt_dmpnn_hub_combine": (
+        _c_int, [_vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i64, _c_int, _c_int, _vp, _vp, _c_i64, _vp],
     ),
     "nt_dmpnn_row_table": (_c_int, [_vp, _vp, _vp, _vp, _c_i64, _c_i64, _vp, _vp]),
     "nt_node_scores": (

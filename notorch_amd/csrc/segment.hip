@@ -821,3 +821,24 @@ extern "C" int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64
                                           chunk_ptr, chunk_seg, comb_seg, ncomb, seg_ptr, V, h, reduce, act,
                                           act_alpha, partial, (float*)H0, (float*)S, amax_out, ld_out, stream);
 }
+
+// The fused layer's hub sub-run partials combined per hub (nt_dmpnn_hub_combine): pass 2 of the
+// chunked reduce with the hubs' slot ranges as the chunk CSR (slot_ptr[v] = slots before node v).
+extern "C" int nt_dmpnn_hub_combine(const void* partial, const int32_t* hubs, const int32_t* slot_ptr, int64_t nhub,
+                                    const int32_t* seg_ptr, int64_t V, int64_t h, int reduce, int dtype,
+                                    float* amax_out, void* out, int64_t ld, void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_hub_combine: fp32 only");
+  NT_REQUIRE(valid_reduce(reduce), NT_EINVAL, "bad reduce code");
+  NT_REQUIRE(nhub >= 0 && nhub <= V && h > 0 && h % 4 == 0, NT_EINVAL, "bad sizes (h % 4 == 0)");
+  if (ld == 0) ld = h;
+  NT_REQUIRE(ld >= h && ld % 4 == 0, NT_EINVAL, "row pitch must be >= h and a multiple of 4");
+  if (nhub == 0) return NT_OK;
+  NT_REQUIRE(partial && hubs && slot_ptr && seg_ptr && out, NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(aligned16(partial) && aligned16(out), NT_EINVAL, "feature pointers must be 16-byte aligned");
+  launch_combine_r<float, true>(reduce, (const float*)partial, slot_ptr, seg_ptr, hubs, nhub, h, (float*)out, amax_out,
+                                as_stream(stream_), ld);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}

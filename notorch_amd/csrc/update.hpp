@@ -23,6 +23,7 @@ struct UpdateArgs {
   // row pitches in elements (0: dense rows of h): H and S inputs, H_out and S_out outputs (fp32 fused
   // layer kernel only)
   int64_t ldi = 0, ldo = 0;
+  float* S_part = nullptr;  // fused fp32: hub partial rows (row table entries < 0), see nt_dmpnn_update_fused
 };
 
 // bf16x6 fp32-emulation kernel (update_x6.hip): h % 4 == 0 and 97 <= h <= 512.

@@ -740,13 +740,13 @@ extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t
                                      int max_in_degree, const int32_t* perm,
                                      const int32_t* dst_sorted, const void* row_table, int reduce,
                                      int agg_act, float agg_alpha, int dtype, const float* amax_in,
-                                     float* amax_out, void* H_out, void* S_out, int64_t ld_in, int64_t ld_out,
-                                     void* stream_) {
+                                     float* amax_out, void* H_out, void* S_out, void* S_part, int64_t ld_in,
+                                     int64_t ld_out, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(ld_in >= 0 && ld_out >= 0, NT_EINVAL, "bad row pitch");
-  NT_REQUIRE(dtype == NT_F32 || ((ld_in == 0 || ld_in == h) && (ld_out == 0 || ld_out == h)), NT_EUNSUPPORTED,
-             "row pitches other than h are fp32 only");
+  NT_REQUIRE(dtype == NT_F32 || ((ld_in == 0 || ld_in == h) && (ld_out == 0 || ld_out == h) && S_part == nullptr),
+             NT_EUNSUPPORTED, "row pitches other than h and hub partials are fp32 only");
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(act >= NT_ACT_IDENTITY && act <= NT_ACT_SIGMOID, NT_EINVAL, "bad act code");
   NT_REQUIRE(agg_act >= NT_ACT_IDENTITY && agg_act <= NT_ACT_SIGMOID, NT_EINVAL, "bad agg_act code");
@@ -778,8 +778,10 @@ extern "C" int nt_dmpnn_update_fused(const void* H, const void* S, const int64_t
                                     H_out, S_out, as_stream(stream_));
   }
   UpdateArgs a{(const float*)H, (const float*)S, src, rev, Wp, (const float*)b, V, E, h,
-               0, 0, residual, act, act_alpha, (float*)H_out, as_stream(stream_), ld_in, ld_out};
+               0, 0, residual, act, act_alpha, (float*)H_out, as_stream(stream_), ld_in, ld_out, (float*)S_part};
   NT_REQUIRE(row_table == nullptr || aligned16(row_table), NT_EINVAL, "row_table must be 16-byte aligned");
+  NT_REQUIRE(S_part == nullptr || (tile_ptr != nullptr && aligned16(S_part)), NT_EINVAL,
+             "S_part needs a tile plan and 16-byte alignment");
   return launch_update_fk(a, (const char*)Wp + fk_offset(h), amax_in, amax_out, tile_ptr, ntiles,
                           tile_rows, max_in_degree, row_table, reduce, agg_act, agg_alpha, (float*)S_out);
 }

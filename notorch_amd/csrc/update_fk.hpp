@@ -108,7 +108,9 @@ constexpr int kThreads = 512;
 constexpr int kWaves = 8;
 constexpr int kImgHdr = 256;  // image header bytes (float s_W at 0, max|W| partials at 1..32); fragments follow
 constexpr int kEmaps = 4;     // row-info buffers (tile index mod 4)
-constexpr int kFlagStart = 1, kFlagEnd = 2;
+// row flags: first / last row of a segment; kFlagPart: a hub sub-run whose sum goes to the partial rows
+// a.SP (row-table entries of hub rows are negative: -((slot << 2) | start | end << 1) - 1)
+constexpr int kFlagStart = 1, kFlagEnd = 2, kFlagPart = 4;
 
 __host__ __device__ constexpr int ks_for(int64_t h) { return (int)((h + 31) / 32); }
 __host__ __device__ constexpr int nt_for(int64_t h) { return (int)((h + 15) / 16); }
@@ -141,6 +143,7 @@ struct Args {
   float aalpha;
   float* O;
   float* SO;  // NULL: no aggregation
+  float* SP = nullptr;  // hub partial rows (slots x h fp32), written at the end rows of kFlagPart sub-runs
   int nxcd;
   int stagger;  // diagnostic: start delay of workgroup b = stagger * ((b / nxcd) % 4) x 8k cycles (0)
   int rtabl;    // FK_RTABL builds only (timing ablations, results invalid): 1 gathers read row 0, 2 W reads
@@ -244,7 +247,10 @@ __device__ __forceinline__ int2 row_offsets(const Args& a, int4 raw, bool valid)
 
 // emap entry {edge (-1 past the tile), node, flags, 0}
 __device__ __forceinline__ int4 row_entry(int4 raw, bool valid) {
-  return valid ? int4{raw.x, raw.w >> 2, raw.w & 3, 0} : int4{-1, -1, kFlagStart | kFlagEnd, 0};
+  if (!valid) return int4{-1, -1, kFlagStart | kFlagEnd, 0};
+  if (raw.w >= 0) return int4{raw.x, raw.w >> 2, raw.w & 3, 0};
+  const int wv = -raw.w - 1;  // a hub sub-run row: {edge, partial slot, flags | kFlagPart}
+  return int4{raw.x, wv >> 2, (wv & 3) | kFlagPart, 0};
 }
 
 // --------------------------------------------------------------------------- kernel
@@ -671,7 +677,9 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC, NW>& st, cons
           cnt = start ? 1.f : yc + 1.f;
         }
       }
-      if ((ri.z & kFlagEnd) && rok && (ABL & 128) == 0) {
+      if ((ri.z & kFlagPart) && (ri.z & kFlagEnd) && rok) {  // a hub sub-run: its raw partial
+        if constexpr (PREC == 0) reinterpret_cast<f32x4*>(a.SP)[(int64_t)ri.y * st.hc + pc] = x;
+      } else if ((ri.z & kFlagEnd) && rok && (ABL & 128) == 0) {
         f32x4 r = x;
         if (!SUMONLY && a.reduce == NT_MEAN) r = x / cnt;
         if constexpr (PREC == 1) {
@@ -845,7 +853,7 @@ __device__ __forceinline__ void fk_epi3_group(State<RT, CT, GD, PREC, NW>& st, c
         const int ns = st.nlist[kNlistN];
         for (int k = rg; k < ns; k += 16) {
           const int r0 = st.nlist[k], r1 = st.nlist[k + 1];
-          if (pok && (em[r1 - 1].z & kFlagEnd)) {  // hub rows (no end flag) are left to the hub kernel
+          if (pok && (em[r1 - 1].z & (kFlagEnd | kFlagPart)) == kFlagEnd) {  // (no hub partials here)
             f32x4 x = *reinterpret_cast<const f32x4*>(st.stage + r0 * kSP + 4 * p);
             for (int r = r0 + 1; r < r1; ++r) {
               const f32x4 y = *reinterpret_cast<const f32x4*>(st.stage + r * kSP + 4 * p);
@@ -941,7 +949,7 @@ __device__ __forceinline__ void fk_epi4_col(State<RT, CT, GD, PREC, NW>& st, con
       f32x4 x = *reinterpret_cast<const f32x4*>(st.stage + r0 * kSP4 + 4 * p4);
       for (int r = r0 + 1; r < r1; ++r) x = x + *reinterpret_cast<const f32x4*>(st.stage + r * kSP4 + 4 * p4);
       const int4 re = em[r1 - 1];  // the node's last row: its id and end flag (hub rows carry none)
-      if ((re.z & kFlagEnd) && re.x >= 0 && pcn < hc) {
+      if ((re.z & (kFlagEnd | kFlagPart)) == kFlagEnd && re.x >= 0 && pcn < hc) {  // (no hub partials here)
         reinterpret_cast<f32x4*>(a.SO)[(int64_t)re.y * st.lo + pcn] = x;
         st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
       }

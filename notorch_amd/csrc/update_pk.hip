@@ -1018,8 +1018,9 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
     a.ldiv = a.ldic = (int)(ldi / 4);
     a.ldoc = (int)(ldo / 4);
 #ifdef NT_DIAG
-    NT_REQUIRE((ldi == u.h && ldo == u.h) || !(fk2_selected(u.h) || fw_active(u.h, NT_F32, u.act, reduce, aact)),
-               NT_EUNSUPPORTED, "diagnostic walks take dense rows only");
+    NT_REQUIRE((ldi == u.h && ldo == u.h && u.S_part == nullptr) ||
+                   !(fk2_selected(u.h) || fw_active(u.h, NT_F32, u.act, reduce, aact)),
+               NT_EUNSUPPORTED, "diagnostic walks take dense rows and no hub partials only");
 #endif
   }
   // an even number of k-steps, at least four, per tile (update_fk_kernel runs two steps per inner
@@ -1037,6 +1038,7 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   a.aalpha = aalpha;
   a.O = u.H_out;
   a.SO = S_out;
+  a.SP = u.S_part;
   a.nxcd = xcd_count();
   {
     // timing experiments only, read once per process: NT_FK_STAGGER (start delay of half the grid),

@@ -578,6 +578,61 @@ def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int, rows: int = 64,
     return tile_ptr, ntiles, dsts
 
 
+def hub_runs(row_table: Tensor, dst_ptr: Tensor, dst_sorted: Tensor, tile_ptr: Tensor, hub_degree: int,
+             run_rows: int) -> tuple[Tensor, int, Tensor, Tensor]:
+    """A row table whose hub rows (nodes with more than hub_degree in-edges) are sub-runs for the fused
+    layer's hub partials: runs of one hub's consecutive positions within a tile (tile_ptr), cut every
+    run_rows rows (<= the launch's max_in_degree, so the kernel's segmented scan covers them), entry
+    w = -((slot << 2) | start | end << 1) - 1.  Returns (table, nslots, hubs, slot_ptr) for
+    dmpnn_update_fused(S_part=...) and hub_combine.  Device ops; one sync (the slot count)."""
+    dev = _require_device(row_table, dst_ptr, dst_sorted, tile_ptr)
+    E, V = row_table.shape[0], dst_ptr.numel() - 1
+    run_rows = max(1, int(run_rows))
+    dp = dst_ptr.long()
+    deg = dp[1:] - dp[:-1]
+    is_hub = deg > hub_degree
+    d = dst_sorted.long()
+    pos = torch.arange(E, device=dev)
+    hub_row = is_hub[d]
+    ts = torch.zeros(E + 1, dtype=torch.bool, device=dev)
+    ts[tile_ptr.long()] = True
+    run_start = hub_row & ((pos == dp[d]) | ts[:E])
+    run_end = hub_row & ((pos + 1 == dp[d + 1]) | ts[1:])
+    # offset of each row in its run (the run's start position by a running max), cut every run_rows
+    rs = torch.cummax(torch.where(run_start, pos, torch.zeros_like(pos)), 0).values
+    off = pos - rs
+    sub_start = hub_row & (off % run_rows == 0)
+    sub_end = hub_row & ((off % run_rows == run_rows - 1) | run_end)
+    slot = torch.cumsum(sub_start.long(), 0) - 1
+    hubs = torch.nonzero(is_hub).flatten()
+    nslots = int(sub_start.sum()) if E else 0
+    w = -(((slot << 2) | sub_start.long() | (sub_end.long() << 1))) - 1
+    out = row_table.clone()
+    out[:, 3] = torch.where(hub_row, w, row_table[:, 3].long()).to(torch.int32)
+    # slot_ptr[v] = sub-runs starting before node v's first position (the hubs' slot CSR)
+    before = torch.zeros(E + 1, dtype=torch.long, device=dev)
+    torch.cumsum(sub_start.long(), 0, out=before[1:])
+    slot_ptr = before[dp].to(torch.int32)
+    return out, nslots, hubs.to(torch.int32), slot_ptr
+
+
+def hub_combine(partial: Tensor, hubs: Tensor, slot_ptr: Tensor, seg_ptr: Tensor, out: Tensor, *,
+                reduce: str = "sum", amax: Tensor | None = None) -> Tensor:
+    """out[v] = reduce over the partial rows [slot_ptr[v], slot_ptr[v + 1]) for v in hubs
+    (nt_dmpnn_hub_combine); out may be a row-padded view."""
+    dev = _require_device(partial, hubs, slot_ptr, seg_ptr, out, amax)
+    if partial.dtype != torch.float32 or out.dtype != torch.float32 or not partial.is_contiguous():
+        raise TypeError("hub_combine: contiguous fp32 partial rows, fp32 out")
+    V = seg_ptr.numel() - 1
+    if slot_ptr.numel() != V + 1 or out.shape[0] != V:
+        raise ValueError("slot_ptr must have V + 1 entries and out V rows")
+    ld = _row_pitch("out", out)
+    h = out.shape[1]
+    _run(dev, _lib.load().nt_dmpnn_hub_combine, _ptr(partial), _ptr(hubs), _ptr(slot_ptr), hubs.numel(),
+         _ptr(seg_ptr), V, h, reduce_code(reduce), NT_F32, _ptr(amax), _ptr(out), 0 if ld == h else ld, _stream(dev))
+    return out
+
+
 def mark_hub_rows(row_table: Tensor, dst_ptr: Tensor, hub_degree: int) -> Tensor:
     """In place: the row-table entries of nodes with more than hub_degree in-edges lose their
     "last in-edge" flag (nt_dmpnn_mark_hub_rows), so the fused layer leaves their S_out rows to
@@ -634,6 +689,7 @@ def dmpnn_update_fused(
     out: Tensor | None = None,
     S_out: Tensor | None = None,
     pitch_out: int | None = None,
+    S_part: Tensor | None = None,
 ) -> tuple[Tensor, Tensor | None]:
     """H_out = (residual ? H : 0) + (S[src] - act(H[rev])) @ W^T + b and, with a tile plan (tiles of at
     most ``tile_rows`` rows), S_out = scatter(agg_act(H_out), dst, reduce) in the same persistent launch.
@@ -645,7 +701,9 @@ def dmpnn_update_fused(
     ``amax_out`` (2 zero-filled floats) receives max|H_out|, max|S_out| for the next layer.
     ``row_table`` (with a plan): nt_dmpnn_row_table of (perm, dst_sorted, src, rev), built here
     when not given (cache it per graph).
-    ``zero_fill`` must be True when some node has no in-edge (its S_out row is then 0)."""
+    ``zero_fill`` must be True when some node has no in-edge (its S_out row is then 0).
+    ``S_part`` (fp32, slots x h): the hub partial rows when the row table marks hub sub-runs
+    (hub_runs); hub_combine then finishes the hubs' S_out rows."""
     dev = _require_device(H, S, src, rev, Wp, bias, out, S_out, perm, amax_in, amax_out)
     ld_in = _row_pitch("H", H)
     code = _DTYPE_CODES[H.dtype]
@@ -697,7 +755,8 @@ def dmpnn_update_fused(
          _ptr(H), _ptr(S), _ptr(src), _ptr(rev), _ptr(Wp), _ptr(bias), V, E, h, int(residual),
          act[0], act[1], _ptr(tile_ptr), ntiles, int(tile_rows), int(max_in_degree), _ptr(perm), _ptr(dsts),
          _ptr(row_table), reduce_code(reduce), agg_act[0], agg_act[1], code, _ptr(amax_in), _ptr(amax_out),
-         _ptr(out), _ptr(S_out), 0 if ld_in == h else ld_in, 0 if ld_out == h else ld_out, _stream(dev))
+         _ptr(out), _ptr(S_out), _ptr(S_part), 0 if ld_in == h else ld_in, 0 if ld_out == h else ld_out,
+         _stream(dev))
     return out, S_out
 
 

@@ -554,11 +554,20 @@ def row_table(lay: DeviceLayout, dsts: Tensor, src: Tensor, rev: Tensor, V: int)
     hit = getattr(lay, "row_table", None)
     if hit is None or hit[0] != key or hit[1] is not rev:
         rt = K.dmpnn_row_table(lay.dst_perm, dsts, src, rev, V)
-        if hub_info(lay) is not None:
-            K.mark_hub_rows(rt, lay.dst_ptr, HUB_DEGREE)
         hit = (key, rev, rt)
         lay.row_table = hit
     return hit[2]
+
+
+def hub_run_table(lay: DeviceLayout, rt: Tensor, tile_ptr: Tensor, dsts: Tensor, run_rows: int) -> tuple:
+    """The row table with hub sub-runs (kernels.hub_runs) for this plan's tiles, cached on the layout
+    (keyed on the base table and the plan): (table, nslots, hubs, slot_ptr)."""
+    key = (rt.data_ptr(), tile_ptr.data_ptr(), tile_ptr.numel(), run_rows)
+    hit = getattr(lay, "hub_runs", None)
+    if hit is None or hit[0] != key:
+        hit = (key, K.hub_runs(rt, lay.dst_ptr, dsts, tile_ptr, HUB_DEGREE, run_rows))
+        lay.hub_runs = hit
+    return hit[1]
 
 
 def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, residual, keep_states, amax):
@@ -574,6 +583,10 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
     timer = UPDATE_EVENTS
     maxdeg = fused_max_in_degree(lay)
     hubs = hub_info(lay)
+    part = None
+    if hubs is not None:  # hub sub-runs: the layer writes their partials, hub_combine finishes the hubs
+        rt, nslots, hub_ids, slot_ptr = hub_run_table(lay, rt, tile_ptr, dsts, max(1, maxdeg))
+        part = torch.empty(max(nslots, 1), H.shape[1], dtype=torch.float32, device=H.device)
     for l in range(d):
         last = l == d - 1
         if keep_states:
@@ -592,15 +605,14 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
             zero_fill=zf_out if last else zf_mid,
             amax_in=None if amax is None else amax[l],
             amax_out=None if (amax is None or last) else amax[l + 1],  # row d has no reader
-            row_table=rt, out=spare_H, S_out=None if last else spare_S, pitch_out=pitch,
+            row_table=rt, out=spare_H, S_out=None if last else spare_S, pitch_out=pitch, S_part=part,
         )
         if timer is not None:
             ev[1].record()
             timer.append(ev)
-        if hubs is not None:  # the hubs' share of the aggregation the fused launch left out
-            K.hub_aggregate(Hn, lay.dst_perm, lay.dst_ptr, hubs[0], Sn, reduce=reduce,
-                            act=_IDENTITY if last else act,
-                            amax=None if (amax is None or last) else amax[l + 1, 1:2])
+        if hubs is not None:  # the hubs' S_out rows from the launch's sub-run partials
+            K.hub_combine(part, hub_ids, slot_ptr, lay.dst_ptr, Sn, reduce=reduce,
+                          amax=None if (amax is None or last) else amax[l + 1, 1:2])
         if l == 0:
             _note_update("fused", H.dtype, H.shape[1], rows)
         if not keep_states:

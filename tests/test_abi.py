@@ -27,7 +27,7 @@ def test_header_declares_the_boundary():
         "nt_dmpnn_dense_matmul", "nt_dmpnn_weight_grad", "nt_dmpnn_weight_grad_workspace", "nt_segment_arg",
         "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg", "nt_absmax", "nt_dmpnn_fused_tile_rows",
         "nt_dmpnn_tile_stride", "nt_dmpnn_row_table", "nt_dmpnn_pack_weight_fk", "nt_dmpnn_tile_plan_hubs",
-        "nt_dmpnn_mark_hub_rows", "nt_dmpnn_hub_aggregate", "nt_dmpnn_weight_grad_fk",
+        "nt_dmpnn_mark_hub_rows", "nt_dmpnn_hub_aggregate", "nt_dmpnn_hub_combine", "nt_dmpnn_weight_grad_fk",
         "nt_softmax_pool_backward", "nt_dmpnn_init_chunked",
     }
 

@@ -41,13 +41,26 @@ def test_device_hub_plans_match_host():
     d = DeviceLayout(lay.dst_ptr.to(DEV), lay.dst_perm.to(DEV))
     hub = _engine.hub_info(d)
     assert torch.equal(hub[0].cpu(), ids) and hub[1:] == (nhub, rest)
-    # the row table marks exactly the hubs' rows: start flag, no end flag
-    rt = _engine.row_table(d, dsts, P.edge_index[0].to(DEV), P.rev_index.to(DEV), P.num_nodes).cpu()
-    flags, node = rt[:, 3] & 3, rt[:, 3] >> 2
+    # the base row table carries every row's node; the hub sub-run table (hub_run_table) turns exactly
+    # the hubs' rows into sub-runs of <= max_in_degree rows inside one tile, slots in dst order
+    rt0 = _engine.row_table(d, dsts, P.edge_index[0].to(DEV), P.rev_index.to(DEV), P.num_nodes)
+    assert (rt0[:, 3] >= 0).all()
+    tile_ptr = lay.plan_wide[0].to(DEV)
+    rt, nslots, hubs, slot_ptr = _engine.hub_run_table(d, rt0, tile_ptr, dsts, rest)
+    rt = rt.cpu()
     is_hub = torch.zeros(P.num_nodes, dtype=torch.bool)
     is_hub[ids.long()] = True
-    assert (flags[is_hub[node.long()]] == 1).all()
-    assert (flags[~is_hub[node.long()]] & 1).sum() == (~is_hub).sum() - (torch.diff(lay.dst_ptr) == 0).sum()
+    hub_row = is_hub[lay.plan[2].long()]
+    w = rt[:, 3]
+    assert torch.equal(w < 0, hub_row) and torch.equal(hubs.cpu(), ids)
+    wv = -w[hub_row] - 1
+    slot, fl = wv >> 2, wv & 3
+    starts = torch.nonzero(fl & 1).flatten()
+    ends = torch.nonzero(fl & 2).flatten()
+    assert starts.numel() == ends.numel() == nslots and torch.equal(slot[starts], torch.arange(nslots))
+    assert ((ends - starts + 1) <= rest).all() and ((ends - starts) >= 0).all()
+    sp = slot_ptr.cpu().long()
+    assert int(sp[-1]) == nslots and int(sp[0]) == 0 and (sp[ids.long() + 1] > sp[ids.long()]).all()
 
 
 _ACTS = {"relu": (nn.ReLU(), torch.relu), "identity": (nn.Identity(), lambda x: x), "silu": (nn.SiLU(), F.silu)}
@@ -221,3 +234,46 @@ def test_padded_rows_chunked_init_and_hub_aggregate_bit_identical():
         res[ld] = (H0.contiguous(), S.contiguous(), am, out.contiguous())
     for name, a, b in zip(("H0", "S", "amax", "hub out"), res[h], res[304]):
         assert torch.equal(a, b), name
+
+
+@pytest.mark.parametrize("rows", [64, 128])
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max"])
+def test_hub_subrun_partials_and_combine(rows, reduce):
+    """ABI 7 hub partials: with the row table's hub rows cut into sub-runs (kernels.hub_runs: within a
+    tile, at most max_in_degree rows), the fused layer writes each sub-run's reduce as a partial row and
+    hub_combine finishes the hubs' S_out rows; every node row against the oracle scatter of the layer
+    output, the non-hub rows bit-identical to the plain fused run's."""
+    from notorch_amd import kernels as K
+    from notorch_amd.data.synth import make_batch
+    from notorch_amd.nn.gnn import _engine
+
+    G = make_batch("polymer", 2, seed=8).collate("nodes").to(DEV)
+    lay = G._nt_layout
+    V, E, h = G.num_nodes, G.num_edges, 64
+    torch.manual_seed(1)
+    H, S = torch.randn(E, h, device=DEV), torch.randn(V, h, device=DEV)
+    W, b = torch.randn(h, h, device=DEV) / 8, torch.randn(h, device=DEV)
+    Wp = K.pack_weights(W)
+    src, rev = G.edge_index[0].contiguous(), G.rev_index
+    relu = K.act_code(nn.ReLU())
+    rows = min(rows, K.fused_tile_rows(h, torch.float32, relu, reduce, relu))
+    plan = _engine.fused_plan(lay, V, E, rows)
+    tile_ptr, ntiles, dsts, zf = plan
+    maxdeg = _engine.fused_max_in_degree(lay)
+    rt0 = K.dmpnn_row_table(lay.dst_perm, dsts, src, rev, V)
+    rt, nslots, hubs, slot_ptr = K.hub_runs(rt0, lay.dst_ptr, dsts, tile_ptr, _engine.HUB_DEGREE, maxdeg)
+    assert nslots > 0 and int(slot_ptr[-1]) == nslots
+    w = rt[:, 3]
+    assert (w < 0).sum() > 0 and torch.equal(rt[:, :3], rt0[:, :3])
+    part = torch.empty(nslots, h, device=DEV)
+    am = torch.zeros(2, 2, device=DEV)
+    K.absmax(H, am[0, 0:1])
+    K.absmax(S, am[0, 1:2])
+    out, Sn = K.dmpnn_update_fused(H, S, src, rev, Wp, b, act=relu, plan=(tile_ptr, ntiles, dsts), tile_rows=rows,
+                                   max_in_degree=maxdeg, perm=lay.dst_perm, reduce=reduce, agg_act=relu,
+                                   zero_fill=True, amax_in=am[0], row_table=rt, S_part=part)
+    K.hub_combine(part, hubs, slot_ptr, lay.dst_ptr, Sn, reduce=reduce)
+    ref = dmpnn_ref.scatter(torch.relu(out.cpu()), G.edge_index[1].cpu(), V, reduce)
+    assert_parity(Sn, ref, 1e-5, f"S_out with hub partials ({reduce})")
+    if reduce == "max":
+        assert torch.equal(Sn.cpu(), ref)
