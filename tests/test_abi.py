@@ -90,6 +90,36 @@ def test_abi_version_and_errors_without_gpu():
     assert rc == 1
 
 
+def test_abi7_row_pitch_and_hub_combine_checks_without_gpu():
+    """ABI 7 arguments are validated before any device call: row pitches (fp32 only, >= h, % 4),
+    hub partials (fp32 only), nt_dmpnn_hub_combine's sizes."""
+    from notorch_amd import _lib
+
+    lib = _lib.load()
+    fake = [ctypes.c_void_p(0x1000 * (i + 1)) for i in range(12)]
+    # nt_dmpnn_update_fused, bf16 with a padded input pitch: EUNSUPPORTED
+    rc = lib.nt_dmpnn_update_fused(*fake[:6], 10, 20, 512, 1, 1, 0.0, None, 0, 64, 4, None, None, None, 0, 1, 0.0,
+                                   1, None, None, fake[6], None, None, 520, 0, None)
+    assert rc == 3 and b"fp32 only" in lib.nt_last_error()
+    rc = lib.nt_dmpnn_update_fused(*fake[:6], 10, 20, 512, 1, 1, 0.0, None, 0, 64, 4, None, None, None, 0, 1, 0.0,
+                                   1, None, None, fake[6], None, fake[7], 0, 0, None)
+    assert rc == 3  # hub partials are fp32 only
+    # nt_dmpnn_init: a padded pitch needs fp32
+    rc = lib.nt_dmpnn_init(*fake[:5], 10, 20, 512, 1, 0.0, 0, 1, fake[5], fake[6], None, 520, None)
+    assert rc == 3 and b"ld_out" in lib.nt_last_error()
+    # nt_dmpnn_init_chunked: pitch % 4
+    rc = lib.nt_dmpnn_init_chunked(*fake[:5], 3, fake[5], None, None, 0, fake[6], 10, 20, 300, 1, 0.0, 0, 0,
+                                   fake[7], fake[8], fake[9], None, 302, None)
+    assert rc == 1 and b"ld_out" in lib.nt_last_error()
+    # nt_dmpnn_hub_combine: h % 4, pitch >= h
+    rc = lib.nt_dmpnn_hub_combine(*fake[:3], 2, fake[3], 10, 6, 0, 0, None, fake[4], 0, None)
+    assert rc == 1 and b"bad sizes" in lib.nt_last_error()
+    rc = lib.nt_dmpnn_hub_combine(*fake[:3], 2, fake[3], 10, 8, 0, 0, None, fake[4], 4, None)
+    assert rc == 1 and b"pitch" in lib.nt_last_error()
+    rc = lib.nt_dmpnn_hub_combine(*fake[:3], 2, fake[3], 10, 8, 0, 1, None, fake[4], 0, None)
+    assert rc == 3  # fp32 only
+
+
 def test_check_raises_with_message():
     from notorch_amd import _lib
 
