@@ -143,11 +143,14 @@ NT_API int nt_csr_build(const int64_t* idx, int64_t n, int64_t nseg, int32_t* se
  * only when S != NULL); the caller zero-fills them.  They are the amax_in of layer 0's
  * nt_dmpnn_update_fused.  ld_out (ABI 7): row pitch in elements of H0 and S (0 = h; > h: fp32 with
  * h % 4 == 0 and ld_out % 4 == 0, the padded rows nt_dmpnn_update_fused's ld_in takes).
+ * skip_degree (ABI 7; fp32 with S, h >= 128, 0 = none): nodes with more in-edges are skipped (no H0 rows
+ * of their in-edges, no S row): a hub graph's hubs then come from nt_dmpnn_init_chunked over a chunk
+ * plan of the hubs alone, so no wave walks a hub's hundreds of in-edges.
  */
 NT_API int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src, const int32_t* seg_ptr,
                   const int32_t* perm, int64_t V, int64_t E, int64_t h, int act, float act_alpha,
                   int reduce, int dtype, void* H0, void* S, float* amax_out, int64_t ld_out,
-                  void* stream);
+                  int skip_degree, void* stream);
 
 /*
  * max |X| over n fp32 elements, atomically max-ed into *out (device float; non-negative floats
@@ -205,14 +208,16 @@ NT_API int nt_segment_reduce_chunked(const void* X, const int32_t* perm, const i
  * on the dst CSR; H0 E x h, S V x h.  Same H0 as nt_dmpnn_init (bit-identical), same S as
  * nt_segment_reduce_chunked of that H0.  amax_out (may be NULL): 2 zero-filled device floats raised to
  * max|H0|, max|S|.  ld_out (ABI 7): row pitch in elements of H0 and S (0 = h; >= h, a multiple of 4;
- * the partial rows stay dense).
+ * the partial rows stay dense).  chunk_ids (ABI 7, may be NULL): pass 1 runs only these nids chunks of
+ * the plan (a hub graph's hub chunks, after nt_dmpnn_init with skip_degree wrote the other nodes).
  */
 NT_API int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64_t* src, const int32_t* perm,
                                  const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
                                  const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb,
                                  const int32_t* seg_ptr, int64_t V, int64_t E, int64_t h, int act,
                                  float act_alpha, int reduce, int dtype, float* partial, void* H0, void* S,
-                                 float* amax_out, int64_t ld_out, void* stream);
+                                 float* amax_out, int64_t ld_out, const int32_t* chunk_ids, int64_t nids,
+                                 void* stream);
 
 /* Bytes of the packed weight image for one h x h layer (see nt_dmpnn_pack_weight). */
 NT_API size_t nt_dmpnn_packed_weight_bytes(int64_t h, int dtype);

@@ -68,7 +68,7 @@ SIGNATURES: dict[str, tuple] = {
     "nt_dmpnn_init": (
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp, _c_i64,
-         _vp],
+         _c_int, _vp],
     ),
     "nt_absmax": (_c_int, [_vp, _c_i64, _c_int, _vp, _vp]),
     "nt_segment_reduce": (
@@ -84,7 +84,7 @@ SIGNATURES: dict[str, tuple] = {
     "nt_dmpnn_init_chunked": (
         _c_int,
         [_vp, _vp, _vp, _vp, _vp, _c_i64, _vp, _vp, _vp, _c_i64, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _c_int,
-         _c_int, _vp, _vp, _vp, _vp, _c_i64, _vp],
+         _c_int, _vp, _vp, _vp, _vp, _c_i64, _vp, _c_i64, _vp],
     ),
     "nt_dmpnn_packed_weight_bytes": (_c_size, [_c_i64, _c_int]),
     "nt_dmpnn_pack_weight": (_c_int, [_vp, _c_i64, _c_i64, _c_int, _vp, _vp]),

@@ -159,7 +159,7 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
     const float4* __restrict__ Xv, const float4* __restrict__ Xe, const int64_t* __restrict__ src,
     const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm, int64_t V, int64_t hv,
     int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S, float* __restrict__ amax,
-    int64_t lo) {  // lo: output row pitch in 16-B pieces (H0, S)
+    int64_t lo, int skip_deg) {  // lo: output row pitch in 16-B pieces (H0, S); skip_deg: see nt_dmpnn_init
   const int lane = threadIdx.x & 63;
   float mh = 0.f, ms = 0.f;  // max |H0|, max |S| of this lane (amax != NULL)
   const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
@@ -169,6 +169,7 @@ __global__ void __launch_bounds__(256) init_aggregate_wave(
   for (int64_t v = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
        v < V; v += nwaves) {
     const int32_t b = seg_ptr[v], en = seg_ptr[v + 1];
+    if (skip_deg > 0 && en - b > skip_deg) continue;  // a hub: its rows and S row come from the chunked init
     for (int64_t c0 = 0; c0 < hv; c0 += 64 * PPL) {
       int64_t cc[PPL];
       bool ok[PPL];
@@ -368,12 +369,14 @@ int fk_absmax(const float* X, int64_t n, float* out, hipStream_t stream);  // up
 extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
                              const int32_t* seg_ptr, const int32_t* perm, int64_t V, int64_t E,
                              int64_t h, int act, float act_alpha, int reduce, int dtype, void* H0,
-                             void* S, float* amax_out, int64_t ld_out, void* stream_) {
+                             void* S, float* amax_out, int64_t ld_out, int skip_degree, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
   NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
-  NT_REQUIRE(V >= 0 && E >= 0 && h > 0 && ld_out >= 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(V >= 0 && E >= 0 && h > 0 && ld_out >= 0 && skip_degree >= 0, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(skip_degree == 0 || (dtype == NT_F32 && S != nullptr && h % 4 == 0 && h >= 128), NT_EUNSUPPORTED,
+             "skip_degree needs fp32, the aggregation, h % 4 == 0 and h >= 128");
   if (ld_out == 0) ld_out = h;
   // padded output rows: the fp32 kernels that take them (the wave-per-node init, h >= 128, and the
   // plain init); every other variant writes dense rows
@@ -388,7 +391,8 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
   }
   const bool vec = (h % 4 == 0) && aligned16(Xv) && aligned16(Xe) && aligned16(H0) &&
                    (S == nullptr || aligned16(S));
-  NT_REQUIRE(ld_out == h || vec, NT_EINVAL, "padded output rows need 16-byte aligned pointers");
+  NT_REQUIRE((ld_out == h && skip_degree == 0) || vec, NT_EINVAL,
+             "padded output rows and skip_degree need 16-byte aligned pointers");
   if (S != nullptr) {
     if (V == 0) return NT_OK;
     NT_REQUIRE(seg_ptr && (perm || E == 0), NT_EINVAL, "fused aggregation needs the dst CSR");
@@ -404,12 +408,12 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
           NT_DISPATCH_RA(reduce, act,
                          (init_aggregate_wave<R_, A_, 1><<<grid, 256, 0, stream>>>(
                              (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
-                             act_alpha, (float4*)H0, (float4*)S, amax_out, lo4)));
+                             act_alpha, (float4*)H0, (float4*)S, amax_out, lo4, skip_degree)));
         } else {
           NT_DISPATCH_RA(reduce, act,
                          (init_aggregate_wave<R_, A_, 2><<<grid, 256, 0, stream>>>(
                              (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
-                             act_alpha, (float4*)H0, (float4*)S, amax_out, lo4)));
+                             act_alpha, (float4*)H0, (float4*)S, amax_out, lo4, skip_degree)));
         }
         NT_LAUNCH_CHECK();
         return NT_OK;
@@ -548,10 +552,12 @@ __global__ void __launch_bounds__(256) init_chunk_partial(const float* __restric
                                                           const int32_t* __restrict__ perm,
                                                           const int32_t* __restrict__ chunk_pos,
                                                           const int32_t* __restrict__ chunk_seg,
+                                                          const int32_t* __restrict__ chunk_ids,
                                                           int64_t nchunks, int64_t h, int act, float alpha,
                                                           float* __restrict__ H0, float* __restrict__ P,
                                                           float* __restrict__ S, float* __restrict__ amax,
                                                           int64_t lo) {  // lo: row pitch of H0 and S
+  // chunk_ids (may be NULL): the chunks to run (nchunks of them), else chunks 0 .. nchunks - 1
   constexpr int N = Piece<float, VEC>::N;
   constexpr int RR = R == NT_MEAN ? NT_SUM : R;  // the mean divides at the end
   const int64_t hw = h / N;
@@ -559,7 +565,8 @@ __global__ void __launch_bounds__(256) init_chunk_partial(const float* __restric
   float m = 0.f, ms = 0.f;
   for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < total;
        t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t k = t / hw, c = (t - k * hw) * N;
+    const int64_t ki = t / hw, c = (t - ki * hw) * N;
+    const int64_t k = chunk_ids ? chunk_ids[ki] : ki;
     const int32_t b = chunk_pos[k], e = chunk_pos[k + 1];
     Reducer<RR> r[N];
 #pragma unroll
@@ -723,13 +730,15 @@ int launch_init_chunked(const float* Xv, const float* Xe, const int64_t* src, co
                         const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
                         const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb, const int32_t* seg_ptr,
                         int64_t nseg, int64_t h, int reduce, int act, float alpha, float* P, float* H0, float* S,
-                        float* amax, int64_t lo, hipStream_t stream) {
+                        float* amax, int64_t lo, const int32_t* chunk_ids, int64_t nids, hipStream_t stream) {
   constexpr int N = Piece<float, VEC>::N;
-  if (nchunks > 0) {
-    const int g1 = grid_for(nchunks * (h / N), 256, 256 * 32);
+  const int64_t nrun = chunk_ids ? nids : nchunks;
+  if (nrun > 0) {
+    const int g1 = grid_for(nrun * (h / N), 256, 256 * 32);
     NT_DISPATCH_RA(reduce, act,
                    (init_chunk_partial<VEC, R_, A_><<<g1, 256, 0, stream>>>(
-                       Xv, Xe, src, perm, chunk_pos, chunk_seg, nchunks, h, act, alpha, H0, P, S, amax, lo)));
+                       Xv, Xe, src, perm, chunk_pos, chunk_seg, chunk_ids, nrun, h, act, alpha, H0, P, S, amax,
+                       lo)));
     NT_LAUNCH_CHECK();
   }
   if (chunk_seg == nullptr) ncomb = nseg;  // every segment through pass 2
@@ -798,12 +807,14 @@ extern "C" int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64
                                      const int32_t* chunk_seg, const int32_t* comb_seg, int64_t ncomb,
                                      const int32_t* seg_ptr, int64_t V, int64_t E, int64_t h, int act,
                                      float act_alpha, int reduce, int dtype, float* partial, void* H0, void* S,
-                                     float* amax_out, int64_t ld_out, void* stream_) {
+                                     float* amax_out, int64_t ld_out, const int32_t* chunk_ids, int64_t nids,
+                                     void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32, NT_EUNSUPPORTED, "nt_dmpnn_init_chunked is fp32 only");
   NT_REQUIRE(valid_reduce(reduce) && valid_act(act), NT_EINVAL, "bad reduce/act code");
-  NT_REQUIRE(V >= 0 && E >= 0 && nchunks >= 0 && h > 0 && ncomb >= 0 && ncomb <= V, NT_EINVAL, "bad sizes");
+  NT_REQUIRE(V >= 0 && E >= 0 && nchunks >= 0 && h > 0 && ncomb >= 0 && ncomb <= V && nids >= 0 &&
+                 nids <= nchunks, NT_EINVAL, "bad sizes");
   if (V == 0) return NT_OK;
   NT_REQUIRE(chunk_ptr && seg_ptr && S && (nchunks == 0 || (Xv && Xe && src && perm && chunk_pos && partial && H0)),
              NT_EINVAL, "NULL pointer");
@@ -816,10 +827,11 @@ extern "C" int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64
   return (h % 4 == 0 && al)
              ? launch_init_chunked<true>((const float*)Xv, (const float*)Xe, src, perm, chunk_pos, nchunks, chunk_ptr,
                                          chunk_seg, comb_seg, ncomb, seg_ptr, V, h, reduce, act, act_alpha, partial,
-                                         (float*)H0, (float*)S, amax_out, ld_out, stream)
+                                         (float*)H0, (float*)S, amax_out, ld_out, chunk_ids, nids, stream)
              : launch_init_chunked<false>((const float*)Xv, (const float*)Xe, src, perm, chunk_pos, nchunks,
                                           chunk_ptr, chunk_seg, comb_seg, ncomb, seg_ptr, V, h, reduce, act,
-                                          act_alpha, partial, (float*)H0, (float*)S, amax_out, ld_out, stream);
+                                          act_alpha, partial, (float*)H0, (float*)S, amax_out, ld_out, chunk_ids, nids,
+                                          stream);
 }
 
 // The fused layer's hub sub-run partials combined per hub (nt_dmpnn_hub_combine): pass 2 of the

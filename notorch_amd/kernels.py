@@ -209,8 +209,11 @@ def dmpnn_init(
     reduce: str = "sum",
     amax: Tensor | None = None,
     pitch: int | None = None,
+    skip_degree: int = 0,
 ) -> tuple[Tensor, Tensor | None]:
     """H0 = Xv[src] + Xe, optionally fused with S = scatter(act(H0), dst) (needs the dst CSR).
+    skip_degree (fp32, with S, h >= 128): nodes with more in-edges are left out (their H0 rows and S
+    row are then dmpnn_init_chunked's with chunk_ids = their chunks).
     amax (fp32, 2 zero-filled device floats): raised to max|H0|, max|S| (layer 0's amax_in).
     pitch (fp32, h % 4 == 0, h >= 128 with the aggregation): H0 and S as row-padded views whose rows
     sit ``pitch`` floats apart (nt_dmpnn_init's ld_out)."""
@@ -235,7 +238,8 @@ def dmpnn_init(
     lib = _lib.load()
     _run(dev, lib.nt_dmpnn_init,
          _ptr(Xv), _ptr(Xe), _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h, act[0], act[1],
-         reduce_code(reduce), code, _ptr(H0), _ptr(S), _ptr(amax), 0 if ld == h else ld, _stream(dev))
+         reduce_code(reduce), code, _ptr(H0), _ptr(S), _ptr(amax), 0 if ld == h else ld, int(skip_degree),
+         _stream(dev))
     return H0, S
 
 
@@ -400,6 +404,9 @@ def dmpnn_init_chunked(
     reduce: str = "sum",
     amax: Tensor | None = None,
     pitch: int | None = None,
+    H0: Tensor | None = None,
+    S: Tensor | None = None,
+    chunk_ids: Tensor | None = None,
 ) -> tuple[Tensor, Tensor]:
     """(H0, S) = dmpnn_init with layer 0's aggregation over the chunk plan of a hub graph (fp32,
     plan = chunk_plan(seg_ptr)): H0 written once, S combined from per-chunk partials.  amax (2
@@ -422,12 +429,20 @@ def dmpnn_init_chunked(
         raise ValueError("shape mismatch between Xv, Xe, src and the dst CSR")
     cargs = _chunk_args(plan, V)
     ld = h if pitch is None else int(pitch)
-    H0 = padded_rows(E, h, ld, torch.float32, dev)
-    S = padded_rows(V, h, ld, torch.float32, dev)
+    if H0 is None:
+        H0 = padded_rows(E, h, ld, torch.float32, dev)
+    if S is None:
+        S = padded_rows(V, h, ld, torch.float32, dev)
+    if H0.shape != (E, h) or S.shape != (V, h) or _row_pitch("H0", H0) != ld or _row_pitch("S", S) != ld:
+        raise ValueError("H0 / S must be E x h / V x h with the given row pitch")
+    if chunk_ids is not None and (chunk_ids.dtype != torch.int32 or not chunk_ids.is_contiguous()
+                                  or chunk_ids.numel() > nchunks):
+        raise ValueError("chunk_ids must be contiguous int32 chunk indices of the plan")
     partial = torch.empty(max(nchunks, 1), h, dtype=torch.float32, device=dev)
     _run(dev, _lib.load().nt_dmpnn_init_chunked,
          _ptr(Xv.contiguous()), _ptr(Xe.contiguous()), _ptr(src), _ptr(perm), *cargs, _ptr(seg_ptr), V, E, h, act[0], act[1], reduce_code(reduce), _DTYPE_CODES[torch.float32],
-         _ptr(partial), _ptr(H0), _ptr(S), _ptr(amax), 0 if ld == h else ld, _stream(dev))
+         _ptr(partial), _ptr(H0), _ptr(S), _ptr(amax), 0 if ld == h else ld, _ptr(chunk_ids),
+         0 if chunk_ids is None else chunk_ids.numel(), _stream(dev))
     return H0, S
 
 

@@ -256,6 +256,21 @@ def dst_chunks(lay: DeviceLayout):
     return ch or None
 
 
+def hub_chunk_ids(lay: DeviceLayout, chunks) -> Tensor:
+    """The chunks of the dst chunk plan that belong to segments longer than MAX_FUSED_IN_DEGREE (the
+    hubs' part of a hub graph's init), int32, cached on the layout with the plan; one sync."""
+    hit = getattr(lay, "hub_chunk_ids", None)
+    if hit is None or hit[0] is not chunks[0]:
+        chunk_ptr = chunks[2].long()
+        nch = chunk_ptr[1:] - chunk_ptr[:-1]
+        deg = (lay.dst_ptr[1:] - lay.dst_ptr[:-1]).long()
+        seg_of = torch.repeat_interleave(torch.arange(deg.numel(), device=deg.device), nch, output_size=chunks[1])
+        ids = torch.nonzero(deg[seg_of] > MAX_FUSED_IN_DEGREE).flatten().to(torch.int32)
+        hit = (chunks[0], ids)
+        lay.hub_chunk_ids = hit
+    return hit[1]
+
+
 def _aggregate(X, seg_ptr, perm, nseg, reduce, act, chunks, out=None, amax=None):
     """scatter(act(X), seg) by the chunked reduce (skewed segments) or the plain one; amax (fp32,
     1 device float) is raised to max|out| (fused into the chunked reduce, a separate pass otherwise)."""
@@ -366,9 +381,16 @@ def block_forward(
                                drop)
     chunks = dst_chunks(lay)
     pitch = row_pitch(Xv.shape[1], Xv.dtype) if (not keep_states and drop is None) else None
-    if chunks is not None and Xv.dtype == torch.float32:
-        # hubs: the initial gather inside pass 1 of the chunked reduce (the wave-per-node init would walk
-        # a hub's in-edges on one wave), so H0 is written once and not re-read
+    if chunks is not None and Xv.dtype == torch.float32 and Xv.shape[1] >= 128 and Xv.shape[1] % 4 == 0:
+        # hubs: the wave-per-node init for every node of in-degree <= MAX_FUSED_IN_DEGREE, then the
+        # chunked init (the initial gather inside pass 1 of the chunked reduce) over the hubs' chunks
+        # alone, so no wave walks a hub's hundreds of in-edges and H0 is written once
+        H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=act, reduce=reduce, amax=a0, pitch=pitch,
+                            skip_degree=MAX_FUSED_IN_DEGREE)
+        K.dmpnn_init_chunked(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, chunks, act=act, reduce=reduce,
+                             amax=a0, pitch=pitch, H0=H, S=S, chunk_ids=hub_chunk_ids(lay, chunks))
+    elif chunks is not None and Xv.dtype == torch.float32:
+        # the chunked init over every node (h < 128: no wave-per-node init)
         H, S = K.dmpnn_init_chunked(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, chunks, act=act, reduce=reduce, amax=a0,
                                     pitch=pitch)
     elif chunks is not None:

@@ -105,11 +105,11 @@ def test_abi7_row_pitch_and_hub_combine_checks_without_gpu():
                                    1, None, None, fake[6], None, fake[7], 0, 0, None)
     assert rc == 3  # hub partials are fp32 only
     # nt_dmpnn_init: a padded pitch needs fp32
-    rc = lib.nt_dmpnn_init(*fake[:5], 10, 20, 512, 1, 0.0, 0, 1, fake[5], fake[6], None, 520, None)
+    rc = lib.nt_dmpnn_init(*fake[:5], 10, 20, 512, 1, 0.0, 0, 1, fake[5], fake[6], None, 520, 0, None)
     assert rc == 3 and b"ld_out" in lib.nt_last_error()
     # nt_dmpnn_init_chunked: pitch % 4
     rc = lib.nt_dmpnn_init_chunked(*fake[:5], 3, fake[5], None, None, 0, fake[6], 10, 20, 300, 1, 0.0, 0, 0,
-                                   fake[7], fake[8], fake[9], None, 302, None)
+                                   fake[7], fake[8], fake[9], None, 302, None, 0, None)
     assert rc == 1 and b"ld_out" in lib.nt_last_error()
     # nt_dmpnn_hub_combine: h % 4, pitch >= h
     rc = lib.nt_dmpnn_hub_combine(*fake[:3], 2, fake[3], 10, 6, 0, 0, None, fake[4], 0, None)

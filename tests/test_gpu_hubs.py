@@ -277,3 +277,32 @@ def test_hub_subrun_partials_and_combine(rows, reduce):
     assert_parity(Sn, ref, 1e-5, f"S_out with hub partials ({reduce})")
     if reduce == "max":
         assert torch.equal(Sn.cpu(), ref)
+
+
+def test_split_hub_init_bit_identical_to_chunked_init():
+    """Hub graphs' init (round 5): the wave-per-node init skipping nodes of in-degree > 32 (ABI 7
+    skip_degree) plus the chunked init over the hubs' chunks alone (chunk_ids) give the full chunked
+    init's H0, S and amax bit for bit."""
+    from notorch_amd import kernels as K
+    from notorch_amd.data.synth import make_batch
+    from notorch_amd.nn.gnn import _engine
+
+    G = make_batch("polymer", 3, seed=9).collate("nodes").to(DEV)
+    lay = G._nt_layout
+    V, E, h = G.num_nodes, G.num_edges, 300
+    torch.manual_seed(4)
+    Xv, Xe = torch.randn(V, h, device=DEV), torch.randn(E, h, device=DEV)
+    src = G.edge_index[0].contiguous()
+    relu = K.act_code(nn.ReLU())
+    chunks = _engine.dst_chunks(lay)
+    assert chunks is not None
+    am0, am1 = torch.zeros(2, device=DEV), torch.zeros(2, device=DEV)
+    H_ref, S_ref = K.dmpnn_init_chunked(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, chunks, act=relu, amax=am0,
+                                        pitch=304)
+    H, S = K.dmpnn_init(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, act=relu, amax=am1, pitch=304,
+                        skip_degree=_engine.MAX_FUSED_IN_DEGREE)
+    ids = _engine.hub_chunk_ids(lay, chunks)
+    assert 0 < ids.numel() < chunks[1]
+    K.dmpnn_init_chunked(Xv, Xe, src, lay.dst_ptr, lay.dst_perm, chunks, act=relu, amax=am1, pitch=304, H0=H, S=S,
+                         chunk_ids=ids)
+    assert torch.equal(H, H_ref) and torch.equal(S, S_ref) and torch.equal(am0, am1)
