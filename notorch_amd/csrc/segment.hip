@@ -155,7 +155,7 @@ __global__ void __launch_bounds__(256) init_aggregate_vec4(
 // Lanes past the row read piece 0 and are masked at the stores.  Same order of operations per piece
 // as init_aggregate_vec4, so the same bits.  Rows wider than one pass loop over passes.
 template <int R, int ACT, int PPL>
-__global__ void __launch_bounds__(256) init_aggregate_wave(
+__global__ void __launch_bounds__(1024) init_aggregate_wave(
     const float4* __restrict__ Xv, const float4* __restrict__ Xe, const int64_t* __restrict__ src,
     const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm, int64_t V, int64_t hv,
     int act, float alpha, float4* __restrict__ H0, float4* __restrict__ S, float* __restrict__ amax,
@@ -403,15 +403,18 @@ extern "C" int nt_dmpnn_init(const void* Xv, const void* Xe, const int64_t* src,
 #ifndef NT_INIT_PPL1
 #define NT_INIT_PPL1 0  // A/B: 1 = one 64-piece pass at a time (the round-3 kernel)
 #endif
-        const int grid = grid_for(V * 64, 256, 256 * 8);  // grid-stride: 32 waves per CU
+#ifndef NT_INIT_BLOCK
+#define NT_INIT_BLOCK 1024  // A/B: threads per block (the amax chain: one atomic pair per block)
+#endif
+        const int grid = grid_for(V * 64, NT_INIT_BLOCK, 256 * 8 * 256 / NT_INIT_BLOCK);  // 32 waves per CU
         if (hv <= 64 || NT_INIT_PPL1) {
           NT_DISPATCH_RA(reduce, act,
-                         (init_aggregate_wave<R_, A_, 1><<<grid, 256, 0, stream>>>(
+                         (init_aggregate_wave<R_, A_, 1><<<grid, NT_INIT_BLOCK, 0, stream>>>(
                              (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
                              act_alpha, (float4*)H0, (float4*)S, amax_out, lo4, skip_degree)));
         } else {
           NT_DISPATCH_RA(reduce, act,
-                         (init_aggregate_wave<R_, A_, 2><<<grid, 256, 0, stream>>>(
+                         (init_aggregate_wave<R_, A_, 2><<<grid, NT_INIT_BLOCK, 0, stream>>>(
                              (const float4*)Xv, (const float4*)Xe, src, seg_ptr, perm, V, hv, act,
                              act_alpha, (float4*)H0, (float4*)S, amax_out, lo4, skip_degree)));
         }

@@ -60,6 +60,9 @@
 #ifndef FK_DEPHASE
 #define FK_DEPHASE 0
 #endif
+#ifndef FK_AMAX_BLOCK
+#define FK_AMAX_BLOCK 1  // A/B: 0 = one atomic pair per wave for the amax chain
+#endif
 // FK_EPI3: the epilogue of 128-row tiles staged through LDS (see fk_epilogue3)
 #ifndef FK_EPI3
 #define FK_EPI3 0
@@ -1291,10 +1294,31 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
 #endif
   if (a.amax_out) {
     const float mh = wave_max(st.mxH), ms = wave_max(st.mxS);
+#if FK_AMAX_BLOCK
+    // one atomic pair per workgroup (the waves' maxima through LDS): every wave of the workgroup ran
+    // the same persistent loop, so all reach this barrier
+    __shared__ float amx[2][NW];
+    if (st.lane == 0) {
+      amx[0][st.wave] = mh;
+      amx[1][st.wave] = ms;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      float bh = amx[0][0], bs = amx[1][0];
+#pragma unroll
+      for (int w = 1; w < NW; ++w) {
+        bh = fmaxf(bh, amx[0][w]);
+        bs = fmaxf(bs, amx[1][w]);
+      }
+      atomic_max_abs(a.amax_out, bh);
+      if (a.SO) atomic_max_abs(a.amax_out + 1, bs);
+    }
+#else
     if (st.lane == 0) {
       atomic_max_abs(a.amax_out, mh);
       if (a.SO) atomic_max_abs(a.amax_out + 1, ms);
     }
+#endif
   }
   if constexpr ((ABL & 256) != 0) {
     if (st.lane == 0) {
