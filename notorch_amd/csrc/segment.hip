@@ -122,6 +122,9 @@ __global__ void __launch_bounds__(256) segment_reduce_scalar(
 }
 
 // ---------------- fused init + first aggregation ----------------
+#ifndef NT_INIT_BATCH
+#define NT_INIT_BATCH 1
+#endif
 #ifndef NT_INIT_MASK
 #define NT_INIT_MASK 1  // A/B: 0 = every lane loads every pass (pieces past the row read piece 0)
 #endif
@@ -181,6 +184,45 @@ __global__ void __launch_bounds__(1024) init_aggregate_wave(
         cc[q] = ok[q] ? c : 0;
         r[q].init();
       }
+#if NT_INIT_BATCH
+      // In-edges 4 at a time, the ragged last batch included (n < 4 under wave-uniform guards), so a
+      // node of in-degree 1..4 issues its whole index chain and every row load before the first use.
+      for (int32_t j = b; j < en; j += 4) {
+        const int n = min(4, en - j);
+        int64_t ed[4] = {0, 0, 0, 0}, sv[4] = {0, 0, 0, 0};
+        float4 a[4][PPL], x[4][PPL];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (u < n) ed[u] = perm[j + u];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (u < n) sv[u] = src[ed[u]];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < PPL; ++q) {
+            if (u < n && (q == 0 || ok[q] || !NT_INIT_MASK)) {
+              a[u][q] = Xv[sv[u] * hv + cc[q]];
+              x[u][q] = Xe[ed[u] * hv + cc[q]];
+            } else {
+              a[u][q] = x[u][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+          }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          if (u >= n) break;
+#pragma unroll
+          for (int q = 0; q < PPL; ++q) {
+            const float4 h0 = a[u][q] + x[u][q];
+            if (ok[q]) {
+              H0[ed[u] * lo + cc[q]] = h0;
+              mh = amax4(mh, h0);
+            }
+            r[q].push(act4_t<ACT>(h0, act, alpha));
+          }
+        }
+      }
+#else
       int32_t j = b;
       for (; j + 4 <= en; j += 4) {
         int64_t ed[4], sv[4];
@@ -224,6 +266,7 @@ __global__ void __launch_bounds__(1024) init_aggregate_wave(
           r[q].push(act4_t<ACT>(h0, act, alpha));
         }
       }
+#endif
 #pragma unroll
       for (int q = 0; q < PPL; ++q) {
         if (ok[q]) {
