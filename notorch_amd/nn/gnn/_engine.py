@@ -380,7 +380,7 @@ def block_forward(
         return _layers_forward(H, None, V, src, rev, lay, weights, biases, act, reduce, residual, keep_states,
                                drop)
     chunks = dst_chunks(lay)
-    pitch = row_pitch(Xv.shape[1], Xv.dtype) if (not keep_states and drop is None) else None
+    pitch = row_pitch(Xv.shape[1], Xv.dtype, chunks is not None) if (not keep_states and drop is None) else None
     if chunks is not None and Xv.dtype == torch.float32 and Xv.shape[1] >= 128 and Xv.shape[1] % 4 == 0:
         # hubs: the wave-per-node init for every node of in-degree <= MAX_FUSED_IN_DEGREE, then the
         # chunked init (the initial gather inside pass 1 of the chunked reduce) over the hubs' chunks
@@ -402,20 +402,25 @@ def block_forward(
                            amax)
 
 
-def row_pitch(h: int, dtype: torch.dtype) -> Optional[int]:
+def row_pitch(h: int, dtype: torch.dtype, hubs: bool = False) -> Optional[int]:
     """Row pitch of the intermediate H_l / S_l of an inference forward: fp32 rows of h % 8 != 0 floats
     padded to a 32-byte multiple (h = 300 -> 304), so that no row shares a 32-B sector with its
     neighbour: the dst-ordered row stores of the init and of the layer kernels then write whole
     sectors, and every 16-B gather piece of a row lies in one sector (measured with tools/r5_pitch.sh:
     the layer kernel at h = 304 runs 113.5 us against 121.1 at h = 300, the same MFMA work).  None:
-    dense rows (h % 8 == 0 already, bf16, h < 128, or NT_ROW_PAD=0)."""
-    if dtype != torch.float32 or h % 4 or h % 8 == 0 or h < 128 or not _ROW_PAD:
+    dense rows (h % 8 == 0 already, bf16, h < 128, or NT_ROW_PAD=0).  Hub graphs (hubs: a node of
+    in-degree > MAX_FUSED_IN_DEGREE, dst_chunks) pad to whole 128-byte L2 lines instead (h = 300 ->
+    320): polymer-16 2.44 -> 2.39 ms per step, layer 658 -> 638 us (tools/r5_align.sh), while 128-B
+    rows lose at config 2 (389 -> 404 us per step) and at qm9-32k (2.99 -> 3.07 ms, tools/r5_align2.sh)."""
+    align = _ROW_ALIGN or (32 if hubs else 8)
+    if dtype != torch.float32 or h % 4 or h % align == 0 or h < 128 or not _ROW_PAD:
         return None
-    return (h + 7) // 8 * 8
+    return (h + align - 1) // align * align
 
 
 _NO_AMAX = torch.empty(0)  # a state without a valid amax row (bf16, or a path that skips the chain)
 _ROW_PAD = os.environ.get("NT_ROW_PAD", "1") != "0"  # A/B: 0 = dense intermediate rows
+_ROW_ALIGN = int(os.environ.get("NT_ROW_ALIGN", "0"))  # A/B: pitch multiple in floats (0: by graph size)
 
 
 # fp32 relu / sum layers on graphs of at most this many edges take 64-row tiles walked by two 4-wave

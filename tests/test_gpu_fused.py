@@ -496,8 +496,8 @@ def test_row_padded_init_and_layer_bit_identical(h, pitch, rows):
 
 @pytest.mark.parametrize("kind,n", [("qm9", 300), ("polymer", 2)])
 def test_block_forward_row_padding_is_invisible(monkeypatch, kind, n):
-    """The inference forward runs its intermediate layers on row-padded buffers (h = 300 -> 304; hub
-    graphs too: the chunked init, the hub aggregation): the block's outputs are dense tensors and
+    """The inference forward runs its intermediate layers on row-padded buffers (h = 300 -> 304, or
+    320 on hub graphs; hub graphs too: the chunked init, the hub aggregation): the block's outputs are dense tensors and
     equal, bit for bit, to the dense-row forward."""
     from notorch_amd.nn import ChempropBlock
     from notorch_amd.nn.gnn import _engine
@@ -509,12 +509,17 @@ def test_block_forward_row_padding_is_invisible(monkeypatch, kind, n):
     blk = ChempropBlock(hidden_dim=h, depth=3).to(DEV).eval()
     Gd = G.update(node_feats=Xv, edge_feats=Xe).to(DEV)
     res = {}
-    for pad in (True, False):
+    for pad, align in ((True, 8), (True, 32), (False, 0)):  # 304 (32-B sectors), 320 (128-B lines), dense
         monkeypatch.setattr(_engine, "_ROW_PAD", pad)
+        monkeypatch.setattr(_engine, "_ROW_ALIGN", align)
         with torch.no_grad():
             out = blk(Gd)
         assert out.node_feats.is_contiguous() and out.edge_feats.is_contiguous()
-        res[pad] = (out.node_feats.clone(), out.edge_feats.clone())
+        res[(pad, align)] = (out.node_feats.clone(), out.edge_feats.clone())
     monkeypatch.setattr(_engine, "_ROW_PAD", True)
+    monkeypatch.setattr(_engine, "_ROW_ALIGN", 32)
+    assert _engine.row_pitch(h, torch.float32) == 320
+    monkeypatch.setattr(_engine, "_ROW_ALIGN", 8)
     assert _engine.row_pitch(h, torch.float32) == 304
-    assert torch.equal(res[True][0], res[False][0]) and torch.equal(res[True][1], res[False][1])
+    for key in ((True, 8), (True, 32)):
+        assert torch.equal(res[key][0], res[(False, 0)][0]) and torch.equal(res[key][1], res[(False, 0)][1])
