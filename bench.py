@@ -20,10 +20,11 @@ GPU; N = 1: all eight in turn) -> fixed total work ("strong").  ``zinc-4096-bf16
 Also in the line:
 * ``roofline`` for the dominant kernel (the fused layer update; per-launch duration from HIP events
   recorded on the launch stream around every launch inside the timed region), with SURVEY §8(d)'s
-  definitions: ``frac`` = fp32 algorithmic flops / launch time / 157.3 TF fp32 MFMA peak (fp32
-  workloads; may exceed 1 because the kernel emulates fp32 on faster 16-bit MFMA), ``hbm_frac`` =
-  algorithmic bytes / launch time / 8 TB/s, ``emu_issue_frac`` = the 16-bit MFMA products actually
-  issued / launch time / 2.5 PF; ``traffic`` = HBM bytes per launch from rocprofv3 FETCH_SIZE (x2,
+  definitions: ``frac`` = t_min / launch time, t_min = max(algorithmic bytes / 8 TB/s, the MFMA
+  products the kernel issues / the peak of that MFMA type) -- the roof of the instructions it really
+  runs (fp32 storage: 3 fp16 products per MAC at 2.5 PF, so HBM binds at h = 300); ``hbm_frac`` =
+  algorithmic bytes / launch time / 8 TB/s; ``fp32_equiv_frac`` = 2·E·h² fp32 flops / launch time /
+  157.3 TF, a throughput figure beside it; ``traffic`` = HBM bytes per launch from rocprofv3 FETCH_SIZE (x2,
   gfx950) + WRITE_SIZE, read from ``--pmc-csv`` or from the committed profile of this workload
   (labelled with the commit it was taken at);
 * ``cpu_baseline``: the oracle restatement (ATen CPU) on the host, rank 0, N=1, a bounded sample,
@@ -204,8 +205,24 @@ def timed_steps(step, steps, warmup, env, dev):
         return time.perf_counter() - t0
 
 
+def issue_model(engine_info, bf16):
+    """(MFMA products per fp32 MAC, the peak those products issue at): the instructions the layer
+    kernel actually issues, so that the roof is the one it sits under.  fp32 storage runs the scaled
+    two-part fp16 split (3 fp16 products per MAC, 16-bit MFMA peak) unless the engine reports the
+    exact fp32 MFMA path; bf16 storage issues one bf16 product per MAC."""
+    products = engine_info.get("products", 1)
+    exact_f32 = not bf16 and products == 1
+    return products, PEAK_FP32_MFMA_TFLOPS if exact_f32 else PEAK_16BIT_MFMA_TFLOPS
+
+
 def launch_roofline(jobs, events, engine_info, traffic, traffic_src):
-    """Roofline of the dominant kernel (the layer update) from the per-launch HIP events."""
+    """Roofline of the dominant kernel (the layer update) from the per-launch HIP events.
+
+    The binding roof is the larger of t_hbm = algorithmic bytes / 8 TB/s and t_mfma = the MFMA
+    products the kernel issues / the peak of that MFMA type; ``frac`` = t_min / launch
+    time, so it can never exceed 1.  The fp32-equivalent throughput (2·E·h² fp32 flops per launch over
+    the fp32 MFMA peak) is reported beside it as ``fp32_equiv_frac``: a throughput figure, not a roof
+    (the kernel issues no fp32 MFMA)."""
     upd_ms = statistics.mean(a.elapsed_time(b) for a, b in events)
     t = upd_ms * 1e-3
     j = max(jobs, key=lambda x: x.E)
@@ -215,26 +232,30 @@ def launch_roofline(jobs, events, engine_info, traffic, traffic_src):
     alg_bytes = fused_bytes(V, E, h, b) if fused else update_bytes(V, E, h, b)
     flops = 2 * E * h * h
     kp, np_ = engine_info.get("kpad", h), engine_info.get("npad", h)
-    emu_flops = engine_info.get("products", 1) * 2 * E * kp * np_
+    products, mfma_peak = issue_model(engine_info, j.bf16)
+    issued = products * 2 * E * kp * np_
+    t_hbm = alg_bytes / (PEAK_HBM_GBPS * 1e9)
+    t_mfma = issued / (mfma_peak * 1e12)
+    t_min = max(t_hbm, t_mfma)
     hbm_gbps = alg_bytes / t / 1e9
     out = {"kernel": engine_info.get("kernel", "?"), "numerics": engine_info.get("numerics", "?")}
-    if j.bf16:
-        # bf16 storage: 1 bf16 product per MAC; HBM-bound
-        out.update(bound="hbm", achieved=hbm_gbps, peak=PEAK_HBM_GBPS, unit="GB/s",
-                   frac=hbm_gbps / PEAK_HBM_GBPS)
+    if t_hbm >= t_mfma:
+        out.update(bound="hbm", achieved=hbm_gbps, peak=PEAK_HBM_GBPS, unit="GB/s")
     else:
-        tf = flops / t / 1e12
-        out.update(bound="mfma", achieved=tf, peak=PEAK_FP32_MFMA_TFLOPS, unit="TFLOP/s",
-                   frac=tf / PEAK_FP32_MFMA_TFLOPS)
+        out.update(bound="mfma", achieved=issued / t / 1e12, peak=mfma_peak, unit="TFLOP/s")
     out.update(
+        frac=t_min / t,
         traffic=traffic, traffic_source=traffic_src,
         traffic_over_alg=None if traffic is None else traffic / alg_bytes,
         launch_us=upd_ms * 1e3, launches_timed=len(events),
         alg_bytes_per_launch=alg_bytes, flops_per_launch_fp32=flops,
         hbm_frac=hbm_gbps / PEAK_HBM_GBPS, alg_hbm_gbps=hbm_gbps,
-        emu_mfma_tflops=emu_flops / t / 1e12, emu_issue_frac=emu_flops / t / 1e12 / PEAK_16BIT_MFMA_TFLOPS,
-        t_min_us=max(alg_bytes / (PEAK_HBM_GBPS * 1e9), emu_flops / (PEAK_16BIT_MFMA_TFLOPS * 1e12)) * 1e6,
+        mfma_issued_per_launch=issued, mfma_issue_peak_tflops=mfma_peak,
+        mfma_issue_tflops=issued / t / 1e12, mfma_issue_frac=issued / t / 1e12 / mfma_peak,
+        t_hbm_us=t_hbm * 1e6, t_mfma_us=t_mfma * 1e6, t_min_us=t_min * 1e6,
     )
+    if not j.bf16:
+        out.update(fp32_equiv_tflops=flops / t / 1e12, fp32_equiv_frac=flops / t / 1e12 / PEAK_FP32_MFMA_TFLOPS)
     return out
 
 
@@ -600,13 +621,18 @@ def summary(res, args, env, pmc_csv=None):
     E = sum(j.E for j in jobs)
     B = sum(j.B for j in jobs)
     fwd_bytes, fwd_flops = forward_bytes_flops(V, E, B, res["h"], res["depth"], b=2 if res["bf16"] else 4)
-    mfma_peak = PEAK_16BIT_MFMA_TFLOPS if res["bf16"] else PEAK_FP32_MFMA_TFLOPS
-    t_min = max(fwd_bytes / (PEAK_HBM_GBPS * 1e9), fwd_flops / (mfma_peak * 1e12))
+    # the same binding-roof model as the layer roofline: bytes at 8 TB/s against the MFMA products the
+    # kernels issue (padded k / n, 3 fp16 products per fp32 MAC) at that MFMA type's peak
+    products, mfma_peak = issue_model(info, res["bf16"])
+    kp, np_ = info.get("kpad", res["h"]), info.get("npad", res["h"])
+    fwd_issued = products * 2 * res["depth"] * E * kp * np_
+    t_min = max(fwd_bytes / (PEAK_HBM_GBPS * 1e9), fwd_issued / (mfma_peak * 1e12))
     return roof, {
-        "alg_bytes_per_rank": fwd_bytes, "flops_per_rank": fwd_flops,
+        "alg_bytes_per_rank": fwd_bytes, "flops_per_rank": fwd_flops, "mfma_issued_per_rank": fwd_issued,
         "hbm_frac": fwd_bytes / t_step / (PEAK_HBM_GBPS * 1e9),
-        "mfma_frac": fwd_flops / t_step / (mfma_peak * 1e12),
+        "mfma_issue_frac": fwd_issued / t_step / (mfma_peak * 1e12),
         "binding_frac": t_min / t_step,
+        "t_min_us": t_min * 1e6,
     }
 
 

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define NT_ABI_VERSION 7
+#define NT_ABI_VERSION 8
 
 #if defined(NT_BUILD)
 #define NT_API __attribute__((visibility("default")))
@@ -210,6 +210,9 @@ NT_API int nt_segment_reduce_chunked(const void* X, const int32_t* perm, const i
  * max|H0|, max|S|.  ld_out (ABI 7): row pitch in elements of H0 and S (0 = h; >= h, a multiple of 4;
  * the partial rows stay dense).  chunk_ids (ABI 7, may be NULL): pass 1 runs only these nids chunks of
  * the plan (a hub graph's hub chunks, after nt_dmpnn_init with skip_degree wrote the other nodes).
+ * Pass 2 still combines every segment in comb_seg, so chunk_ids must list EVERY chunk of every
+ * multi-chunk segment: with skip_degree <= the plan's chunk rows (kernels.CHUNK_ROWS = 32), each node
+ * nt_dmpnn_init skipped has all its chunks listed and each node it wrote is a single chunk.
  */
 NT_API int nt_dmpnn_init_chunked(const void* Xv, const void* Xe, const int64_t* src, const int32_t* perm,
                                  const int32_t* chunk_pos, int64_t nchunks, const int32_t* chunk_ptr,
@@ -521,15 +524,6 @@ NT_API int nt_dmpnn_weight_grad_fk(const void* G, const void* H, const void* S, 
                                    float act_alpha, const float* amax_G, const float* amax_HS, int dtype,
                                    void* workspace, int64_t workspace_bytes, void* dW_out, void* db_out,
                                    void* stream);
-
-/* Device status word of the calling device (no reference counterpart: the reference's ops cannot
- * hang).  The persistent fp32 update kernel hands work between its waves through bounded LDS waits;
- * a wait that gives up sets this word (sticky) and the launch's outputs are invalid.
- * nt_device_status enqueues on `stream` a copy of the word into *host_out (caller-owned, pinned for
- * an asynchronous copy); the wrapper raises on a nonzero word at its next call.
- * nt_device_status_reset clears it (stream-ordered). */
-NT_API int nt_device_status(uint32_t* host_out, void* stream);
-NT_API int nt_device_status_reset(void* stream);
 
 #ifdef __cplusplus
 }

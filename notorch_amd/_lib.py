@@ -23,7 +23,7 @@ if _NT_LIB.startswith("variant:"):
     LIB_PATH = os.path.join(_LIB_DIR, f"libnotorch_amd_{_NT_LIB.split(':', 1)[1]}.so")
 else:
     LIB_PATH = os.path.join(_LIB_DIR, "libnotorch_amd_diag.so" if DIAG else "libnotorch_amd.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 NT_F32, NT_BF16 = 0, 1
 NT_SUM, NT_MEAN, NT_MAX, NT_MIN = 0, 1, 2, 3
@@ -149,8 +149,6 @@ SIGNATURES: dict[str, tuple] = {
         [_vp, _vp, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64, _c_int, _c_f32, _vp, _vp, _c_int, _vp, _c_i64, _vp, _vp,
          _vp],
     ),
-    "nt_device_status": (_c_int, [_vp, _vp]),
-    "nt_device_status_reset": (_c_int, [_vp]),
 }
 
 

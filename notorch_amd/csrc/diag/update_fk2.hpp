@@ -318,7 +318,6 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk2_kernel(Args a) {
       st.emap[0 * ROWS + st.grow] = row_entry(r0, v0);
       st.emap[1 * ROWS + st.grow] = row_entry(r1, v1);
     }
-    if ((h0.n > ROWS || (ntl > 1 && h1.n > ROWS)) && tid == 0) atomicOr(&g_pk_timeout, 2u);
     n_cur = h0.n < ROWS ? h0.n : ROWS;
     n_nxt = h1.n < ROWS ? h1.n : ROWS;
   }
@@ -428,7 +427,6 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk2_kernel(Args a) {
           const bool v2 = st.grow < h2.n;
           nxt = row_offsets(a, raw2, v2);
           if (info_writer) st.emap[((i + 1) % kEmaps) * ROWS + st.grow] = row_entry(raw2, v2);
-          if (h2.n > ROWS && i + 1 < ntl && tid == 0) atomicOr(&g_pk_timeout, 2u);
           n_nxt = h2.n < ROWS ? h2.n : ROWS;
           h2 = h3;
           raw2 = row_raw<RT, TABLE>(a, h2, st.grow);

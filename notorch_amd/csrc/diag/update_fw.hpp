@@ -702,7 +702,6 @@ __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int ts
       st.emap[0 * kRows + st.grow] = fk::row_entry(r0, v0);
       st.emap[1 * kRows + st.grow] = fk::row_entry(r1, v1);
     }
-    if ((h0.n > kRows || (ntl > 1 && h1.n > kRows)) && tid == 0) atomicOr(&g_pk_timeout, 2u);
     n_cur = h0.n < kRows ? h0.n : kRows;
     n_nxt = h1.n < kRows ? h1.n : kRows;
   }
@@ -788,7 +787,6 @@ __device__ __forceinline__ void fw_run(const Args& a, char* smem, int t0, int ts
     const bool v2 = st.grow < h2.n;
     nxt = fk::row_offsets(a, raw2, v2);
     if (info_writer) st.emap[((i + 2) % kEmaps) * kRows + st.grow] = fk::row_entry(raw2, v2);
-    if (h2.n > kRows && i + 2 < ntl && tid == 0) atomicOr(&g_pk_timeout, 2u);
     n_nxt = h2.n < kRows ? h2.n : kRows;
     h2 = h3;
     raw2 = fk::row_raw<kRT, true>(a, h2, st.grow);

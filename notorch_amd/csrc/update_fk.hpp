@@ -1,6 +1,7 @@
 // fp32 D-MPNN layer kernel on fp16 MFMA with a two-part split ("fk"), optionally fused with the
-// aggregation its output feeds.  Included by update_pk.hip (it shares that unit's device status
-// word g_pk_timeout).
+// aggregation its output feeds.  Included by update_pk.hip.  Tiles hold at most 16 RT rows: the plan
+// builders guarantee it and check it when they build a plan (kernels.tile_plan, host_tile_plan); the
+// kernel clamps a larger tile to its capacity (memory-safe) and keeps no device status word.
 //
 //   H_out[e] = (residual ? H[e] : 0) + W (S[src[e]] - act(H[rev[e]])) + b        (chemprop.py:36-43,
 //                                                                                 residual.py:27-28)
@@ -1112,7 +1113,6 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
       st.emap[0 * ROWS + st.grow] = row_entry(r0, v0);
       st.emap[1 * ROWS + st.grow] = row_entry(r1, v1);
     }
-    if ((h0.n > ROWS || (ntl > 1 && h1.n > ROWS)) && tid == 0) atomicOr(&g_pk_timeout, 2u);
     n_cur = h0.n < ROWS ? h0.n : ROWS;
     n_nxt = h1.n < ROWS ? h1.n : ROWS;
   }
@@ -1276,7 +1276,6 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
       const bool v2 = st.grow < h2.n;
       nxt = row_offsets(a, raw2, v2);
       if (info_writer) st.emap[((i + 1) % kEmaps) * ROWS + st.grow] = row_entry(raw2, v2);
-      if (h2.n > ROWS && i + 1 < ntl && tid == 0) atomicOr(&g_pk_timeout, 2u);
       n_nxt = h2.n < ROWS ? h2.n : ROWS;
       h2 = h3;
       raw2 = row_raw<RT, TABLE>(a, h2, st.grow);
@@ -1320,6 +1319,7 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
     }
 #endif
   }
+#ifdef NT_DIAG
   if constexpr ((ABL & 256) != 0) {
     if (st.lane == 0) {
       for (int q = 0; q < 5; ++q) atomicAdd(&g_pk_stamps[q], tacc[q]);
@@ -1327,6 +1327,7 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
       atomicAdd(&g_pk_stamps[7], 1ull);
     }
   }
+#endif
 }
 
 // Row table of a fused plan (one 16-B entry per dst-sorted position, so the layer kernel reaches a

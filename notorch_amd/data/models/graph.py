@@ -545,10 +545,20 @@ def host_tile_stride(E: int, max_in_degree: int, rows: int, ncu: int) -> int:
     return max(1, min(L, lmax))
 
 
-def host_tile_ptr(dst_ptr: np.ndarray, E: int, stride: int, hub_degree: int = 0) -> tuple:
+def check_tile_rows(tile_ptr: np.ndarray, rows: int) -> None:
+    """The layer kernels hold at most `rows` rows per tile: a plan with a larger tile is rejected where
+    it is built (the kernels keep no device status word to report it later)."""
+    if len(tile_ptr) > 1:
+        mx = int(np.diff(tile_ptr.astype(np.int64)).max())
+        if mx > rows:
+            raise ValueError(f"tile plan holds a tile of {mx} rows > the kernel's {rows}: the max in-degree "
+                             "given to the planner is below the graph's")
+
+
+def host_tile_ptr(dst_ptr: np.ndarray, E: int, stride: int, hub_degree: int = 0, rows: Optional[int] = None) -> tuple:
     """(tile_ptr[ntiles+1], ntiles) as nt_dmpnn_tile_plan builds them: tile k starts at
     dst_ptr[first v with dst_ptr[v] >= k stride]; with hub_degree > 0 as nt_dmpnn_tile_plan_hubs
-    (a target inside a node with more in-edges is kept as the cut)."""
+    (a target inside a node with more in-edges is kept as the cut).  rows: checked tile capacity."""
     ntiles = (E + stride - 1) // stride if E > 0 else 0
     tile_ptr = np.empty(ntiles + 1, dtype=np.int32)
     if ntiles:
@@ -561,6 +571,8 @@ def host_tile_ptr(dst_ptr: np.ndarray, E: int, stride: int, hub_degree: int = 0)
             v = np.searchsorted(dst_ptr, t, side="left")
             tile_ptr[:ntiles] = dst_ptr[v]
     tile_ptr[ntiles] = E
+    if rows is not None:
+        check_tile_rows(tile_ptr, rows)
     return torch.from_numpy(tile_ptr), ntiles
 
 
@@ -570,7 +582,7 @@ def host_tile_plan(dst_ptr: np.ndarray, E: int, max_in_degree: int, rows: int = 
     nt_dmpnn_tile_plan_hubs) builds them with the stride of nt_dmpnn_tile_stride(E, max_in_degree,
     rows, ncu)."""
     stride = host_tile_stride(E, max_in_degree, rows, ncu) if E > 0 else 1
-    tile_ptr, ntiles = host_tile_ptr(dst_ptr, E, stride, hub_degree)
+    tile_ptr, ntiles = host_tile_ptr(dst_ptr, E, stride, hub_degree, rows)
     counts = np.diff(dst_ptr.astype(np.int64))
     dsts = np.repeat(np.arange(len(counts), dtype=np.int32), counts)
     return tile_ptr, ntiles, torch.from_numpy(dsts)
@@ -615,7 +627,8 @@ def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional
     if E > 0 and V > 0:
         tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg, rows=64, ncu=PLAN_NCU, hub_degree=hub)
         lay.plan = (tile_ptr, ntiles, dsts, mindeg == 0)
-        lay.plan_wide = host_tile_ptr(dst_ptr, E, host_tile_stride(E, maxdeg, WIDE_TILE_ROWS, PLAN_NCU), hub)
+        lay.plan_wide = host_tile_ptr(dst_ptr, E, host_tile_stride(E, maxdeg, WIDE_TILE_ROWS, PLAN_NCU), hub,
+                                      WIDE_TILE_ROWS)
     lay.dst_chunks = host_chunk_plan(dst_ptr) if lay.deg_range[0] > LONG_SEGMENT else False
     if mol_ptr is not None:
         n = np.diff(mol_ptr.astype(np.int64))

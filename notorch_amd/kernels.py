@@ -44,10 +44,6 @@ __all__ = [
     "segment_arg",
     "dmpnn_edge_backward_arg",
     "gather_rows_arg",
-    "watch_device_status",
-    "check_device_status",
-    "reset_device_status",
-    "DeviceStatusError",
 ]
 
 
@@ -572,7 +568,9 @@ def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int, rows: int = 64,
     at most `rows` rows (max_in_degree <= 32), balanced to whole rounds of ncu tiles (ncu = 0: the
     largest tiles; the engine's 128-row plans use PLAN_NCU).  hub_degree > 0: nodes with more
     in-edges are hubs, cut at the stride (nt_dmpnn_tile_plan_hubs; max_in_degree is then the largest
-    non-hub in-degree)."""
+    non-hub in-degree).  The plan's largest tile is checked against `rows` here, where the plan is
+    built (one device->host read per plan; the engine builds one per graph layout): the layer kernels
+    clamp a larger tile and keep no status word, so a wrong max_in_degree must fail at this call."""
     dev = _require_device(dst_ptr)
     if dst_ptr.dtype != torch.int32:
         raise TypeError("dst_ptr must be int32")
@@ -590,6 +588,11 @@ def tile_plan(dst_ptr: Tensor, E: int, max_in_degree: int, rows: int = 64,
     else:
         _run(dev, lib.nt_dmpnn_tile_plan,
              _ptr(dst_ptr), V, E, stride, _ptr(tile_ptr), ntiles, _ptr(dsts), _stream(dev))
+    if ntiles > 0:
+        mx = int((tile_ptr[1:] - tile_ptr[:-1]).max())
+        if mx > rows:
+            raise ValueError(f"tile plan holds a tile of {mx} rows > {rows}: max_in_degree={max_in_degree} is "
+                             "below the graph's largest (non-hub) in-degree")
     return tile_ptr, ntiles, dsts
 
 
@@ -705,6 +708,7 @@ def dmpnn_update_fused(
     S_out: Tensor | None = None,
     pitch_out: int | None = None,
     S_part: Tensor | None = None,
+    n_nodes: int | None = None,
 ) -> tuple[Tensor, Tensor | None]:
     """H_out = (residual ? H : 0) + (S[src] - act(H[rev])) @ W^T + b and, with a tile plan (tiles of at
     most ``tile_rows`` rows), S_out = scatter(agg_act(H_out), dst, reduce) in the same persistent launch.
@@ -718,7 +722,9 @@ def dmpnn_update_fused(
     when not given (cache it per graph).
     ``zero_fill`` must be True when some node has no in-edge (its S_out row is then 0).
     ``S_part`` (fp32, slots x h): the hub partial rows when the row table marks hub sub-runs
-    (hub_runs); hub_combine then finishes the hubs' S_out rows."""
+    (hub_runs); hub_combine then finishes the hubs' S_out rows.
+    ``n_nodes``: the aggregation's segment count, i.e. the rows S_out must hold (default: S's rows;
+    the backward's fused dA passes S = G with E rows and S_out with the graph's V)."""
     dev = _require_device(H, S, src, rev, Wp, bias, out, S_out, perm, amax_in, amax_out)
     ld_in = _row_pitch("H", H)
     code = _DTYPE_CODES[H.dtype]
@@ -747,18 +753,28 @@ def dmpnn_update_fused(
         tile_ptr, ntiles, dsts = plan
         if perm is None or perm.dtype != torch.int32 or perm.numel() != E:
             raise ValueError("fused aggregation needs the int32 dst CSR permutation")
+        if dsts is None or dsts.dtype != torch.int32 or dsts.numel() != E:
+            raise ValueError("the plan's dst_sorted must be int32 with E entries")
+        n_out = V if n_nodes is None else int(n_nodes)
+        if S_part is not None and (S_part.dtype != torch.float32 or not S_part.is_contiguous()
+                                   or S_part.dim() != 2 or S_part.shape[1] != h or S_part.shape[0] < 1):
+            raise ValueError("S_part must be a contiguous fp32 (slots x h) tensor")
         if S_out is None:
-            S_out = padded_rows(V, h, ld_out, H.dtype, dev)
+            S_out = padded_rows(n_out, h, ld_out, H.dtype, dev)
             if zero_fill:
                 S_out.zero_()
         else:
             if _row_pitch("S_out", S_out, H.dtype) != ld_out:
                 raise ValueError("out and S_out must share one row pitch")
+            if S_out.shape[0] < n_out or S_out.shape[1] != h:
+                raise ValueError(f"S_out must hold n_nodes={n_out} rows of h={h}")
             if zero_fill:
                 S_out.zero_()
     else:
         perm = None
         S_out = None
+        if S_part is not None:
+            raise ValueError("S_part needs a tile plan")
     if plan is not None and row_table is None and E > 0:
         row_table = dmpnn_row_table(perm, dsts, src, rev, V)
     if H.dtype == torch.float32 and amax_in is None and E > 0:
@@ -1180,64 +1196,3 @@ def dropout_residual(Y: Tensor, p: float, seed: int, offset: int = 0, *, base: T
     return out
 
 
-# ------------------------------------------------------------------------------------ status word
-class DeviceStatusError(RuntimeError):
-    """A bounded wait inside the persistent update kernel gave up: outputs are invalid."""
-
-
-_STATUS: dict = {}  # device index -> [pinned uint32[1], torch.cuda.Event, forwards since the last copy]
-STATUS_EVERY = 8  # copy the (sticky) word every STATUS_EVERY forwards: ~10 us per copy on the stream
-
-
-def _status_error(dev: torch.device) -> DeviceStatusError:
-    return DeviceStatusError(
-        f"notorch_amd: a bounded producer/consumer wait in update_pk_kernel gave up on {dev}; the "
-        "outputs of the forward(s) since the last status check are invalid "
-        "(reset with notorch_amd.kernels.reset_device_status)")
-
-
-def watch_device_status(dev: torch.device) -> None:
-    """Called after every forward that ran the persistent kernel: raise if an EARLIER forward on
-    this device set the status word (checked without a host sync once its copy has landed), then
-    enqueue an asynchronous copy of the word into pinned host memory for the next call."""
-    if torch.cuda.is_current_stream_capturing():
-        return  # no queries / copies inside a hipGraph capture: replays are checked by check_device_status
-    ent = _STATUS.get(dev.index)
-    if ent is None:
-        ent = [torch.zeros(1, dtype=torch.int32).pin_memory(), torch.cuda.Event(), 0]
-        _STATUS[dev.index] = ent
-        fresh = True
-    else:
-        fresh = False
-    host, ev, n = ent
-    if not fresh and ev.query() and int(host[0]) != 0:
-        raise _status_error(dev)
-    ent[2] = n + 1
-    if n % STATUS_EVERY:
-        return  # the word is sticky: a give-up is seen by the next copy, at most STATUS_EVERY forwards on
-    _run(dev, _lib.load().nt_device_status, host.data_ptr(), _stream(dev))
-    ev.record(torch.cuda.current_stream(dev))
-
-
-def check_device_status(dev: torch.device | str | int = "cuda") -> None:
-    """Synchronous check (syncs dev's current stream): raise DeviceStatusError if the status word
-    is set."""
-    dev = torch.device(dev) if not isinstance(dev, int) else torch.device("cuda", dev)
-    if dev.index is None:
-        dev = torch.device("cuda", torch.cuda.current_device())
-    host = torch.zeros(1, dtype=torch.int32).pin_memory()
-    _run(dev, _lib.load().nt_device_status, host.data_ptr(), _stream(dev))
-    torch.cuda.current_stream(dev).synchronize()
-    if int(host[0]) != 0:
-        raise _status_error(dev)
-
-
-def reset_device_status(dev: torch.device | str | int = "cuda") -> None:
-    dev = torch.device(dev) if not isinstance(dev, int) else torch.device("cuda", dev)
-    if dev.index is None:
-        dev = torch.device("cuda", torch.cuda.current_device())
-    _run(dev, _lib.load().nt_device_status_reset, _stream(dev))
-    ent = _STATUS.get(dev.index)
-    if ent is not None:
-        torch.cuda.current_stream(dev).synchronize()
-        ent[0].zero_()

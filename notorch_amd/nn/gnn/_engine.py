@@ -169,6 +169,9 @@ def _degree_range(lay: DeviceLayout) -> tuple[int, int]:
 
 
 MAX_FUSED_IN_DEGREE = 32  # larger in-degrees do not fit node-aligned tiles: the graph has hubs
+# the hub-graph init (nt_dmpnn_init with skip_degree = MAX_FUSED_IN_DEGREE, then the chunked init over
+# the skipped nodes' chunks) needs every multi-chunk segment to be a skipped node (notorch_amd.h)
+assert K.CHUNK_ROWS >= MAX_FUSED_IN_DEGREE, "chunk rows must cover the wave init's in-degree cut"
 HUB_DEGREE = 9  # in a hub graph, nodes with more in-edges are cut at the stride and reduced separately
 
 
@@ -569,8 +572,6 @@ def _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residu
             spare = H  # H_l is dead once H_{l+1} exists: reuse its buffer for H_{l+2}
         H = Hn
     node = _aggregate(H, lay.dst_ptr, lay.dst_perm, V, reduce, _IDENTITY, chunks)
-    if persistent:
-        K.watch_device_status(H.device)
     return node, H, states
 
 
@@ -646,8 +647,6 @@ def _fused_forward(H, S, src, rev, lay, plan, rows, Wps, biases, act, reduce, re
             spare_H = H
             spare_S = S
         H, S = Hn, Sn
-    if H.dtype == torch.float32:  # the persistent kernel's device status word
-        K.watch_device_status(H.device)
     return S, H, states
 
 
@@ -853,7 +852,7 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
     src_ptr, src_perm, rev_ptr, rev_perm = backward_layout(lay, src, rev, V, E)
     mean_ptr = lay.dst_ptr if reduce == "mean" else None
     d = len(weights)
-    gdtype = (dH if dH is not None else dnode).dtype
+    gdtype = dH.dtype if dH is not None else (dnode.dtype if dnode is not None else states[0][0].dtype)
     # G = dL/dH_d: the gather of dnode below writes it whole when H_d itself has no gradient (no
     # E x h zero fill to add it to)
     G = dH.contiguous() if dH is not None else None
@@ -920,7 +919,7 @@ def block_backward(dnode, dH, states, weights, src, dst, rev, lay, act, reduce, 
             dA, dS = K.dmpnn_update_fused(Gu, Gu, ident, none, packed_transpose(weights[l]), None,
                                           residual=False, act=_RELU, plan=plan3, tile_rows=64, max_in_degree=dmax,
                                           perm=src_perm, reduce="sum", agg_act=_IDENTITY, amax_in=amx,
-                                          row_table=rt, S_out=dS)
+                                          row_table=rt, S_out=dS, n_nodes=V)
         else:
             if fk_dense:
                 dA = K.dense_matmul(Gu, packed_transpose(weights[l]), amax=gmax)
@@ -975,6 +974,8 @@ class ChempropBlockFunction(torch.autograd.Function):
         nparams = len(is_none)
         params = [None if n else p for p, n in zip(rest[:nparams], is_none)]
         need = ctx.needs_input_grad
+        if dnode is None and dH is None:  # set_materialize_grads(False): neither output reached the loss
+            return (None,) * (11 + nparams)
         if kernel_bwd:
             flat = rest[nparams:]
             states = [tuple(flat[3 * i:3 * i + 3]) for i in range(nlayers)]

@@ -28,11 +28,11 @@ def pytest_collection_modifyitems(config, items):
 
 
 @pytest.fixture(autouse=True)
-def _device_status_clean(request):
-    """Every GPU test ends with the persistent kernel's status word clear (no bounded wait gave
-    up anywhere in the test): kernels.check_device_status syncs and raises otherwise."""
+def _device_sync(request):
+    """Every GPU test ends with a device synchronisation, so an asynchronous kernel error surfaces in
+    the test that launched the kernel."""
     yield
     if "gpu" in request.keywords and _gpu_available():
-        from notorch_amd import kernels
+        import torch
 
-        kernels.check_device_status()
+        torch.cuda.synchronize()

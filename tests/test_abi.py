@@ -23,7 +23,7 @@ def test_header_declares_the_boundary():
         "nt_dmpnn_pack_weight", "nt_dmpnn_pack_weights_fk", "nt_dmpnn_update", "nt_dmpnn_tile_count", "nt_dmpnn_tile_plan",
         "nt_dmpnn_update_fused", "nt_dmpnn_message", "nt_dmpnn_edge_backward", "nt_gather_rows",
         "nt_embed_bag", "nt_dmpnn_init_embed", "nt_node_scores", "nt_softmax_pool",
-        "nt_collate_graphs", "nt_segment_reduce_chunked", "nt_device_status", "nt_device_status_reset",
+        "nt_collate_graphs", "nt_segment_reduce_chunked",
         "nt_dmpnn_dense_matmul", "nt_dmpnn_weight_grad", "nt_dmpnn_weight_grad_workspace", "nt_segment_arg",
         "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg", "nt_absmax", "nt_dmpnn_fused_tile_rows",
         "nt_dmpnn_tile_stride", "nt_dmpnn_row_table", "nt_dmpnn_pack_weight_fk", "nt_dmpnn_tile_plan_hubs",
@@ -48,7 +48,7 @@ def test_abi_version_and_errors_without_gpu():
     from notorch_amd import _lib
 
     lib = _lib.load()
-    assert lib.nt_abi_version() == _lib.ABI_VERSION == 7
+    assert lib.nt_abi_version() == _lib.ABI_VERSION == 8
     assert lib.nt_last_kernel() == b""  # no layer call yet on this thread
     assert lib.nt_dmpnn_packed_weight_bytes(300, 0) > 0
     assert lib.nt_dmpnn_packed_weight_bytes(0, 0) == 0

@@ -219,8 +219,8 @@ def test_fused_kernel_variants_and_no_spin_timeouts(variant, monkeypatch):
     from notorch_amd import _lib
 
     K = _K()
-    if variant == "ps" and not _lib.DIAG:
-        pytest.skip("the ps kernel is an A/B variant: diagnostic library only (NT_LIB=diag)")
+    if not _lib.DIAG:
+        pytest.skip("the pk / ps ring kernels are A/B variants: diagnostic library only (NT_LIB=diag)")
     monkeypatch.setenv("NT_FUSED_KERNEL", variant)
     lib = _lib.load()
     fn = lib.nt_debug_pk_timeouts
@@ -291,40 +291,6 @@ def test_forward_on_a_non_current_device():
             b = blk.to(dev)
             outs.append(b(G.update(node_feats=Xv, edge_feats=Xe).to(dev)).edge_feats.cpu())
     assert torch.equal(outs[0], outs[1])
-
-
-def test_device_status_word_raises_on_next_forward():
-    """A set status word (what a give-up of a bounded ring wait leaves) makes the next forward
-    raise DeviceStatusError, and the synchronous check raises too; a reset clears both."""
-    import ctypes
-
-    from notorch_amd import _lib
-    from notorch_amd import kernels as K
-    from notorch_amd.nn import ChempropBlock
-
-    lib = _lib.load()
-    fn = lib.nt_debug_pk_timeouts
-    fn.argtypes = [ctypes.POINTER(ctypes.c_uint), ctypes.c_int]
-    cnt = ctypes.c_uint(0)
-    G = _graph("qm9", 32, seed=3)
-    torch.manual_seed(0)
-    Gd = G.update(node_feats=torch.randn(G.num_nodes, 64), edge_feats=torch.randn(G.num_edges, 64)).to(DEV)
-    blk = ChempropBlock(hidden_dim=64, depth=2).eval().to(DEV)
-    with torch.no_grad():
-        blk(Gd)
-        torch.cuda.synchronize()
-        K.check_device_status()
-        assert fn(ctypes.byref(cnt), 2) == 0  # simulate a give-up
-        with pytest.raises(K.DeviceStatusError):
-            for _ in range(K.STATUS_EVERY + 2):  # the periodic copy picks the word up
-                blk(Gd)
-                torch.cuda.synchronize()
-        with pytest.raises(K.DeviceStatusError):
-            K.check_device_status()
-        K.reset_device_status()
-        blk(Gd)
-        blk(Gd)
-    K.check_device_status()
 
 
 def _n_for_tiles(pred, lo, hi, step=1):
