@@ -89,6 +89,9 @@ NT_API int nt_embed_bag(const void* table, int64_t num_types, const int64_t* idx
  * amax_out (fp32 only, may be NULL): 2 device floats, atomically raised to max|H0| and max|S| (the
  * caller zero-fills them); the fp32 layer kernel scales its fp16 split by them.  ld_out (ABI 7): row
  * pitch in elements of H0 and S (0 = h; > h: fp32 with S, 7 + 2 type columns, as nt_dmpnn_init's).
+ * records (ABI 8, may be NULL): nt_embed_edge_records of this graph; with it (fp32, S given, 7 + 2
+ * type columns, h % 4 == 0, (num_node_types + num_edge_types + 2) * h * 4 <= 72 KiB) the init runs one
+ * wave per node over the records with both tables in LDS (the same bits).
  */
 NT_API int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_types,
                                const int64_t* node_types, int64_t kv, const void* edge_table,
@@ -96,7 +99,18 @@ NT_API int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_types,
                                const int64_t* src, const int32_t* seg_ptr, const int32_t* perm,
                                int64_t V, int64_t E, int64_t h, int act, float act_alpha, int reduce,
                                int dtype, void* H0, void* S, float* amax_out, int64_t ld_out,
-                               void* stream);
+                               const void* records, void* stream);
+
+/*
+ * Type records of a graph for nt_dmpnn_init_embed (ABI 8; no reference counterpart: a layout of the
+ * reference's node_feats / edge_feats type columns, transforms/graph.py:32-43): per position p of the
+ * dst CSR (perm), 16 B {e = perm[p], node_types[src e][0..6] and edge_types[e][0..1] as bytes}; an
+ * out-of-range index is stored as 255 (a zero row).  node_types V x 7, edge_types E x 2 (int64),
+ * fewer than 255 types of each kind; records: E x 16 B, 16-B aligned.
+ */
+NT_API int nt_embed_edge_records(const int64_t* node_types, int64_t num_node_types, const int64_t* edge_types,
+                                 int64_t num_edge_types, const int64_t* src, const int32_t* perm, int64_t V,
+                                 int64_t E, void* records, void* stream);
 
 /*
  * Host-side collate of B per-molecule graphs (BatchedGraph.from_graphs, notorch/data/models/

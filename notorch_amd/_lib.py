@@ -56,8 +56,9 @@ SIGNATURES: dict[str, tuple] = {
     "nt_dmpnn_init_embed": (
         _c_int,
         [_vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _c_i64, _vp, _vp, _vp, _c_i64, _c_i64, _c_i64,
-         _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp, _c_i64, _vp],
+         _c_int, _c_f32, _c_int, _c_int, _vp, _vp, _vp, _c_i64, _vp, _vp],
     ),
+    "nt_embed_edge_records": (_c_int, [_vp, _c_i64, _vp, _c_i64, _vp, _vp, _c_i64, _c_i64, _vp, _vp]),
     "nt_collate_graphs": (
         _c_int,
         [_c_i64, _vp, _vp, _c_i64, _vp, _vp, _c_i64, _vp, _vp, _c_int, _vp, _vp, _vp, _vp, _vp, _vp,

@@ -234,6 +234,162 @@ __global__ void __launch_bounds__(256) init_embed_only(EmbedArgs a, const int64_
   }
 }
 
+// ---------------------------------------------------------------------- type records + wave init
+// Per dst-sorted position p of the dst CSR, one 16-B record of the in-edge e = perm[p] with both bags'
+// type indices as bytes (nt_embed_edge_records): {e, vt0..3, vt4..6 | et0 << 24, et1}, where vt are
+// node_types[src e][0..6] and et edge_types[e][0..1]; an out-of-range index is stored as 255, which the
+// init maps to a zero table row.  Built once per graph (7 + 2 type columns, < 255 types of each kind),
+// it turns the init's dependent chain perm -> src -> 9 type loads into one load per in-edge.
+__global__ void __launch_bounds__(256) edge_records_kernel(const int64_t* __restrict__ vtypes, int64_t nv,
+                                                           const int64_t* __restrict__ etypes, int64_t ne,
+                                                           const int64_t* __restrict__ src,
+                                                           const int32_t* __restrict__ perm, int64_t V,
+                                                           int64_t E, int4* __restrict__ out) {
+  for (int64_t p = blockIdx.x * 256LL + threadIdx.x; p < E; p += (int64_t)gridDim.x * 256) {
+    const int e = perm[p];
+    const int64_t sv = src[e];
+    const bool sok = sv >= 0 && sv < V;
+    unsigned b[9];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      const int64_t t = sok ? vtypes[sv * 7 + q] : -1;
+      b[q] = (t >= 0 && t < nv) ? (unsigned)t : 255u;
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int64_t t = etypes[(int64_t)e * 2 + q];
+      b[7 + q] = (t >= 0 && t < ne) ? (unsigned)t : 255u;
+    }
+    out[p] = int4{e, (int)(b[0] | b[1] << 8 | b[2] << 16 | b[3] << 24),
+                  (int)(b[4] | b[5] << 8 | b[6] << 16 | b[7] << 24), (int)b[8]};
+  }
+}
+
+// One wave per node with both tables (plus a zero row each) in LDS: the node's range and its in-edge
+// records are wave-uniform (scalar loads), 4 in-edges at a time; lane l takes row pieces l + 64 q, q <
+// PPL (pieces past the row read piece 0 and are masked at the stores).  Same sums in the same order
+// as init_embed_aggregate_k (each bag from +0.0 in ascending column, then xv + xe): the same bits.
+constexpr int kWaveThreads = 512;  // 8 waves; two workgroups per CU (<= 128 VGPRs, 2 x 72 KiB LDS)
+template <int R, int ACT, int PPL>
+__global__ void __launch_bounds__(kWaveThreads, 2) init_embed_wave(
+    const float* __restrict__ Tv_g, int64_t nv, const float* __restrict__ Te_g, int64_t ne,
+    const int4* __restrict__ rec, const int32_t* __restrict__ seg_ptr, int64_t V, int64_t h, int act,
+    float alpha, float4* __restrict__ H0, float4* __restrict__ S, float* __restrict__ amax, int64_t lo) {
+  __shared__ uint4 tab[kTabB / 16];
+  const int64_t hq = h / 4;  // 16-B pieces per row
+  const int64_t nvq = nv * hq, neq = ne * hq;
+  // [node table | zero row | edge table | zero row]
+  for (int64_t i = threadIdx.x; i < nvq + neq + 2 * hq; i += blockDim.x) {
+    uint4 x = uint4{0u, 0u, 0u, 0u};
+    if (i < nvq) x = reinterpret_cast<const uint4*>(Tv_g)[i];
+    else if (i >= nvq + hq && i < nvq + hq + neq) x = reinterpret_cast<const uint4*>(Te_g)[i - nvq - hq];
+    tab[i] = x;
+  }
+  __syncthreads();
+  const float4* Tv = reinterpret_cast<const float4*>(tab);
+  const float4* Te = Tv + nvq + hq;
+  const unsigned zv = (unsigned)nv, ze = (unsigned)ne;  // zero rows
+  const int lane = threadIdx.x & 63;
+  float mh = 0.f, ms = 0.f;
+  int64_t cc[PPL];
+  bool ok[PPL];
+#pragma unroll
+  for (int q = 0; q < PPL; ++q) {
+    const int64_t c = lane + 64 * q;
+    ok[q] = c < hq;
+    cc[q] = ok[q] ? c : 0;
+  }
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t v = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)));
+       v < V; v += nwaves) {
+    const int32_t b = seg_ptr[v], en = seg_ptr[v + 1];
+    Reducer4<R> r[PPL];
+#pragma unroll
+    for (int q = 0; q < PPL; ++q) r[q].init();
+    for (int32_t j = b; j < en; j += 4) {
+      const int n = min(4, en - j);
+      int4 rc[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) rc[u] = u < n ? rec[j + u] : int4{0, 0, 0, 0};
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (u >= n) break;
+        const unsigned w1 = (unsigned)rc[u].y, w2 = (unsigned)rc[u].z, w3 = (unsigned)rc[u].w;
+        unsigned t[9] = {w1 & 255u, (w1 >> 8) & 255u, (w1 >> 16) & 255u, w1 >> 24,
+                         w2 & 255u, (w2 >> 8) & 255u, (w2 >> 16) & 255u, w2 >> 24, w3 & 255u};
+#pragma unroll
+        for (int i = 0; i < 7; ++i) t[i] = t[i] < zv ? t[i] : zv;
+#pragma unroll
+        for (int i = 7; i < 9; ++i) t[i] = t[i] < ze ? t[i] : ze;
+#pragma unroll
+        for (int q = 0; q < PPL; ++q) {
+          float4 xv = make_float4(0.f, 0.f, 0.f, 0.f), xe = xv;
+#pragma unroll
+          for (int i = 0; i < 7; ++i) xv = xv + Tv[t[i] * hq + cc[q]];
+#pragma unroll
+          for (int i = 7; i < 9; ++i) xe = xe + Te[t[i] * hq + cc[q]];
+          const float4 h0 = xv + xe;
+          if (ok[q]) {
+            H0[(int64_t)rc[u].x * lo + cc[q]] = h0;
+            mh = fmaxf(mh, fmaxf(fmaxf(fabsf(h0.x), fabsf(h0.y)), fmaxf(fabsf(h0.z), fabsf(h0.w))));
+          }
+          r[q].push(act4_t<ACT>(h0, act, alpha));
+        }
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < PPL; ++q) {
+      if (ok[q]) {
+        const float4 y = r[q].result();
+        S[v * lo + cc[q]] = y;
+        ms = fmaxf(ms, fmaxf(fmaxf(fabsf(y.x), fabsf(y.y)), fmaxf(fabsf(y.z), fabsf(y.w))));
+      }
+    }
+  }
+  if (amax) block_max_to(amax, mh, ms, true);  // one atomic max per block
+}
+
+// the wave init over records (fp32, 7 + 2 type columns, both tables + zero rows in LDS, h <= 256 PPL)
+int launch_init_embed_wave(const EmbedArgs& a, const int4* rec, const int32_t* seg_ptr, int64_t V, int64_t h,
+                           int act, float alpha, int reduce, float* H0, float* S, float* amax, int64_t lo,
+                           hipStream_t stream) {
+  const int grid = (int)std::min<int64_t>((V + kWaveThreads / 64 - 1) / (kWaveThreads / 64), 2 * (int64_t)cu_count());
+  const int64_t hq = h / 4;
+#define NT_IEW(R_, A_, P_)                                                                                  \
+  init_embed_wave<R_, A_, P_><<<grid, kWaveThreads, 0, stream>>>((const float*)a.Tv, a.nv, (const float*)a.Te, \
+                                                                 a.ne, rec, seg_ptr, V, h, act, alpha,       \
+                                                                 (float4*)H0, (float4*)S, amax, lo / 4)
+#define NT_IEW_P(R_, A_)              \
+  do {                                \
+    if (hq <= 64) NT_IEW(R_, A_, 1);  \
+    else NT_IEW(R_, A_, 2);           \
+  } while (0)
+#define NT_IEW_A(R_)                                                   \
+  do {                                                                 \
+    if (act == NT_ACT_IDENTITY) NT_IEW_P(R_, NT_ACT_IDENTITY);         \
+    else if (act == NT_ACT_RELU) NT_IEW_P(R_, NT_ACT_RELU);            \
+    else NT_IEW_P(R_, -1);                                             \
+  } while (0)
+  switch (reduce) {
+    case NT_SUM: NT_IEW_A(NT_SUM); break;
+    case NT_MEAN: NT_IEW_A(NT_MEAN); break;
+    case NT_MAX: NT_IEW_A(NT_MAX); break;
+    default: NT_IEW_A(NT_MIN); break;
+  }
+#undef NT_IEW_A
+#undef NT_IEW_P
+#undef NT_IEW
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
+// the record path applies: fp32 rows of whole 16-B pieces, h <= 512, 7 + 2 type columns, both tables
+// plus their zero rows in kTabB of LDS
+bool wave_embed_ok(const EmbedArgs& a, int64_t h) {
+  return a.kv == 7 && a.ke == 2 && h % 4 == 0 && h <= 512 && a.nv < 255 && a.ne < 255 &&
+         (a.nv + a.ne + 2) * h * 4 <= kTabB;
+}
+
 template <typename T, bool VEC>
 int launch_init_embed(const EmbedArgs& a, const int64_t* src, const int32_t* seg_ptr,
                       const int32_t* perm, int64_t V, int64_t E, int64_t h, int act, float alpha,
@@ -324,13 +480,32 @@ extern "C" int nt_embed_bag(const void* table, int64_t num_types, const int64_t*
   return NT_OK;
 }
 
+extern "C" int nt_embed_edge_records(const int64_t* node_types, int64_t num_node_types,
+                                     const int64_t* edge_types, int64_t num_edge_types, const int64_t* src,
+                                     const int32_t* perm, int64_t V, int64_t E, void* records,
+                                     void* stream_) {
+  using namespace nt;
+  clear_error();
+  NT_REQUIRE(V >= 0 && E >= 0 && E < (int64_t(1) << 31), NT_EINVAL, "bad sizes");
+  NT_REQUIRE(num_node_types >= 0 && num_node_types < 255 && num_edge_types >= 0 && num_edge_types < 255,
+             NT_EUNSUPPORTED, "type records hold fewer than 255 types of each kind");
+  if (E == 0) return NT_OK;
+  NT_REQUIRE(node_types && edge_types && src && perm && records, NT_EINVAL, "NULL pointer");
+  NT_REQUIRE(aligned16(records), NT_EINVAL, "records must be 16-B aligned");
+  hipStream_t stream = as_stream(stream_);
+  edge_records_kernel<<<grid_for(E, 256), 256, 0, stream>>>(node_types, num_node_types, edge_types, num_edge_types,
+                                                            src, perm, V, E, (int4*)records);
+  NT_LAUNCH_CHECK();
+  return NT_OK;
+}
+
 extern "C" int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_types,
                                    const int64_t* node_types, int64_t kv, const void* edge_table,
                                    int64_t num_edge_types, const int64_t* edge_types, int64_t ke,
                                    const int64_t* src, const int32_t* seg_ptr, const int32_t* perm,
                                    int64_t V, int64_t E, int64_t h, int act, float act_alpha,
                                    int reduce, int dtype, void* H0, void* S, float* amax_out,
-                                   int64_t ld_out, void* stream_) {
+                                   int64_t ld_out, const void* records, void* stream_) {
   using namespace nt;
   clear_error();
   NT_REQUIRE(dtype == NT_F32 || dtype == NT_BF16, NT_EUNSUPPORTED, "dtype must be NT_F32 or NT_BF16");
@@ -351,6 +526,13 @@ extern "C" int nt_dmpnn_init_embed(const void* node_table, int64_t num_node_type
                     edge_table, num_edge_types, edge_types, ke};
   const bool al = aligned16(node_table) && aligned16(edge_table) && aligned16(H0) &&
                   (S == nullptr || aligned16(S));
+  if (records != nullptr) {
+    NT_REQUIRE(dtype == NT_F32 && S != nullptr && al && wave_embed_ok(a, h) && aligned16(records), NT_EUNSUPPORTED,
+               "records: fp32 with S, 16-B aligned rows, 7 + 2 type columns, h % 4 == 0, tables in LDS");
+    if (V == 0) return NT_OK;
+    return launch_init_embed_wave(a, (const int4*)records, seg_ptr, V, h, act, act_alpha, reduce, (float*)H0,
+                                  (float*)S, amax_out, ld_out, stream);
+  }
   if (dtype == NT_F32) {
     if (h % 4 == 0 && al)
       return launch_init_embed<float, true>(a, src, seg_ptr, perm, V, E, h, act, act_alpha, reduce, H0, S,

@@ -67,6 +67,8 @@ class DeviceLayout:
     bwd: object = None
     # the fp32 layer kernel's row table (key, rev_index, E x 4 int32), built lazily by _engine.row_table
     row_table: object = None
+    # the fused embedding init's type records (key, E x 4 int32), built lazily by _engine.embed_records
+    embed_records: object = None
     # host-computed statistics the collate ships with the CSR, so a fresh batch needs no
     # device -> host sync: (max, min) in-degree, largest molecule, (min, max) type index of the
     # node / edge feature columns when they are integer type matrices
@@ -530,6 +532,7 @@ CHUNK_ROWS = 32  # rows per chunk of nt_segment_reduce_chunked
 
 
 PLAN_NCU = 256  # kernels.PLAN_NCU: the CU count the balanced plans are cut for
+PLAN_SLOTS64 = PLAN_NCU  # kernels.PLAN_SLOTS64 (64-row plans)
 WIDE_TILE_ROWS = 128  # rows of the diagnostic build's update_fk_kernel tiles (the shipping kernels: 64)
 
 
@@ -625,7 +628,7 @@ def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional
         lay.hubs = (torch.from_numpy(ids), int(ids.size), int(rest.max()) if rest.size else 0)
         hub, maxdeg = HUB_CUT_DEGREE, lay.hubs[2]
     if E > 0 and V > 0:
-        tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg, rows=64, ncu=PLAN_NCU, hub_degree=hub)
+        tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg, rows=64, ncu=PLAN_SLOTS64, hub_degree=hub)
         lay.plan = (tile_ptr, ntiles, dsts, mindeg == 0)
         lay.plan_wide = host_tile_ptr(dst_ptr, E, host_tile_stride(E, maxdeg, WIDE_TILE_ROWS, PLAN_NCU), hub,
                                       WIDE_TILE_ROWS)

@@ -37,6 +37,7 @@ __all__ = [
     "gather_rows",
     "embed_bag",
     "dmpnn_init_embed",
+    "embed_edge_records",
     "node_scores",
     "softmax_pool",
     "dense_matmul",
@@ -548,6 +549,11 @@ def fused_supported(V: int, E: int, h: int, dtype: torch.dtype = torch.float32) 
 
 
 PLAN_NCU = 256  # CUs the balanced tile plans are cut for (MI355X; host and device plans agree)
+# slots the 64-row plans are balanced over.  Their kernels run two workgroups per CU, but balancing
+# for 512 workgroups (~51-row tiles) measured slower than for the 256 CUs (~61 rows, whose tile count
+# leaves some workgroups one tile short): config 2 layer 118-119 vs 107-110 us, config 3 233-235 vs
+# 228 us, training 1.545 vs 1.478-1.495 ms (tools/r6_slots.sh, profiles/r6/slots_ab.txt)
+PLAN_SLOTS64 = PLAN_NCU
 
 
 def fused_tile_rows(h: int, dtype: torch.dtype, act: tuple[int, float] = (_lib.NT_ACT_RELU, 0.0),
@@ -1067,11 +1073,14 @@ def dmpnn_init_embed(
     validate: bool = True,
     amax: Tensor | None = None,
     pitch: int | None = None,
+    records: Tensor | None = None,
 ) -> tuple[Tensor, Tensor | None]:
     """H0 = Xv[src] + Xe with Xv = EmbeddingBag(node_table)(node_types), Xe likewise, never
     materialised; optionally fused with S = scatter(act(H0), dst) (needs the dst CSR).
-    amax (fp32, 2 zero-filled device floats): raised to max|H0|, max|S|."""
-    dev = _require_device(node_table, node_types, edge_table, edge_types, src, seg_ptr, perm, amax)
+    amax (fp32, 2 zero-filled device floats): raised to max|H0|, max|S|.
+    records: embed_edge_records of this graph (fp32 with S, 7 + 2 type columns): the wave-per-node
+    init over them (same bits)."""
+    dev = _require_device(node_table, node_types, edge_table, edge_types, src, seg_ptr, perm, amax, records)
     _require_amax(amax, node_table.dtype)
     code = _require_feat("node_table", node_table)
     _require_feat("edge_table", edge_table, node_table.dtype)
@@ -1086,6 +1095,8 @@ def dmpnn_init_embed(
     h = node_table.shape[1]
     if src.numel() != E:
         raise ValueError("src must have one entry per edge")
+    if records is not None and (records.dtype != torch.int32 or records.shape != (E, 4) or not records.is_contiguous()):
+        raise ValueError("records must be the (E, 4) int32 embed_edge_records of this graph")
     ld = h if pitch is None else int(pitch)  # row-padded H0 / S views (as dmpnn_init's pitch)
     H0 = padded_rows(E, h, ld, node_table.dtype, dev)
     S = None if seg_ptr is None else padded_rows(V, h, ld, node_table.dtype, dev)
@@ -1093,8 +1104,28 @@ def dmpnn_init_embed(
          _ptr(node_table), node_table.shape[0], _ptr(node_types), kv, _ptr(edge_table),
          edge_table.shape[0], _ptr(edge_types), ke, _ptr(src), _ptr(seg_ptr), _ptr(perm), V, E, h,
          act[0], act[1], reduce_code(reduce), code, _ptr(H0), _ptr(S), _ptr(amax), 0 if ld == h else ld,
-         _stream(dev))
+         _ptr(records), _stream(dev))
     return H0, S
+
+
+def embed_edge_records(node_types: Tensor, num_node_types: int, edge_types: Tensor, num_edge_types: int,
+                       src: Tensor, perm: Tensor) -> Tensor:
+    """(E, 4) int32 type records of a graph for dmpnn_init_embed (nt_embed_edge_records): per position of
+    the dst CSR permutation, the in-edge and its 7 node-type and 2 edge-type indices as bytes (255 =
+    out of range).  Build once per graph."""
+    dev = _require_device(node_types, edge_types, src, perm)
+    _require_i64("node_types", node_types)
+    _require_i64("edge_types", edge_types)
+    _require_i64("src", src)
+    if node_types.dim() != 2 or node_types.shape[1] != 7 or edge_types.dim() != 2 or edge_types.shape[1] != 2:
+        raise ValueError("type records need 7 node-type and 2 edge-type columns")
+    V, E = node_types.shape[0], edge_types.shape[0]
+    if perm.dtype != torch.int32 or perm.numel() != E or src.numel() != E:
+        raise ValueError("perm (int32) and src need one entry per edge")
+    out = torch.empty(max(E, 1), 4, dtype=torch.int32, device=dev)[:E]
+    _run(dev, _lib.load().nt_embed_edge_records, _ptr(node_types.contiguous()), int(num_node_types),
+         _ptr(edge_types.contiguous()), int(num_edge_types), _ptr(src), _ptr(perm), V, E, _ptr(out), _stream(dev))
+    return out
 
 
 # ------------------------------------------------------------------------------------ attention readouts

@@ -2,15 +2,17 @@
 autograd wrapper.
 
 Forward (per call, all on ``torch.cuda.current_stream()``, inputs already resident).  Fused path
-(every node's in-degree <= 32 and h % 4 == 0, h <= 304 — molecules):
+(every node's in-degree <= 32 and h % 4 == 0 — molecules; hub graphs cut their hubs into sub-runs):
 
     nt_dmpnn_init         H0 = Xv[src] + Xe  fused with  S = scatter(act(H0), dst)  chemprop.py:82-83,37-39
+      (GraphEmbedding models: nt_dmpnn_init_embed from the type indices, over the graph's type records)
     for l in 0..d-1:
       nt_dmpnn_update_fused  H_{l+1} = H_l + W_l (S[src] - act(H_l)[rev]) + b_l      chemprop.py:40-41, residual.py:28
                              S = scatter(act(H_{l+1}), dst)   (last layer: node = scatter(H_d, dst),
                                                                chemprop.py:86)
 
-d + 1 launches (+ one nt_dmpnn_pack_weight per distinct weight, cached).  Otherwise (hubs, other h):
+d + 1 launches (+ one nt_dmpnn_pack_weights_fk launch pair per new set of weights).  Otherwise
+(dropout, or no fused plan):
 
     nt_dmpnn_init; for l: nt_dmpnn_update, nt_segment_reduce; nt_segment_reduce (node)   2 + 2d launches
 
@@ -20,18 +22,18 @@ kernel code, or layers that differ in activation / dropout, run layer by layer
 (block_forward_layerwise).
 
 Backward (training): the forward keeps (H_l, S_l) of every layer; per layer,
-last to first (csrc/backward.hip):
+last to first (csrc/backward.hip, csrc/wgrad.hip):
 
-    nt_dmpnn_weight_grad    dW_l = G^T A_l, db_l = colsum(G), A_l = S_l[src] - act(H_l)[rev] formed
-                            while staging (fp32: split-K bf16x6 MFMA; bf16: nt_dmpnn_message + a
-                            split-K library GEMM)
-    nt_dmpnn_dense_matmul   dA = G W_l                 (fp32: the bf16x6 MFMA kernel; bf16: library)
-    nt_segment_reduce       dS = scatter_sum(dA, src)            (src CSR, cached on the layout)
-    nt_dmpnn_edge_backward  G <- G + act'(H_l) * (dS[dst] / c - scatter_sum(dA, rev))  (rev CSR)
-      (max / min, fp32: nt_segment_arg + nt_dmpnn_edge_backward_arg: dS[dst] reaches only the arg)
+    nt_dmpnn_weight_grad_fk  dW_l = G^T A_l, db_l = colsum(G), A_l = S_l[src] - act(H_l)[rev] formed
+                             while staging (fp32 h <= 320: the two-part fp16 split; above it
+                             nt_dmpnn_weight_grad's bf16x6; bf16: the bf16 weight-grad kernel)
+    nt_dmpnn_update_fused    dA = G W_l and dS = scatter_sum(dA, src) in ONE launch of the layer kernel
+                             over the src-sorted plan (dA_plan; nt_dmpnn_dense_matmul + nt_segment_reduce
+                             where the plan does not apply; bf16: the bf16 layer kernel's dense mode)
+    nt_dmpnn_edge_backward   G <- G + act'(H_l) * (dS[dst] / c - scatter_sum(dA, rev))  (rev CSR)
+      (max / min: nt_segment_arg + nt_dmpnn_edge_backward_arg, fp32 and bf16: dS[dst] reaches only the arg)
 
-then dXe = G, dXv = scatter_sum(G, src).  bf16 max / min recompute the block in PyTorch device ops
-and run autograd (``_torch_block``).
+then dXe = G, dXv = scatter_sum(G, src).
 """
 from __future__ import annotations
 
@@ -228,7 +230,7 @@ def fused_plan(lay: DeviceLayout, V: int, E: int, rows: int = 64, dtype: torch.d
         if E > 0 and V > 0:
             mx, mindeg = _degree_range(lay)
             tile_ptr, ntiles, dsts = K.tile_plan(lay.dst_ptr, E, mx if maxdeg is None else maxdeg, rows=64,
-                                                 ncu=K.PLAN_NCU, hub_degree=hub)
+                                                 ncu=K.PLAN_SLOTS64, hub_degree=hub)
             plan = (tile_ptr, ntiles, dsts, mindeg == 0)
         lay.plan = plan
     if not lay.plan:
@@ -497,9 +499,13 @@ def block_forward_embedded(
     amax = _amax_buffer(len(weights), node_table, reuse=True)
     k72 = node_types.dim() == 2 and node_types.shape[1] == 7 and edge_types.dim() == 2 and edge_types.shape[1] == 2
     pitch = row_pitch(node_table.shape[1], node_table.dtype) if k72 else None
+    rec = None
+    if k72 and node_table.dtype == torch.float32 and embed_wave_ok(node_table.shape[0], edge_table.shape[0],
+                                                                   node_table.shape[1]):
+        rec = embed_records(lay, node_types, node_table.shape[0], edge_types, edge_table.shape[0], src)
     H, S = K.dmpnn_init_embed(node_table, node_types, edge_table, edge_types, src, lay.dst_ptr,
                               lay.dst_perm, act=act, reduce=reduce, validate=validate,
-                              amax=None if amax is None else amax[0], pitch=pitch)
+                              amax=None if amax is None else amax[0], pitch=pitch, records=rec)
     node, H, _ = _layers_forward(H, S, V, src, rev, lay, weights, biases, act, reduce, residual, False,
                                  amax=amax)
     return node, H
@@ -585,6 +591,27 @@ def row_table(lay: DeviceLayout, dsts: Tensor, src: Tensor, rev: Tensor, V: int)
         hit = (key, rev, rt)
         lay.row_table = hit
     return hit[2]
+
+
+EMBED_TABLE_BYTES = 72 * 1024  # LDS the wave-per-node embedding init holds the two tables in (embed.hip kTabB)
+
+
+def embed_wave_ok(nv: int, ne: int, h: int) -> bool:
+    """The wave-per-node fused embedding init applies (fp32, 7 + 2 type columns checked by the caller):
+    both tables plus a zero row each fit its LDS, fewer than 255 types of each kind."""
+    return h % 4 == 0 and h <= 512 and nv < 255 and ne < 255 and (nv + ne + 2) * h * 4 <= EMBED_TABLE_BYTES
+
+
+def embed_records(lay: DeviceLayout, node_types: Tensor, nv: int, edge_types: Tensor, ne: int, src: Tensor) -> Tensor:
+    """The graph's type records for the wave-per-node embedding init (kernels.embed_edge_records),
+    cached on the layout, keyed on the type tensors (identity and version) and src."""
+    key = (node_types.data_ptr(), node_types._version, edge_types.data_ptr(), edge_types._version,
+           src.data_ptr(), src.numel(), nv, ne)
+    hit = getattr(lay, "embed_records", None)
+    if hit is None or hit[0] != key:
+        hit = (key, K.embed_edge_records(node_types, nv, edge_types, ne, src, lay.dst_perm))
+        lay.embed_records = hit
+    return hit[1]
 
 
 def hub_run_table(lay: DeviceLayout, rt: Tensor, tile_ptr: Tensor, dsts: Tensor, run_rows: int) -> tuple:
@@ -796,7 +823,7 @@ def dA_plan(lay: DeviceLayout, src: Tensor, V: int, E: int, src_ptr: Tensor, src
             outdeg = src_ptr[1:] - src_ptr[:-1]
             dmax, dmin = int(outdeg.max()), int(outdeg.min())
             if dmax <= MAX_FUSED_IN_DEGREE:
-                tile_ptr, ntiles, dsts = K.tile_plan(src_ptr, E, dmax, rows=64, ncu=K.PLAN_NCU)
+                tile_ptr, ntiles, dsts = K.tile_plan(src_ptr, E, dmax, rows=64, ncu=K.PLAN_SLOTS64)
                 ident = torch.arange(E, dtype=torch.int64, device=src.device)
                 none = torch.full((E,), -1, dtype=torch.int64, device=src.device)
                 # the gathered operand is G (E rows): the row table's bound on the "src" index is E

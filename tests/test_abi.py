@@ -22,7 +22,7 @@ def test_header_declares_the_boundary():
         "nt_dmpnn_init", "nt_segment_reduce", "nt_dmpnn_aggregate", "nt_dmpnn_packed_weight_bytes",
         "nt_dmpnn_pack_weight", "nt_dmpnn_pack_weights_fk", "nt_dmpnn_update", "nt_dmpnn_tile_count", "nt_dmpnn_tile_plan",
         "nt_dmpnn_update_fused", "nt_dmpnn_message", "nt_dmpnn_edge_backward", "nt_gather_rows",
-        "nt_embed_bag", "nt_dmpnn_init_embed", "nt_node_scores", "nt_softmax_pool",
+        "nt_embed_bag", "nt_dmpnn_init_embed", "nt_embed_edge_records", "nt_node_scores", "nt_softmax_pool",
         "nt_collate_graphs", "nt_segment_reduce_chunked",
         "nt_dmpnn_dense_matmul", "nt_dmpnn_weight_grad", "nt_dmpnn_weight_grad_workspace", "nt_segment_arg",
         "nt_dmpnn_edge_backward_arg", "nt_gather_rows_arg", "nt_absmax", "nt_dmpnn_fused_tile_rows",

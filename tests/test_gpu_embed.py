@@ -93,6 +93,47 @@ def test_init_embed_padded_rows_bit_identical(h):
     assert torch.equal(H0p, H0) and torch.equal(Sp, S) and torch.equal(am0, am1)
 
 
+@pytest.mark.parametrize("h,n,kind", [(300, 4096, "qm9"), (300, 37, "qm9"), (64, 500, "zinc"), (512, 64, "qm9"),
+                                      (4, 40, "qm9")])
+def test_init_embed_records_bit_identical(h, n, kind):
+    """The wave-per-node init over the type records (ABI 8 nt_embed_edge_records) gives the bits of the
+    thread-per-piece init: every reduce, relu / identity, padded rows, the amax chain; an out-of-range
+    type index contributes a zero row in both."""
+    from notorch_amd import kernels as K
+
+    G = _graph(kind, n, seed=9)
+    torch.manual_seed(4)
+    Tv, Te = torch.randn(42, h, device=DEV), torch.randn(13, h, device=DEV)
+    nt, et = G.node_feats.to(DEV), G.edge_feats.to(DEV)
+    src, dst = G.edge_index[0].to(DEV), G.edge_index[1].to(DEV)
+    seg_ptr, perm = K.csr_build(dst, G.num_nodes)
+    rec = K.embed_edge_records(nt, 42, et, 13, src, perm)
+    assert rec.shape == (G.num_edges, 4) and torch.equal(rec[:, 0].long(), perm.long())
+    if (42 + 13 + 2) * h * 4 > 72 * 1024:  # the tables do not fit the wave init's LDS: refused
+        with pytest.raises(RuntimeError, match="records"):
+            K.dmpnn_init_embed(Tv, nt, Te, et, src, seg_ptr, perm, records=rec)
+        return
+    relu = K.act_code(torch.nn.ReLU())
+    ident = K.act_code(torch.nn.Identity())
+    pitch = (h + 7) // 8 * 8 if h % 8 else h + 8
+    for act in (relu, ident):
+        for reduce in ("sum", "mean", "max", "min"):
+            for ld in (None, pitch):
+                am0, am1 = torch.zeros(2, device=DEV), torch.zeros(2, device=DEV)
+                H0, S = K.dmpnn_init_embed(Tv, nt, Te, et, src, seg_ptr, perm, act=act, reduce=reduce, amax=am0,
+                                           pitch=ld)
+                H0r, Sr = K.dmpnn_init_embed(Tv, nt, Te, et, src, seg_ptr, perm, act=act, reduce=reduce, amax=am1,
+                                             pitch=ld, records=rec)
+                assert torch.equal(H0r, H0) and torch.equal(Sr, S) and torch.equal(am1, am0), (act, reduce, ld)
+    # out-of-range indices (validate=False): both paths add a zero row for them
+    bad = nt.clone()
+    bad[::7, 3] = 99
+    rec_bad = K.embed_edge_records(bad, 42, et, 13, src, perm)
+    H0, S = K.dmpnn_init_embed(Tv, bad, Te, et, src, seg_ptr, perm, validate=False)
+    H0r, Sr = K.dmpnn_init_embed(Tv, bad, Te, et, src, seg_ptr, perm, validate=False, records=rec_bad)
+    assert torch.equal(H0r, H0) and torch.equal(Sr, S)
+
+
 def _modules(h, depth, dtype=torch.float32, **opts):
     from notorch_amd.nn import ChempropBlock, EmbeddedChempropBlock, GraphEmbedding
 

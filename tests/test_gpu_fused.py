@@ -261,7 +261,7 @@ def test_host_plans_equal_device_planners():
         lay = G._nt_layout
         tile_ptr, ntiles, dsts, _ = lay.plan
         d_tile_ptr, d_ntiles, d_dsts = K.tile_plan(lay.dst_ptr.to(DEV), G.num_edges, lay.deg_range[0], rows=64,
-                                                   ncu=K.PLAN_NCU)
+                                                   ncu=K.PLAN_SLOTS64)
         assert d_ntiles == ntiles
         assert torch.equal(d_tile_ptr.cpu(), tile_ptr) and torch.equal(d_dsts.cpu(), dsts)
     P = make_batch("polymer", 2, seed=2).collate("nodes")
