@@ -27,7 +27,23 @@ endif
 OBJS    := $(patsubst $(SRC_DIR)/%.hip,$(BDIR)/%.o,$(SRCS))
 DIAG_OBJS := $(filter $(BDIR)/diag/%,$(OBJS))
 
+# host-only CPython helper of the native collate (csrc/host/collate_py.cpp): g++ against torch's headers
+PY      ?= python3
+PYEXT   := notorch_amd/lib/_collate_py$(shell $(PY) -c "import sysconfig; print(sysconfig.get_config_var('EXT_SUFFIX'))")
+TORCH_FLAGS = $(shell $(PY) -c "import sysconfig, os, torch, torch.utils.cpp_extension as c; \
+  print(' '.join('-I' + p for p in c.include_paths()), '-I' + sysconfig.get_paths()['include'], \
+  '-D_GLIBCXX_USE_CXX11_ABI=%d' % int(torch._C._GLIBCXX_USE_CXX11_ABI), \
+  '-L' + os.path.join(os.path.dirname(torch.__file__), 'lib'))")
+
+ifeq ($(DIAG)$(VARIANT),)
+all: $(OUT) $(PYEXT)
+else
 all: $(OUT)
+endif
+
+$(PYEXT): $(SRC_DIR)/host/collate_py.cpp
+	@mkdir -p $(dir $@)
+	g++ -O2 -std=c++17 -shared -fPIC -Wall $(TORCH_FLAGS) $< -o $@ -ltorch_python -ltorch_cpu -lc10
 
 $(BDIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	@mkdir -p $(dir $@)
@@ -42,6 +58,6 @@ resource-usage: $(SRCS)
 	@for f in $(SRCS); do $(HIPCC) $(FLAGS) -c $$f -o /dev/null -Rpass-analysis=kernel-resource-usage 2>&1 | grep -E "Function Name|VGPRs:|AGPRs|LDS Size|Occupancy|SGPRs:"; done
 
 clean:
-	rm -rf build build_diag notorch_amd/lib/libnotorch_amd.so notorch_amd/lib/libnotorch_amd_diag.so
+	rm -rf build build_diag notorch_amd/lib/libnotorch_amd.so notorch_amd/lib/libnotorch_amd_diag.so $(PYEXT)
 
 .PHONY: all clean resource-usage

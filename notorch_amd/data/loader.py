@@ -13,8 +13,9 @@ Here:
   Workers are forked from the main process and only run host code (the library was loaded before
   the fork; a worker makes no HIP call).
 * The collator packs every tensor of the batch (features, indices, CSR layout, tile plan) into one
-  buffer (``Graph.pack``): one storage crosses the worker queue, is pinned and is copied to the
-  device, instead of ~15.
+  buffer (``Graph.pack``), allocated in shared memory inside a worker: one storage crosses the
+  worker queue without a further copy, is pinned and is copied to the device, instead of ~15.
+  The per-graph walk that feeds the native collate runs in C++ too (``csrc/host/collate_py.cpp``).
 * ``pin_memory=True`` makes the DataLoader's pin thread call ``BatchedGraph.pin_memory()``.
 * :class:`DevicePrefetcher` issues batch i+1's copies (``non_blocking``) on a side stream while the
   caller's stream computes on batch i; the caller's stream waits on the copy's event before it
@@ -37,8 +38,10 @@ class GraphCollator:
         self.rev_offset = rev_offset
 
     def __call__(self, graphs: Sequence[Graph]) -> BatchedGraph:
-        # one buffer per batch: one storage to ship to the main process, pin and copy to the device
-        return BatchedGraph.from_graphs(graphs, self.rev_offset).pack()
+        # one buffer per batch: one storage to ship to the main process, pin and copy to the device;
+        # in a worker it is allocated in shared memory, where the worker queue would copy it anyway
+        in_worker = torch.utils.data.get_worker_info() is not None
+        return BatchedGraph.from_graphs(graphs, self.rev_offset).pack(shared=in_worker)
 
 
 class DevicePrefetcher:

@@ -21,6 +21,7 @@ bit for bit; ``rev_offset="edges"`` is the corrected collate.
 """
 from __future__ import annotations
 
+import os
 import weakref
 from itertools import repeat
 from operator import attrgetter
@@ -202,10 +203,11 @@ class Graph(UpdateMixin):
                 moved.type_range = None
             other._nt_layout = moved
 
-    def pack(self):
+    def pack(self, shared: bool = False):
         """Copy every host tensor of the graph and its layout into ONE contiguous buffer (views at
         64-B aligned offsets), so pickling to the main process, pinning and the H2D copy each move
-        one storage instead of ~15 (DataLoader workers: data/loader.py)."""
+        one storage instead of ~15 (DataLoader workers: data/loader.py).  shared: allocate the
+        buffer in shared memory, so that a worker's queue ships it without another copy."""
         ts, seen = [], set()
         for t in self.tensors():
             if id(t) not in seen:
@@ -217,7 +219,10 @@ class Graph(UpdateMixin):
         for t in ts:
             offs[id(t)] = total
             total += (t.numel() * t.element_size() + 63) // 64 * 64
-        buf = torch.empty(total, dtype=torch.uint8)
+        if shared:
+            buf = torch.empty(0, dtype=torch.uint8).set_(torch.UntypedStorage._new_shared(total), 0, (total,), (1,))
+        else:
+            buf = torch.empty(total, dtype=torch.uint8)
         views = {}
         for t in ts:
             o = offs[id(t)]
@@ -344,8 +349,10 @@ class BatchedGraph(Graph):
             raise ValueError("from_graphs needs at least one graph")
         if rev_offset not in ("nodes", "edges"):
             raise ValueError(f"rev_offset must be 'nodes' or 'edges', got {rev_offset!r}")
-        if all(map(attrgetter("edge_index.is_cpu"), Gs)) and all(map(attrgetter("node_feats.is_cpu"), Gs)):
-            return _native_collate(cls, Gs, rev_offset)
+        fast = _collate_py()
+        r = fast.graph_arrays(Gs) if fast is not None else (1,)
+        if r[0] != 1 or (all(map(attrgetter("edge_index.is_cpu"), Gs)) and all(map(attrgetter("node_feats.is_cpu"), Gs))):
+            return _native_collate(cls, Gs, rev_offset, r)
         return cls._from_graphs_device(Gs, rev_offset)
 
     @classmethod
@@ -393,21 +400,49 @@ def _row_bytes(x: Tensor) -> int:
     return int(np.prod(x.shape[1:], dtype=np.int64)) * x.element_size()
 
 
-def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
-    """BatchedGraph.from_graphs through nt_collate_graphs (host C++; see include/notorch_amd.h)."""
-    import ctypes
+_COLLATE_PY: list = []
 
-    from notorch_amd import _lib
 
+def _collate_py():
+    """The collate's CPython helper (notorch_amd/lib/_collate_py*.so, built by make), or None."""
+    if not _COLLATE_PY:
+        import glob
+        import importlib.util
+
+        mod = None
+        lib_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "lib")
+        for path in glob.glob(os.path.join(lib_dir, "_collate_py*.so")):
+            spec = importlib.util.spec_from_file_location("_collate_py", path)
+            mod = importlib.util.module_from_spec(spec)
+            spec.loader.exec_module(mod)
+            break
+        _COLLATE_PY.append(mod)
+    return _COLLATE_PY[0]
+
+
+def _native_collate(cls, Gs: list, rev_offset: RevOffset, r: tuple) -> "BatchedGraph":
+    """BatchedGraph.from_graphs through nt_collate_graphs (host C++; see include/notorch_amd.h).
+    r: _collate_py().graph_arrays(Gs), or (1,) for the Python walk."""
     B = len(Gs)
     i64 = torch.int64
 
     def _c(x):  # contiguous int64 view, without a call per graph in the common case
         return x if (x.dtype is i64 and x.is_contiguous()) else x.to(i64).contiguous()
 
-    # per-graph work through C-level map() over the tensors' own methods: the per-graph Python cost
-    # is what bounds this collate (the copies and the CSR are one C++ pass)
     T = Tensor
+    if r[0] == 2:
+        raise RuntimeError("from_graphs: node_feats of the graphs differ in dtype or row shape")
+    if r[0] == 3:
+        raise RuntimeError("from_graphs: edge_feats of the graphs differ in dtype or row shape")
+    if r[0] == 4:
+        raise RuntimeError("from_graphs: edge_index / rev_index do not match edge_feats")
+    if r[0] == 0:  # the per-graph walk in C++ (csrc/host/collate_py.cpp)
+        _, n_nodes, n_edges, gptr, V, E = r
+        nd, ed = Gs[0].node_feats, Gs[0].edge_feats
+        return _collate_into(cls, Gs, rev_offset, n_nodes, n_edges, V, E, nd, ed,
+                             [gptr[k].numpy() for k in range(4)])
+    # per-graph work through C-level map() over the tensors' own methods (the extension's fallback:
+    # non-contiguous features, non-int64 indices)
     nf = list(map(attrgetter("node_feats"), Gs))
     ef = list(map(attrgetter("edge_feats"), Gs))
     ei = list(map(attrgetter("edge_index"), Gs))
@@ -423,7 +458,6 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
     nn_ = list(map(T.size, nf, repeat(0)))  # Tensor.size(0): C-level (len() goes through Python)
     ne_ = list(map(T.size, ef, repeat(0)))
     nd, ed = nf[0], ef[0]
-    nrow, erow = nd.shape[1:], ed.shape[1:]
     if len({(x.dtype, x.shape[1:]) for x in nf}) != 1:
         raise RuntimeError("from_graphs: node_feats of the graphs differ in dtype or row shape")
     if len({(x.dtype, x.shape[1:]) for x in ef}) != 1:
@@ -433,6 +467,19 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
     n_nodes = torch.tensor(nn_, dtype=i64)
     n_edges = torch.tensor(ne_, dtype=i64)
     V, E = int(n_nodes.sum()), int(n_edges.sum())
+
+    def ptrs(ts):  # the B data pointers as one array
+        return np.fromiter(map(T.data_ptr, ts), dtype=np.uint64, count=B)
+
+    return _collate_into(cls, Gs, rev_offset, n_nodes, n_edges, V, E, nd, ed, [ptrs(nf), ptrs(ef), ptrs(ei), ptrs(rv)])
+
+
+def _collate_into(cls, Gs, rev_offset, n_nodes, n_edges, V, E, nd, ed, gptrs) -> "BatchedGraph":
+    """nt_collate_graphs over the graphs' data pointers (gptrs: four arrays of B pointers: node_feats,
+    edge_feats, edge_index, rev_index), then the layout's host statistics and plans."""
+    from notorch_amd import _lib
+
+    B = len(Gs)
     node_out = torch.empty((V,) + tuple(nd.shape[1:]), dtype=nd.dtype)
     edge_out = torch.empty((E,) + tuple(ed.shape[1:]), dtype=ed.dtype)
     edge_index = torch.empty(2, E, dtype=torch.int64)
@@ -442,17 +489,12 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset) -> "BatchedGraph":
     dst_ptr = torch.empty(V + 1, dtype=torch.int32)
     dst_perm = torch.empty(E, dtype=torch.int32)
     mol_ptr = torch.empty(B + 1, dtype=torch.int32)
-    def ptrs(ts):  # array of the B data pointers, passed as one pointer
-        a = np.fromiter(map(T.data_ptr, ts), dtype=np.uint64, count=B)
-        keep.append(a)
-        return a.ctypes.data
-
-    keep: list = []
+    gp = [np.ascontiguousarray(a) for a in gptrs]
     lib = _lib.load()
     _lib.check(lib.nt_collate_graphs(
-        B, ptrs(nf), n_nodes.data_ptr(), _row_bytes(nd),
-        ptrs(ef), n_edges.data_ptr(), _row_bytes(ed),
-        ptrs(ei), ptrs(rv), 0 if rev_offset == "nodes" else 1, node_out.data_ptr(), edge_out.data_ptr(),
+        B, gp[0].ctypes.data, n_nodes.data_ptr(), _row_bytes(nd),
+        gp[1].ctypes.data, n_edges.data_ptr(), _row_bytes(ed),
+        gp[2].ctypes.data, gp[3].ctypes.data, 0 if rev_offset == "nodes" else 1, node_out.data_ptr(), edge_out.data_ptr(),
         edge_index.data_ptr(), rev_index.data_ptr(), bni.data_ptr(), bei.data_ptr(),
         dst_ptr.data_ptr(), dst_perm.data_ptr(), mol_ptr.data_ptr(),
     ))

@@ -218,3 +218,46 @@ def test_collate_ships_balanced_plans():
         assert all(int(t) in starts for t in tp)  # every cut is a node boundary
         assert (rounds - 1) * 256 < ntiles <= rounds * 256, (rows, ntiles)
     assert lay.plan[1] > lay.plan_wide[1]  # the 64-row plan has more, smaller tiles
+
+
+def test_collate_helper_walk_matches_python_walk():
+    """csrc/host/collate_py.cpp (the per-graph walk in C++) feeds nt_collate_graphs exactly what the
+    Python walk does: same batch, same layout; non-contiguous features and int32 indices take the
+    Python walk; mismatched rows / index sizes raise the same errors."""
+    from notorch_amd.data.models import graph as gm
+
+    fast = gm._collate_py()
+    assert fast is not None, "notorch_amd/lib/_collate_py*.so not built (run make)"
+    Gs = make_batch("zinc", 40, seed=11).to_graphs()
+    r = fast.graph_arrays(Gs)
+    assert r[0] == 0 and r[4] == sum(G.num_nodes for G in Gs) and r[5] == sum(G.num_edges for G in Gs)
+    assert r[3][0, 3].item() == Gs[3].node_feats.data_ptr() and r[3][3, 5].item() == Gs[5].rev_index.data_ptr()
+    for mode in ("nodes", "edges"):
+        a = gm._native_collate(BatchedGraph, Gs, mode, r)
+        b = gm._native_collate(BatchedGraph, Gs, mode, (1,))
+        for f in FIELDS:
+            assert torch.equal(getattr(a, f), getattr(b, f)), f
+        la, lb = a._nt_layout, b._nt_layout
+        for x, y in zip(la.tensors(), lb.tensors()):
+            assert torch.equal(x, y)
+        assert (la.deg_range, la.mol_max, la.type_range) == (lb.deg_range, lb.mol_max, lb.type_range)
+    # Python-walk cases: non-contiguous features, int32 indices
+    nc = [Graph(G.node_feats.t().contiguous().t(), G.edge_feats, G.edge_index, G.rev_index) for G in Gs[:4]]
+    i32 = [Graph(G.node_feats, G.edge_feats, G.edge_index.int(), G.rev_index.int()) for G in Gs[:4]]
+    for case in (nc, i32):
+        assert fast.graph_arrays(case) == (1,)
+        BG = BatchedGraph.from_graphs(case)
+        ref = collate_ref.from_graphs(case)
+        for f in FIELDS:
+            assert torch.equal(getattr(BG, f), ref[f].to(getattr(BG, f).dtype)), f
+    # errors
+    g0 = Gs[0]
+    bad_nf = [g0, Graph(g0.node_feats[:, :3].contiguous(), g0.edge_feats, g0.edge_index, g0.rev_index)]
+    bad_ef = [g0, Graph(g0.node_feats, g0.edge_feats.float(), g0.edge_index, g0.rev_index)]
+    bad_ix = [g0, Graph(g0.node_feats, g0.edge_feats, g0.edge_index, g0.rev_index[:-1])]
+    for case, code, msg in ((bad_nf, 2, "node_feats"), (bad_ef, 3, "edge_feats"), (bad_ix, 4, "rev_index")):
+        assert fast.graph_arrays(case) == (code,)
+        with pytest.raises(RuntimeError, match=msg):
+            BatchedGraph.from_graphs(case)
+    with pytest.raises(TypeError):
+        fast.graph_arrays(3)
