@@ -16,7 +16,8 @@ Here:
   buffer (``Graph.pack``), allocated in shared memory inside a worker: one storage crosses the
   worker queue without a further copy, is pinned and is copied to the device, instead of ~15.
   The per-graph walk that feeds the native collate runs in C++ too (``csrc/host/collate_py.cpp``).
-* ``pin_memory=True`` makes the DataLoader's pin thread call ``BatchedGraph.pin_memory()``.
+* ``BatchedGraph.pin_memory()`` runs on a small thread pool of the main process
+  (``DevicePrefetcher(pin_threads=...)``; the DataLoader's own pin thread with ``pin_threads=0``).
 * :class:`DevicePrefetcher` issues batch i+1's copies (``non_blocking``) on a side stream while the
   caller's stream computes on batch i; the caller's stream waits on the copy's event before it
   touches the batch, and every moved tensor is recorded on the caller's stream for the caching
@@ -44,13 +45,64 @@ class GraphCollator:
         return BatchedGraph.from_graphs(graphs, self.rev_offset).pack(shared=in_worker)
 
 
-class DevicePrefetcher:
-    """Iterate host batches as device batches, one batch of H2D copies ahead of the consumer."""
+def pinned_in_order(batches: Iterable, threads: int, pin, device_index: Optional[int] = None) -> Iterator:
+    """pin(b) for every b of `batches`, computed by `threads` threads, yielded in the input order.
+    A feeder thread draws from `batches` (at most 2 x threads pins in flight); an exception of the
+    source or of a pin is raised to the consumer at that batch's position."""
+    import queue
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
 
-    def __init__(self, batches: Iterable[BatchedGraph], device: torch.device | str):
+    init = (lambda: torch.cuda.set_device(device_index)) if device_index is not None else None
+    pool = ThreadPoolExecutor(threads, initializer=init, thread_name_prefix="nt_pin")
+    q: queue.Queue = queue.Queue(maxsize=2 * threads)
+    stop = threading.Event()
+    end = object()
+
+    def feed():
+        try:
+            for b in batches:
+                if stop.is_set():
+                    return
+                q.put(pool.submit(pin, b))
+            q.put(end)
+        except BaseException as e:  # the consumer re-raises it
+            q.put(e)
+
+    t = threading.Thread(target=feed, daemon=True, name="nt_pin_feed")
+    t.start()
+    try:
+        while True:
+            f = q.get()
+            if f is end:
+                return
+            if isinstance(f, BaseException):
+                raise f
+            yield f.result()
+    finally:
+        stop.set()
+        while t.is_alive():  # unblock a feeder waiting on a full queue
+            try:
+                q.get_nowait()
+            except queue.Empty:
+                t.join(timeout=0.01)
+        pool.shutdown(wait=True)
+
+
+class DevicePrefetcher:
+    """Iterate host batches as device batches, one batch of H2D copies ahead of the consumer.
+
+    pin_threads > 0: the host batches are pageable (DataLoader(pin_memory=False)); a feeder thread
+    takes them from the loader in order and `pin_threads` threads pin them concurrently (each pin is
+    a 7 MB copy out of the worker's shared-memory segment at config 2, which one pin thread -- the
+    DataLoader's own -- cannot do at the device's rate).  Order is kept: batches come out as the
+    loader yields them."""
+
+    def __init__(self, batches: Iterable[BatchedGraph], device: torch.device | str, pin_threads: int = 0):
         self.batches = batches
         self.device = torch.device(device)
         self.stream = torch.cuda.Stream(self.device)
+        self.pin_threads = pin_threads
 
     def _issue(self, it: Iterator[BatchedGraph]) -> Optional[tuple]:
         try:
@@ -64,7 +116,11 @@ class DevicePrefetcher:
         return dev, ev
 
     def __iter__(self) -> Iterator[BatchedGraph]:
-        it = iter(self.batches)
+        if self.pin_threads > 0:
+            idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
+            it = pinned_in_order(self.batches, self.pin_threads, BatchedGraph.pin_memory, idx)
+        else:
+            it = iter(self.batches)
         nxt = self._issue(it)
         while nxt is not None:
             G, ev = nxt
@@ -86,15 +142,17 @@ def graph_loader(
     rev_offset: RevOffset = "nodes",
     shuffle: bool = False,
     prefetch_factor: int = 2,
+    pin_threads: int = 4,
     **kwargs,
 ) -> DevicePrefetcher:
-    """DataLoader (workers collate, pin thread pins) wrapped in a :class:`DevicePrefetcher`."""
+    """DataLoader (workers collate) wrapped in a :class:`DevicePrefetcher` whose `pin_threads`
+    threads pin the batches (0: the DataLoader's single pin thread)."""
     from notorch_amd import _lib
 
     _lib.load()  # load the collate library before the workers fork
     dl = torch.utils.data.DataLoader(
         dataset, batch_size=batch_size, shuffle=shuffle, collate_fn=GraphCollator(rev_offset),
-        num_workers=num_workers, pin_memory=True, persistent_workers=num_workers > 0,
+        num_workers=num_workers, pin_memory=pin_threads == 0, persistent_workers=num_workers > 0,
         prefetch_factor=prefetch_factor if num_workers > 0 else None, **kwargs,
     )
-    return DevicePrefetcher(dl, device)
+    return DevicePrefetcher(dl, device, pin_threads=pin_threads)

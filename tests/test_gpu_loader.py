@@ -8,7 +8,8 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda"
 
 
-def test_graph_loader_batches_and_forward_bit_identical():
+@pytest.mark.parametrize("pin_threads", [0, 3])
+def test_graph_loader_batches_and_forward_bit_identical(pin_threads):
     from notorch_amd.data.loader import graph_loader
     from notorch_amd.data.models.graph import BatchedGraph
     from notorch_amd.data.synth import make_batch
@@ -19,11 +20,12 @@ def test_graph_loader_batches_and_forward_bit_identical():
     enc = EmbeddedChempropBlock(GraphEmbedding(42, 13, 64), ChempropBlock(hidden_dim=64, depth=3)).eval().to(DEV)
     got = []
     with torch.no_grad():
-        for G in graph_loader(graphs, 64, DEV, num_workers=2):
+        for G in graph_loader(graphs, 64, DEV, num_workers=2, pin_threads=pin_threads):
             assert G.node_feats.device.type == "cuda" and G._nt_layout.dst_ptr.device.type == "cuda"
             got.append(Sum()(enc(G)))
     torch.cuda.synchronize()
     assert len(got) == 4
+    # the batches arrive in the loader's order (several pin threads)
     with torch.no_grad():
         for i, r in enumerate(got):
             ref = Sum()(enc(BatchedGraph.from_graphs(graphs[64 * i:64 * (i + 1)]).to(DEV)))

@@ -62,3 +62,42 @@ def test_pack_one_buffer_same_values_and_pickles_as_one_storage():
     for x, y in zip(G3.tensors(), ref.tensors()):
         assert torch.equal(x, y)
     assert G3._nt_layout.type_range is None  # the statistics described the replaced tensor
+
+
+def test_pinned_in_order_keeps_order_and_raises():
+    """The prefetcher's pin pool (data/loader.py pinned_in_order): several threads, input order kept,
+    a source error surfaces at its position, an early stop releases the feeder."""
+    import random
+    import time
+
+    import pytest
+
+    from notorch_amd.data.loader import pinned_in_order
+
+    def slow(b):
+        time.sleep(random.random() * 0.005)
+        return b * 10
+
+    assert list(pinned_in_order(range(40), 4, slow)) == [10 * i for i in range(40)]
+
+    def src():
+        yield 1
+        yield 2
+        raise ValueError("bad batch")
+
+    got = []
+    with pytest.raises(ValueError, match="bad batch"):
+        for x in pinned_in_order(src(), 3, slow):
+            got.append(x)
+    assert got == [10, 20]
+
+    def bad_pin(b):
+        if b == 3:
+            raise RuntimeError("pin failed")
+        return b
+
+    with pytest.raises(RuntimeError, match="pin failed"):
+        list(pinned_in_order(range(10), 2, bad_pin))
+    it = pinned_in_order(range(1000), 2, slow)
+    assert next(it) == 0
+    it.close()  # the feeder stops and the pool shuts down

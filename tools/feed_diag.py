@@ -15,6 +15,7 @@ sys.path.insert(0, ROOT)
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--workers", type=int, default=8)
+    p.add_argument("--pin-threads", type=int, default=4)
     a = p.parse_args()
     import torch
 
@@ -33,10 +34,10 @@ def main():
     graphs = make_batch("qm9", 4096, seed=1000).to_graphs()
     W = a.workers
     warm, n = W * 2 + 4, 3 * W
-    out = {"workers": W}
+    out = {"workers": W, "pin_threads": a.pin_threads}
 
     def run_loader(model: bool):
-        loader = graph_loader(graphs * (warm + n), 4096, dev, num_workers=W)
+        loader = graph_loader(graphs * (warm + n), 4096, dev, num_workers=W, pin_threads=a.pin_threads)
         it = iter(loader)
         with torch.no_grad():
             for _ in range(warm):

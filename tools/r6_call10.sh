@@ -1,8 +1,9 @@
 #!/bin/bash
-# host-feed breakdown (tools/feed_diag.py) at 8 and 14 workers
+# host-feed breakdown (tools/feed_diag.py): DataLoader pin thread vs a 4-thread pin pool, 8 / 14 workers
 set -uo pipefail
 mkdir -p gpurun_out
-timeout -k 10 300 python tools/feed_diag.py --workers 8 > gpurun_out/feed_diag8.txt 2>&1 || { tail -30 gpurun_out/feed_diag8.txt; exit 2; }
-tail -1 gpurun_out/feed_diag8.txt
-timeout -k 10 300 python tools/feed_diag.py --workers 14 > gpurun_out/feed_diag14.txt 2>&1 || { tail -30 gpurun_out/feed_diag14.txt; exit 3; }
-tail -1 gpurun_out/feed_diag14.txt
+for cfg in "8 0" "8 4" "14 4"; do
+  set -- $cfg
+  timeout -k 10 300 python tools/feed_diag.py --workers $1 --pin-threads $2 > gpurun_out/feed_diag_$1_$2.txt 2>&1 || { tail -30 gpurun_out/feed_diag_$1_$2.txt; exit 2; }
+  tail -1 gpurun_out/feed_diag_$1_$2.txt
+done
