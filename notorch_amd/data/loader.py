@@ -32,17 +32,149 @@ import torch
 from notorch_amd.data.models.graph import BatchedGraph, Graph, RevOffset
 
 
+class SlotRing:
+    """Fixed shared-memory batch slots that DataLoader workers pack into, mapped once by every process.
+
+    Created in the main process before the workers fork (they inherit the mapping); the main process
+    then page-locks the whole ring once (``hipHostRegister``), so a batch goes from the worker's pack
+    straight to the device by DMA: no per-batch shared-memory segment, file-descriptor hand-off,
+    mapping, pinned copy or unmapping in the main process.  Worker w owns slots
+    [w * per_worker, (w + 1) * per_worker); ``flags[s]`` is 1 from the worker's pack until the main
+    process's copy out of slot s has completed."""
+
+    def __init__(self, workers: int, per_worker: int, slot_bytes: int):
+        self.workers, self.per_worker = workers, per_worker
+        self.slot_bytes = (slot_bytes + 63) // 64 * 64
+        n = workers * per_worker
+        self.buf = torch.empty(0, dtype=torch.uint8).set_(
+            torch.UntypedStorage._new_shared(n * self.slot_bytes), 0, (n * self.slot_bytes,), (1,))
+        self.flags = torch.zeros(n, dtype=torch.int32).share_memory_()
+        self.registered = False
+
+    def slot(self, s: int) -> torch.Tensor:
+        return self.buf[s * self.slot_bytes:(s + 1) * self.slot_bytes]
+
+    def acquire(self, worker: int, timeout_s: float = 2.0) -> int:
+        """A free slot of `worker` (marked in use), or -1 after timeout_s (the caller then ships the
+        batch the ordinary way)."""
+        import time
+
+        f = self.flags.numpy()
+        t_end = time.monotonic() + timeout_s
+        while True:
+            for s in range(worker * self.per_worker, (worker + 1) * self.per_worker):
+                if f[s] == 0:
+                    f[s] = 1
+                    return s
+            if time.monotonic() > t_end:
+                return -1
+            time.sleep(5e-5)
+
+    def release(self, s: int) -> None:
+        self.flags.numpy()[s] = 0
+
+    def register(self) -> bool:
+        """Page-lock the ring for DMA (main process, after the workers forked)."""
+        if not self.registered and torch.cuda.is_available():
+            rc = torch.cuda.cudart().cudaHostRegister(self.buf.data_ptr(), self.buf.numel(), 0)
+            self.registered = int(rc) == 0
+        return self.registered
+
+    def unregister(self) -> None:
+        if self.registered:
+            torch.cuda.cudart().cudaHostUnregister(self.buf.data_ptr())
+            self.registered = False
+
+    def __del__(self):
+        try:
+            self.unregister()
+        except Exception:  # interpreter shutdown: the runtime may be gone
+            pass
+
+    @staticmethod
+    def fits(nbytes: int) -> bool:
+        """Whether /dev/shm has room for nbytes twice over (tmpfs raises SIGBUS on a page past its
+        limit, so the ring is only used when it fits with margin)."""
+        import os
+
+        try:
+            st = os.statvfs("/dev/shm")
+        except OSError:
+            return False
+        return st.f_bavail * st.f_frsize >= 2 * nbytes
+
+
+class SlotBatch:
+    """What a worker returns for a batch packed into ring slot `slot`: the batch pickled with every
+    tensor inside the slot replaced by its (offset, dtype, shape, stride): a few KB through the
+    worker queue instead of a shared-memory segment."""
+
+    __slots__ = ("slot", "blob")
+
+    def __init__(self, slot: int, blob: bytes):
+        self.slot, self.blob = slot, blob
+
+    @staticmethod
+    def pack(G: BatchedGraph, ring: SlotRing, s: int) -> "SlotBatch":
+        import io
+        import pickle
+
+        G.pack(out=ring.slot(s))
+        base = ring.slot(s).data_ptr()
+        end = base + ring.slot_bytes
+
+        class P(pickle.Pickler):
+            def persistent_id(self, obj):
+                if isinstance(obj, torch.Tensor) and obj.device.type == "cpu" and base <= obj.data_ptr() < end:
+                    return ("nt_slot", obj.data_ptr() - base, obj.dtype, tuple(obj.shape), tuple(obj.stride()))
+                return None
+
+        f = io.BytesIO()
+        P(f, pickle.HIGHEST_PROTOCOL).dump(G)
+        return SlotBatch(s, f.getvalue())
+
+    def load(self, ring: SlotRing) -> BatchedGraph:
+        import io
+        import pickle
+
+        storage = ring.buf.untyped_storage()
+        off0 = self.slot * ring.slot_bytes
+
+        class U(pickle.Unpickler):
+            def persistent_load(self, pid):
+                _, off, dtype, shape, stride = pid
+                isz = torch.empty(0, dtype=dtype).element_size()
+                return torch.empty(0, dtype=dtype).set_(storage, (off0 + off) // isz, shape, stride)
+
+        return U(io.BytesIO(self.blob)).load()
+
+
 class GraphCollator:
-    """``collate_fn`` for a dataset of per-molecule :class:`Graph` items (transforms/graph.py:45)."""
+    """``collate_fn`` for a dataset of per-molecule :class:`Graph` items (transforms/graph.py:45).
+    ring: pack worker batches into its slots (graph_loader sets it); None: one shared-memory buffer
+    per batch."""
 
-    def __init__(self, rev_offset: RevOffset = "nodes"):
+    def __init__(self, rev_offset: RevOffset = "nodes", ring: Optional[SlotRing] = None):
         self.rev_offset = rev_offset
+        self.ring = ring
 
-    def __call__(self, graphs: Sequence[Graph]) -> BatchedGraph:
+    def __call__(self, graphs: Sequence[Graph]):
         # one buffer per batch: one storage to ship to the main process, pin and copy to the device;
         # in a worker it is allocated in shared memory, where the worker queue would copy it anyway
-        in_worker = torch.utils.data.get_worker_info() is not None
-        return BatchedGraph.from_graphs(graphs, self.rev_offset).pack(shared=in_worker)
+        info = torch.utils.data.get_worker_info()
+        s = self.ring.acquire(info.id) if info is not None and self.ring is not None else -1
+        if s < 0:
+            return BatchedGraph.from_graphs(graphs, self.rev_offset).pack(shared=info is not None)
+        # the collate writes straight into the slot; pack() then copies only the layout's plans
+        slot = self.ring.slot(s)
+        G = BatchedGraph.from_graphs(graphs, self.rev_offset, out=slot)
+        if 0 < G.packed_nbytes() <= self.ring.slot_bytes:
+            return SlotBatch.pack(G, self.ring, s)
+        # does not fit (or does not pack): move every tensor out of the slot, then free it
+        base, end = slot.data_ptr(), slot.data_ptr() + slot.numel()
+        G._apply(lambda t: t.clone() if base <= t.data_ptr() < end else t, G)
+        self.ring.release(s)
+        return G.pack(shared=True)
 
 
 def pinned_in_order(batches: Iterable, threads: int, pin, device_index: Optional[int] = None) -> Iterator:
@@ -89,6 +221,10 @@ def pinned_in_order(batches: Iterable, threads: int, pin, device_index: Optional
         pool.shutdown(wait=True)
 
 
+def _pin(b):
+    return b if isinstance(b, SlotBatch) else BatchedGraph.pin_memory(b)
+
+
 class DevicePrefetcher:
     """Iterate host batches as device batches, one batch of H2D copies ahead of the consumer.
 
@@ -98,39 +234,72 @@ class DevicePrefetcher:
     DataLoader's own -- cannot do at the device's rate).  Order is kept: batches come out as the
     loader yields them."""
 
-    def __init__(self, batches: Iterable[BatchedGraph], device: torch.device | str, pin_threads: int = 0):
+    def __init__(self, batches: Iterable[BatchedGraph], device: torch.device | str, pin_threads: int = 0,
+                 ring: Optional[SlotRing] = None):
         self.batches = batches
         self.device = torch.device(device)
         self.stream = torch.cuda.Stream(self.device)
         self.pin_threads = pin_threads
+        self.ring = ring
+        self._held: list = []  # (event, slot): ring slots whose device copy may still be running
+
+    def _release_done(self, wait: bool = False) -> None:
+        keep = []
+        for ev, s in self._held:
+            if wait:
+                ev.synchronize()
+            if wait or ev.query():
+                self.ring.release(s)
+            else:
+                keep.append((ev, s))
+        self._held = keep
 
     def _issue(self, it: Iterator[BatchedGraph]) -> Optional[tuple]:
+        if self._held:
+            self._release_done()  # before blocking on the loader: a worker may be waiting for a slot
         try:
             host = next(it)
         except StopIteration:
             return None
+        slot = -1
+        if isinstance(host, SlotBatch):
+            slot, host = host.slot, host.load(self.ring)
+            if not self.ring.registered:  # no page-locked ring: copy out into pinned memory first
+                pinned = host.pin_memory()
+                self.ring.release(slot)
+                slot, host = -1, pinned
+        elif self.ring is not None:  # a batch that missed a slot (no DataLoader pin thread here)
+            host = host.pin_memory()
         with torch.cuda.stream(self.stream):
             dev = host.to(self.device, non_blocking=True)
             ev = torch.cuda.Event()
             ev.record(self.stream)
+        if slot >= 0:
+            self._held.append((ev, slot))
         return dev, ev
 
     def __iter__(self) -> Iterator[BatchedGraph]:
         if self.pin_threads > 0:
             idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
-            it = pinned_in_order(self.batches, self.pin_threads, BatchedGraph.pin_memory, idx)
+            it = pinned_in_order(self.batches, self.pin_threads, _pin, idx)
         else:
-            it = iter(self.batches)
-        nxt = self._issue(it)
-        while nxt is not None:
-            G, ev = nxt
-            cur = torch.cuda.current_stream(self.device)
-            cur.wait_event(ev)
-            buf = G._packed_base()  # the allocator must not reuse these before the consumer is done
-            for t in ([buf] if buf is not None else G.tensors()):
-                t.record_stream(cur)
-            nxt = self._issue(it)  # the next batch's copies overlap this batch's compute
-            yield G
+            it = iter(self.batches)  # (forks the DataLoader's workers: the ring is registered after)
+        if self.ring is not None:
+            self.ring.register()
+        try:
+            nxt = self._issue(it)
+            while nxt is not None:
+                G, ev = nxt
+                cur = torch.cuda.current_stream(self.device)
+                cur.wait_event(ev)
+                buf = G._packed_base()  # the allocator must not reuse these before the consumer is done
+                for t in ([buf] if buf is not None else G.tensors()):
+                    t.record_stream(cur)
+                nxt = self._issue(it)  # the next batch's copies overlap this batch's compute
+                yield G
+        finally:
+            if self.ring is not None:
+                self._release_done(wait=True)
 
 
 def graph_loader(
@@ -142,17 +311,49 @@ def graph_loader(
     rev_offset: RevOffset = "nodes",
     shuffle: bool = False,
     prefetch_factor: int = 2,
-    pin_threads: int = 4,
+    pin_threads: int = 0,
+    ring_slots: int = 3,
     **kwargs,
 ) -> DevicePrefetcher:
-    """DataLoader (workers collate) wrapped in a :class:`DevicePrefetcher` whose `pin_threads`
-    threads pin the batches (0: the DataLoader's single pin thread)."""
+    """DataLoader (workers collate) wrapped in a :class:`DevicePrefetcher`.
+
+    ring_slots > 0 (and workers): batches travel through a page-locked :class:`SlotRing` of
+    `ring_slots` slots per worker, sized from the first batch (x 1.5); a batch that does not fit, or
+    finds no free slot, takes the path below.  Otherwise each batch is one shared-memory buffer, pinned
+    by the DataLoader's pin thread (pin_threads = 0) or by `pin_threads` threads of the main process."""
     from notorch_amd import _lib
 
     _lib.load()  # load the collate library before the workers fork
-    dl = torch.utils.data.DataLoader(
-        dataset, batch_size=batch_size, shuffle=shuffle, collate_fn=GraphCollator(rev_offset),
-        num_workers=num_workers, pin_memory=pin_threads == 0, persistent_workers=num_workers > 0,
-        prefetch_factor=prefetch_factor if num_workers > 0 else None, **kwargs,
-    )
-    return DevicePrefetcher(dl, device, pin_threads=pin_threads)
+    ring = None
+    if ring_slots > 0 and num_workers > 0 and len(dataset) > 0 and torch.cuda.is_available():
+        first = BatchedGraph.from_graphs([dataset[i] for i in range(min(batch_size, len(dataset)))], rev_offset)
+        slot = first.packed_nbytes() * 3 // 2 + (1 << 16)
+        if first.packed_nbytes() > 0 and SlotRing.fits(num_workers * ring_slots * slot):
+            ring = SlotRing(num_workers, ring_slots, slot)
+    coll = GraphCollator(rev_offset, ring)
+    common = dict(num_workers=num_workers, persistent_workers=num_workers > 0,
+                  prefetch_factor=prefetch_factor if num_workers > 0 else None, collate_fn=coll)
+    # with the ring, batches arrive page-locked (a batch that missed a slot is pinned in _issue): no
+    # DataLoader pin thread, whose hand-off costs the consumer thread time per batch
+    pin = pin_threads == 0 and ring is None
+    if not shuffle and not kwargs and isinstance(dataset, (list, tuple)):
+        # sequential batches as slices: the index queue carries one range per batch instead of
+        # batch_size ints, and a worker fetches its graphs with one slice
+        dl = torch.utils.data.DataLoader(_Slices(dataset, batch_size), batch_size=None, pin_memory=pin, **common)
+    else:
+        dl = torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=shuffle, pin_memory=pin, **common,
+                                         **kwargs)
+    return DevicePrefetcher(dl, device, pin_threads=pin_threads, ring=ring)
+
+
+class _Slices(torch.utils.data.Dataset):
+    """Batch b of a list dataset = its b-th slice of batch_size items (the last one shorter)."""
+
+    def __init__(self, data, batch_size: int):
+        self.data, self.batch_size = data, batch_size
+
+    def __len__(self) -> int:
+        return (len(self.data) + self.batch_size - 1) // self.batch_size
+
+    def __getitem__(self, b: int):
+        return self.data[b * self.batch_size:(b + 1) * self.batch_size]

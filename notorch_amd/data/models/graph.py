@@ -21,6 +21,7 @@ bit for bit; ``rev_offset="edges"`` is the corrected collate.
 """
 from __future__ import annotations
 
+import ctypes
 import os
 import weakref
 from itertools import repeat
@@ -187,10 +188,11 @@ class Graph(UpdateMixin):
             self._apply(lambda t: t.to(device, non_blocking=non_blocking), self)
         return self
 
-    def _apply(self, fn, other) -> None:
+    def _apply(self, fn, other, types_ok: Optional[bool] = None) -> None:
         """other's fields and kernel layout := fn(self's); the layout's host statistics stay bound
-        to the features when they described them."""
-        types_ok = self._layout_types_ok()
+        to the features when they described them (types_ok: that answer, taken before fn ran)."""
+        if types_ok is None:
+            types_ok = self._layout_types_ok()
         lay = getattr(self, "_nt_layout", None)
         for name in self._field_names():
             setattr(other, name, fn(getattr(self, name)))
@@ -203,23 +205,45 @@ class Graph(UpdateMixin):
                 moved.type_range = None
             other._nt_layout = moved
 
-    def pack(self, shared: bool = False):
-        """Copy every host tensor of the graph and its layout into ONE contiguous buffer (views at
-        64-B aligned offsets), so pickling to the main process, pinning and the H2D copy each move
-        one storage instead of ~15 (DataLoader workers: data/loader.py).  shared: allocate the
-        buffer in shared memory, so that a worker's queue ships it without another copy."""
+    def _pack_plan(self):
+        """(tensors, their byte offsets, total bytes) of pack()'s one-buffer layout, or None when a
+        tensor is off the CPU or empty (the graph then stays unpacked)."""
         ts, seen = [], set()
         for t in self.tensors():
             if id(t) not in seen:
                 seen.add(id(t))
                 ts.append(t)
         if any(t.device.type != "cpu" or t.numel() == 0 for t in ts):
-            return self
+            return None
         offs, total = {}, 0
         for t in ts:
             offs[id(t)] = total
             total += (t.numel() * t.element_size() + 63) // 64 * 64
-        if shared:
+        return ts, offs, total
+
+    def packed_nbytes(self) -> int:
+        """Bytes of pack()'s buffer (0: the graph does not pack)."""
+        plan = self._pack_plan()
+        return 0 if plan is None else plan[2]
+
+    def pack(self, shared: bool = False, out: Optional[Tensor] = None):
+        """Copy every host tensor of the graph and its layout into ONE contiguous buffer (views at
+        64-B aligned offsets), so pickling to the main process, pinning and the H2D copy each move
+        one storage instead of ~15 (DataLoader workers: data/loader.py).  shared: allocate the
+        buffer in shared memory, so that a worker's queue ships it without another copy.  out: a
+        1-D uint8 CPU tensor of at least packed_nbytes() bytes to pack into (its first bytes)."""
+        plan = self._pack_plan()
+        if plan is None:
+            return self
+        ts, offs, total = plan
+        # before any copy: with from_graphs(out=...) the fields are views of `out`, whose version
+        # counter the copies below advance
+        types_ok = self._layout_types_ok()
+        if out is not None:
+            if out.dtype != torch.uint8 or out.dim() != 1 or out.numel() < total or out.device.type != "cpu":
+                raise ValueError(f"pack(out=...) needs a CPU uint8 vector of >= {total} bytes")
+            buf = out[:total]
+        elif shared:
             buf = torch.empty(0, dtype=torch.uint8).set_(torch.UntypedStorage._new_shared(total), 0, (total,), (1,))
         else:
             buf = torch.empty(total, dtype=torch.uint8)
@@ -227,9 +251,10 @@ class Graph(UpdateMixin):
         for t in ts:
             o = offs[id(t)]
             v = buf[o:o + t.numel() * t.element_size()].view(t.dtype).view(t.shape)
-            v.copy_(t)
+            if v.data_ptr() != t.data_ptr():  # from_graphs(out=...) already wrote it in place
+                v.copy_(t)
             views[id(t)] = v
-        self._apply(lambda t: views[id(t)], self)
+        self._apply(lambda t: views[id(t)], self, types_ok)
         self._nt_packed = buf
         return self
 
@@ -260,7 +285,10 @@ class Graph(UpdateMixin):
         other = copy(self)
         buf = self._packed_base()
         if buf is not None:
-            new = buf.pin_memory()
+            # the packed buffer's copy through ctypes.memmove, which releases the GIL (Tensor.pin_memory
+            # holds it for the whole copy: 7 MB at config 2, stalling the thread that launches kernels)
+            new = torch.empty(buf.numel(), dtype=torch.uint8, pin_memory=True)
+            ctypes.memmove(new.data_ptr(), buf.data_ptr(), buf.numel())
             self._apply(_rebaser(buf, new), other)
             other._nt_packed = new
         else:
@@ -335,14 +363,17 @@ class BatchedGraph(Graph):
         return [getattr(self, n) for n in self._field_names()]
 
     @classmethod
-    def from_graphs(cls, Gs: Iterable[Graph], rev_offset: RevOffset = "nodes") -> "BatchedGraph":
+    def from_graphs(cls, Gs: Iterable[Graph], rev_offset: RevOffset = "nodes", *,
+                    out: Optional[Tensor] = None) -> "BatchedGraph":
         """Collate (reference ``graph.py:186-223``) + the CSR layout the kernels consume.
 
         ``rev_offset="nodes"`` reproduces the reference exactly, including the offset of
         ``rev_index`` by the cumulative node count (``graph.py:200``); ``"edges"`` fixes it.
         Host graphs go through the native one-pass collate (``nt_collate_graphs``: copies, offsets,
         validation and an O(V+E) counting-sort CSR in C++); graphs already on a device are
-        collated with device ops.
+        collated with device ops.  out (host graphs; data/loader.py): a 1-D uint8 CPU buffer the
+        native collate writes its outputs into, at the offsets pack() gives them, so that a later
+        pack(out=out) copies only the layout's plans (the outputs may be views into out).
         """
         Gs = list(Gs)
         if len(Gs) == 0:
@@ -352,7 +383,7 @@ class BatchedGraph(Graph):
         fast = _collate_py()
         r = fast.graph_arrays(Gs) if fast is not None else (1,)
         if r[0] != 1 or (all(map(attrgetter("edge_index.is_cpu"), Gs)) and all(map(attrgetter("node_feats.is_cpu"), Gs))):
-            return _native_collate(cls, Gs, rev_offset, r)
+            return _native_collate(cls, Gs, rev_offset, r, out)
         return cls._from_graphs_device(Gs, rev_offset)
 
     @classmethod
@@ -420,7 +451,7 @@ def _collate_py():
     return _COLLATE_PY[0]
 
 
-def _native_collate(cls, Gs: list, rev_offset: RevOffset, r: tuple) -> "BatchedGraph":
+def _native_collate(cls, Gs: list, rev_offset: RevOffset, r: tuple, out: Optional[Tensor] = None) -> "BatchedGraph":
     """BatchedGraph.from_graphs through nt_collate_graphs (host C++; see include/notorch_amd.h).
     r: _collate_py().graph_arrays(Gs), or (1,) for the Python walk."""
     B = len(Gs)
@@ -440,7 +471,7 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset, r: tuple) -> "BatchedG
         _, n_nodes, n_edges, gptr, V, E = r
         nd, ed = Gs[0].node_feats, Gs[0].edge_feats
         return _collate_into(cls, Gs, rev_offset, n_nodes, n_edges, V, E, nd, ed,
-                             [gptr[k].numpy() for k in range(4)])
+                             [gptr[k].numpy() for k in range(4)], out)
     # per-graph work through C-level map() over the tensors' own methods (the extension's fallback:
     # non-contiguous features, non-int64 indices)
     nf = list(map(attrgetter("node_feats"), Gs))
@@ -471,24 +502,29 @@ def _native_collate(cls, Gs: list, rev_offset: RevOffset, r: tuple) -> "BatchedG
     def ptrs(ts):  # the B data pointers as one array
         return np.fromiter(map(T.data_ptr, ts), dtype=np.uint64, count=B)
 
-    return _collate_into(cls, Gs, rev_offset, n_nodes, n_edges, V, E, nd, ed, [ptrs(nf), ptrs(ef), ptrs(ei), ptrs(rv)])
+    return _collate_into(cls, Gs, rev_offset, n_nodes, n_edges, V, E, nd, ed, [ptrs(nf), ptrs(ef), ptrs(ei), ptrs(rv)],
+                         out)
 
 
-def _collate_into(cls, Gs, rev_offset, n_nodes, n_edges, V, E, nd, ed, gptrs) -> "BatchedGraph":
+def _collate_into(cls, Gs, rev_offset, n_nodes, n_edges, V, E, nd, ed, gptrs, out=None) -> "BatchedGraph":
     """nt_collate_graphs over the graphs' data pointers (gptrs: four arrays of B pointers: node_feats,
-    edge_feats, edge_index, rev_index), then the layout's host statistics and plans."""
+    edge_feats, edge_index, rev_index), then the layout's host statistics and plans.  out: write the
+    nine collate outputs into this uint8 buffer at pack()'s offsets (when they fit)."""
     from notorch_amd import _lib
 
     B = len(Gs)
-    node_out = torch.empty((V,) + tuple(nd.shape[1:]), dtype=nd.dtype)
-    edge_out = torch.empty((E,) + tuple(ed.shape[1:]), dtype=ed.dtype)
-    edge_index = torch.empty(2, E, dtype=torch.int64)
-    rev_index = torch.empty(E, dtype=torch.int64)
-    bni = torch.empty(V, dtype=torch.int64)
-    bei = torch.empty(E, dtype=torch.int64)
-    dst_ptr = torch.empty(V + 1, dtype=torch.int32)
-    dst_perm = torch.empty(E, dtype=torch.int32)
-    mol_ptr = torch.empty(B + 1, dtype=torch.int32)
+    specs = [((V,) + tuple(nd.shape[1:]), nd.dtype), ((E,) + tuple(ed.shape[1:]), ed.dtype), ((2, E), torch.int64),
+             ((E,), torch.int64), ((V,), torch.int64), ((E,), torch.int64), ((V + 1,), torch.int32),
+             ((E,), torch.int32), ((B + 1,), torch.int32)]
+    sizes = [int(np.prod(sh, dtype=np.int64)) * torch.empty(0, dtype=dt).element_size() for sh, dt in specs]
+    if out is not None and min(sizes) > 0 and sum((n + 63) // 64 * 64 for n in sizes) <= out.numel():
+        outs, o = [], 0  # pack()'s layout: the graph's fields, then dst_ptr, dst_perm, mol_ptr, 64-B aligned
+        for (sh, dt), n in zip(specs, sizes):
+            outs.append(out[o:o + n].view(dt).view(sh))
+            o += (n + 63) // 64 * 64
+    else:
+        outs = [torch.empty(sh, dtype=dt) for sh, dt in specs]
+    node_out, edge_out, edge_index, rev_index, bni, bei, dst_ptr, dst_perm, mol_ptr = outs
     gp = [np.ascontiguousarray(a) for a in gptrs]
     lib = _lib.load()
     _lib.check(lib.nt_collate_graphs(

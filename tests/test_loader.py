@@ -101,3 +101,46 @@ def test_pinned_in_order_keeps_order_and_raises():
     it = pinned_in_order(range(1000), 2, slow)
     assert next(it) == 0
     it.close()  # the feeder stops and the pool shuts down
+
+
+def test_slot_ring_worker_batches_equal_main_process_collate():
+    """Workers pack into SlotRing slots and ship only offsets (data/loader.py SlotBatch): the batch
+    rebuilt over the ring equals from_graphs in the main process; slots are held until released; a
+    batch larger than a slot takes the shared-memory path."""
+    from notorch_amd.data.loader import SlotBatch, SlotRing
+
+    graphs = make_batch("qm9", 96, seed=3).to_graphs()
+    nbytes = BatchedGraph.from_graphs(graphs[:32]).packed_nbytes()
+    ring = SlotRing(2, 3, nbytes * 3 // 2)
+    dl = torch.utils.data.DataLoader(graphs, batch_size=32, collate_fn=GraphCollator("nodes", ring), num_workers=2)
+    got = list(dl)
+    assert all(isinstance(b, SlotBatch) for b in got)
+    assert sorted(b.slot for b in got) == sorted({b.slot for b in got})  # distinct slots: none released yet
+    assert ring.flags.sum().item() == 3
+    for i, b in enumerate(got):
+        G = b.load(ring)
+        _same(G, BatchedGraph.from_graphs(graphs[32 * i:32 * (i + 1)], "nodes"))
+        assert G._packed_base() is not None and G._layout_types_ok()
+        base = ring.slot(b.slot).data_ptr()
+        assert all(base <= t.data_ptr() < base + ring.slot_bytes for t in G.tensors())
+        ring.release(b.slot)
+    assert ring.flags.sum().item() == 0
+    # slots too small: the ordinary shared-memory batch
+    small = SlotRing(1, 2, 4096)
+    (G,) = list(torch.utils.data.DataLoader(graphs[:32], batch_size=32, collate_fn=GraphCollator("nodes", small),
+                                            num_workers=1))
+    assert isinstance(G, BatchedGraph) and small.flags.sum().item() == 0
+    _same(G, BatchedGraph.from_graphs(graphs[:32], "nodes"))
+    # the collate outputs fit the slot but the plans do not: every tensor moved out, slot freed
+    G0 = BatchedGraph.from_graphs(graphs[:32], "nodes")
+    nine = [G0.node_feats, G0.edge_feats, G0.edge_index, G0.rev_index, G0.batch_node_index, G0.batch_edge_index,
+            G0._nt_layout.dst_ptr, G0._nt_layout.dst_perm, G0._nt_layout.mol_ptr]
+    tight = SlotRing(1, 1, sum((t.numel() * t.element_size() + 63) // 64 * 64 for t in nine) + 64)
+    assert tight.slot_bytes < G0.packed_nbytes()
+    (G,) = list(torch.utils.data.DataLoader(graphs[:32], batch_size=32, collate_fn=GraphCollator("nodes", tight),
+                                            num_workers=1))
+    assert isinstance(G, BatchedGraph) and tight.flags.sum().item() == 0
+    _same(G, G0)
+    # no free slot within the timeout: also the ordinary path
+    ring.flags.fill_(1)
+    assert ring.acquire(0, timeout_s=0.01) == -1

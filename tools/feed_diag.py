@@ -15,7 +15,9 @@ sys.path.insert(0, ROOT)
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--workers", type=int, default=8)
-    p.add_argument("--pin-threads", type=int, default=4)
+    p.add_argument("--pin-threads", type=int, default=0)
+    p.add_argument("--ring-slots", type=int, default=3)
+    p.add_argument("--profile", action="store_true")
     a = p.parse_args()
     import torch
 
@@ -34,10 +36,11 @@ def main():
     graphs = make_batch("qm9", 4096, seed=1000).to_graphs()
     W = a.workers
     warm, n = W * 2 + 4, 3 * W
-    out = {"workers": W, "pin_threads": a.pin_threads}
+    out = {"workers": W, "pin_threads": a.pin_threads, "ring_slots": a.ring_slots}
 
     def run_loader(model: bool):
-        loader = graph_loader(graphs * (warm + n), 4096, dev, num_workers=W, pin_threads=a.pin_threads)
+        loader = graph_loader(graphs * (warm + n), 4096, dev, num_workers=W, pin_threads=a.pin_threads,
+                              ring_slots=a.ring_slots)
         it = iter(loader)
         with torch.no_grad():
             for _ in range(warm):
@@ -66,6 +69,16 @@ def main():
         del loader, it
         return {"ms_per_batch": t / k * 1e3, "next_ms": t_next / k * 1e3, "enqueue_ms": t_fwd / k * 1e3, "batches": k}
 
+    # (a0) the workers alone: DataLoader without pinning or device copies
+    dl = torch.utils.data.DataLoader(graphs * (warm + n), batch_size=4096, collate_fn=GraphCollator(),
+                                     num_workers=W, persistent_workers=True, prefetch_factor=2)
+    it = iter(dl)
+    for _ in range(warm):
+        next(it)
+    t0 = time.perf_counter()
+    k = sum(1 for _ in it)
+    out["a0_workers_only"] = {"ms_per_batch": (time.perf_counter() - t0) / k * 1e3, "batches": k}
+    del it, dl
     out["a_loader_only"] = run_loader(False)
     # (b) fresh batches from pinned host buffers, no workers
     coll = GraphCollator()
@@ -83,6 +96,20 @@ def main():
             torch.cuda.synchronize(dev)
             t = time.perf_counter() - t0
         out["b_pinned_fresh"] = {"ms_per_batch": t / 24 * 1e3, "enqueue_ms": t_enq / 24 * 1e3}
+        if a.profile:
+            import cProfile
+            import io
+            import pstats
+
+            pr = cProfile.Profile()
+            pr.enable()
+            for i in range(24):
+                readout(enc(_copy_to(hosts[i % 4], dev)))
+            pr.disable()
+            torch.cuda.synchronize(dev)
+            sio = io.StringIO()
+            pstats.Stats(pr, stream=sio).sort_stats("tottime").print_stats(30)
+            print(sio.getvalue(), flush=True)
         # resident: the same device batch again
         G = _copy_to(hosts[0], dev)
         for _ in range(5):
