@@ -526,12 +526,13 @@ def end_to_end_leg(res, dev):
             "total_ms": total, "value": job.E * job.depth / (total * 1e-3), "unit": "edge-messages/s"}
 
 
-def pipeline_leg(res, dev, workers, prefetch=2):
+def pipeline_leg(res, dev, workers, prefetch=3):
     """Steady-state host feed: per-molecule Graphs -> DataLoader workers (native collate, CSR and
     tile plan) -> pinned batches -> H2D on a side stream overlapped with the previous batch's
-    EmbeddedChempropBlock + Sum (notorch_amd.data.loader.graph_loader).  The DataLoader dispatches
-    workers x prefetch batches at once; the timed batches start after that many (+ 4) have been
-    consumed, so they are collated at the workers' steady rate, not drained from the initial burst."""
+    EmbeddedChempropBlock + Sum (notorch_amd.data.loader.graph_loader: GraphFeeder workers collating
+    into a page-locked slot ring).  The workers fill workers x slots batches ahead; the timed batches
+    start after that many (+ 4) have been consumed, so they are collated at the workers' steady rate,
+    not drained from the initial burst."""
     from notorch_amd.data.loader import graph_loader
     from notorch_amd.nn import EmbeddedChempropBlock
 
@@ -542,7 +543,7 @@ def pipeline_leg(res, dev, workers, prefetch=2):
     n_batches = warm + 3 * workers
     dataset = graphs * n_batches  # the same molecules every batch (references, no copies)
     enc = EmbeddedChempropBlock(res["embedding"], res["block"], fuse=True).eval()
-    loader = graph_loader(dataset, B, dev, num_workers=workers, prefetch_factor=prefetch)
+    loader = graph_loader(dataset, B, dev, num_workers=workers, ring_slots=prefetch)
     with torch.no_grad():
         it = iter(loader)
         for _ in range(warm):
@@ -555,12 +556,14 @@ def pipeline_leg(res, dev, workers, prefetch=2):
             n += 1
         torch.cuda.synchronize(dev)
         t = (time.perf_counter() - t0) / max(n, 1)
+    if hasattr(loader.batches, "close"):
+        loader.batches.close()
     del loader, it
     device_ms = res["secs"] / res["steps"] / len(res["jobs"]) * 1e3
-    return {"step": f"{B} host Graphs per batch -> DataLoader({workers} workers, native collate, "
-                    "pin_memory) -> side-stream non_blocking H2D overlapped with the previous batch's "
-                    "EmbeddedChempropBlock + Sum; steady state over "
-                    f"{n} batches after {warm} (workers x prefetch + 4: the initial burst consumed)",
+    return {"step": f"{B} host Graphs per batch -> GraphFeeder({workers} forked workers, native collate "
+                    f"into {prefetch} page-locked ring slots each) -> side-stream DMA overlapped with the "
+                    "previous batch's EmbeddedChempropBlock + Sum; steady state over "
+                    f"{n} batches after {warm} (workers x slots + 4: the initial burst consumed)",
             "workers": workers, "ms_per_batch": t * 1e3,
             "device_step_ms": device_ms, "ratio_to_device_step": t * 1e3 / device_ms,
             "value": job.E * job.depth / t, "unit": "edge-messages/s"}

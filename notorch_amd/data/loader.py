@@ -19,9 +19,13 @@ Here:
 * ``BatchedGraph.pin_memory()`` runs on a small thread pool of the main process
   (``DevicePrefetcher(pin_threads=...)``; the DataLoader's own pin thread with ``pin_threads=0``).
 * :class:`DevicePrefetcher` issues batch i+1's copies (``non_blocking``) on a side stream while the
-  caller's stream computes on batch i; the caller's stream waits on the copy's event before it
-  touches the batch, and every moved tensor is recorded on the caller's stream for the caching
-  allocator.
+  caller's stream computes on batch i (from a thread of its own by default, so that receiving and
+  issuing a batch does not delay the caller's kernel launches); the caller's stream waits on the
+  copy's event before it touches the batch, and every moved tensor is recorded on the caller's
+  stream for the caching allocator.
+* :class:`SlotRing` (the default with workers): page-locked shared-memory slots the workers
+  collate straight into; a batch crosses the worker queue as a few KB of offsets and goes to the
+  device by DMA from the slot, which is reused once that copy has completed.
 """
 from __future__ import annotations
 
@@ -48,7 +52,7 @@ class SlotRing:
         n = workers * per_worker
         self.buf = torch.empty(0, dtype=torch.uint8).set_(
             torch.UntypedStorage._new_shared(n * self.slot_bytes), 0, (n * self.slot_bytes,), (1,))
-        self.flags = torch.zeros(n, dtype=torch.int32).share_memory_()
+        self.flags = torch.zeros(n, dtype=torch.int64).share_memory_()
         self.registered = False
 
     def slot(self, s: int) -> torch.Tensor:
@@ -115,11 +119,12 @@ class SlotBatch:
         self.slot, self.blob = slot, blob
 
     @staticmethod
-    def pack(G: BatchedGraph, ring: SlotRing, s: int) -> "SlotBatch":
+    def pack(G: BatchedGraph, ring: SlotRing, s: int, out: Optional[torch.Tensor] = None) -> "SlotBatch":
+        """out: the part of slot s to pack into (default: all of it)."""
         import io
         import pickle
 
-        G.pack(out=ring.slot(s))
+        G.pack(out=ring.slot(s) if out is None else out)
         base = ring.slot(s).data_ptr()
         end = base + ring.slot_bytes
 
@@ -235,12 +240,13 @@ class DevicePrefetcher:
     loader yields them."""
 
     def __init__(self, batches: Iterable[BatchedGraph], device: torch.device | str, pin_threads: int = 0,
-                 ring: Optional[SlotRing] = None):
+                 ring: Optional[SlotRing] = None, background: bool = False):
         self.batches = batches
         self.device = torch.device(device)
         self.stream = torch.cuda.Stream(self.device)
         self.pin_threads = pin_threads
         self.ring = ring
+        self.background = background
         self._held: list = []  # (event, slot): ring slots whose device copy may still be running
 
     def _release_done(self, wait: bool = False) -> None:
@@ -279,27 +285,72 @@ class DevicePrefetcher:
         return dev, ev
 
     def __iter__(self) -> Iterator[BatchedGraph]:
+        idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
         if self.pin_threads > 0:
-            idx = self.device.index if self.device.index is not None else torch.cuda.current_device()
             it = pinned_in_order(self.batches, self.pin_threads, _pin, idx)
         else:
             it = iter(self.batches)  # (forks the DataLoader's workers: the ring is registered after)
         if self.ring is not None:
             self.ring.register()
+        src = self._background(it, idx) if self.background else self._inline(it)
         try:
-            nxt = self._issue(it)
-            while nxt is not None:
-                G, ev = nxt
+            for G, ev in src:
                 cur = torch.cuda.current_stream(self.device)
                 cur.wait_event(ev)
                 buf = G._packed_base()  # the allocator must not reuse these before the consumer is done
                 for t in ([buf] if buf is not None else G.tensors()):
                     t.record_stream(cur)
-                nxt = self._issue(it)  # the next batch's copies overlap this batch's compute
                 yield G
         finally:
+            src.close()
             if self.ring is not None:
                 self._release_done(wait=True)
+
+    def _inline(self, it):
+        nxt = self._issue(it)
+        while nxt is not None:
+            cur = nxt
+            nxt = self._issue(it)  # the next batch's copies overlap this batch's compute
+            yield cur
+
+    def _background(self, it, idx: int):
+        """_issue on a thread of its own, two batches ahead: the consumer thread only waits on a queue,
+        so its kernel launches do not queue behind the loader's bookkeeping and the H2D issue."""
+        import queue
+        import threading
+
+        q: queue.Queue = queue.Queue(maxsize=2)
+        stop = threading.Event()
+        end = object()
+
+        def produce():
+            torch.cuda.set_device(idx)
+            try:
+                while not stop.is_set():
+                    nxt = self._issue(it)
+                    q.put(end if nxt is None else nxt)
+                    if nxt is None:
+                        return
+            except BaseException as e:  # re-raised by the consumer
+                q.put(e)
+
+        t = threading.Thread(target=produce, daemon=True, name="nt_h2d_feed")
+        t.start()
+        try:
+            while True:
+                item = q.get()
+                if item is end:
+                    return
+                if isinstance(item, BaseException):
+                    raise item
+                yield item
+        finally:
+            stop.set()
+            while t.is_alive():  # unblock a producer waiting on a full queue
+                try:
+                    q.get_nowait()
+                except queue.Empty:
+                    t.join(timeout=0.01)
 
 
 def graph_loader(
@@ -313,6 +364,10 @@ def graph_loader(
     prefetch_factor: int = 2,
     pin_threads: int = 0,
     ring_slots: int = 3,
+    background: bool = False,
+    feeder: bool = True,
+    generator: Optional[torch.Generator] = None,
+    drop_last: bool = False,
     **kwargs,
 ) -> DevicePrefetcher:
     """DataLoader (workers collate) wrapped in a :class:`DevicePrefetcher`.
@@ -320,10 +375,22 @@ def graph_loader(
     ring_slots > 0 (and workers): batches travel through a page-locked :class:`SlotRing` of
     `ring_slots` slots per worker, sized from the first batch (x 1.5); a batch that does not fit, or
     finds no free slot, takes the path below.  Otherwise each batch is one shared-memory buffer, pinned
-    by the DataLoader's pin thread (pin_threads = 0) or by `pin_threads` threads of the main process."""
+    by the DataLoader's pin thread (pin_threads = 0) or by `pin_threads` threads of the main process.
+    background: receive batches and issue their H2D copies on a thread of the prefetcher's own.
+    feeder (with workers and ring slots, no other DataLoader arguments): the DataLoader-free
+    :class:`notorch_amd.data.feeder.GraphFeeder` instead of a torch DataLoader."""
     from notorch_amd import _lib
 
     _lib.load()  # load the collate library before the workers fork
+    if feeder and ring_slots > 0 and num_workers > 0 and not kwargs and len(dataset) > 0 and torch.cuda.is_available():
+        from notorch_amd.data.feeder import META_BYTES, GraphFeeder
+
+        first = BatchedGraph.from_graphs([dataset[i] for i in range(min(batch_size, len(dataset)))], rev_offset)
+        slot = first.packed_nbytes() * 3 // 2 + (1 << 16)
+        if first.packed_nbytes() > 0 and SlotRing.fits(num_workers * ring_slots * (slot + META_BYTES)):
+            f = GraphFeeder(dataset, batch_size, num_workers, ring_slots, rev_offset, shuffle, drop_last, generator,
+                            slot_bytes=slot)
+            return DevicePrefetcher(f, device, ring=f.ring, background=background)
     ring = None
     if ring_slots > 0 and num_workers > 0 and len(dataset) > 0 and torch.cuda.is_available():
         first = BatchedGraph.from_graphs([dataset[i] for i in range(min(batch_size, len(dataset)))], rev_offset)
@@ -336,14 +403,14 @@ def graph_loader(
     # with the ring, batches arrive page-locked (a batch that missed a slot is pinned in _issue): no
     # DataLoader pin thread, whose hand-off costs the consumer thread time per batch
     pin = pin_threads == 0 and ring is None
-    if not shuffle and not kwargs and isinstance(dataset, (list, tuple)):
+    if not shuffle and not drop_last and not kwargs and isinstance(dataset, (list, tuple)):
         # sequential batches as slices: the index queue carries one range per batch instead of
         # batch_size ints, and a worker fetches its graphs with one slice
         dl = torch.utils.data.DataLoader(_Slices(dataset, batch_size), batch_size=None, pin_memory=pin, **common)
     else:
         dl = torch.utils.data.DataLoader(dataset, batch_size=batch_size, shuffle=shuffle, pin_memory=pin, **common,
-                                         **kwargs)
-    return DevicePrefetcher(dl, device, pin_threads=pin_threads, ring=ring)
+                                         generator=generator, drop_last=drop_last, **kwargs)
+    return DevicePrefetcher(dl, device, pin_threads=pin_threads, ring=ring, background=background)
 
 
 class _Slices(torch.utils.data.Dataset):

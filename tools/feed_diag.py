@@ -18,6 +18,7 @@ def main():
     p.add_argument("--pin-threads", type=int, default=0)
     p.add_argument("--ring-slots", type=int, default=3)
     p.add_argument("--profile", action="store_true")
+    p.add_argument("--inline", action="store_true", help="issue H2D on the consumer thread")
     a = p.parse_args()
     import torch
 
@@ -35,12 +36,12 @@ def main():
     readout = Sum()
     graphs = make_batch("qm9", 4096, seed=1000).to_graphs()
     W = a.workers
-    warm, n = W * 2 + 4, 3 * W
-    out = {"workers": W, "pin_threads": a.pin_threads, "ring_slots": a.ring_slots}
+    warm, n = W * 3 + 4, 3 * W
+    out = {"workers": W, "pin_threads": a.pin_threads, "ring_slots": a.ring_slots, "background": not a.inline}
 
     def run_loader(model: bool):
         loader = graph_loader(graphs * (warm + n), 4096, dev, num_workers=W, pin_threads=a.pin_threads,
-                              ring_slots=a.ring_slots)
+                              ring_slots=a.ring_slots, background=not a.inline)
         it = iter(loader)
         with torch.no_grad():
             for _ in range(warm):
@@ -66,6 +67,8 @@ def main():
                 k += 1
             torch.cuda.synchronize(dev)
             t = time.perf_counter() - t0
+        if hasattr(loader.batches, "close"):
+            loader.batches.close()
         del loader, it
         return {"ms_per_batch": t / k * 1e3, "next_ms": t_next / k * 1e3, "enqueue_ms": t_fwd / k * 1e3, "batches": k}
 
