@@ -46,10 +46,11 @@ def test_graph_feeder_epochs_early_stop_and_shuffle():
 
     graphs = make_batch("qm9", 300, seed=6).to_graphs()
     loader = graph_loader(graphs, 64, DEV, num_workers=3, ring_slots=2)
-    assert loader.ring is not None and loader.ring.registered
+    assert loader.ring is not None
     for stop in (2, None):
         got = []
         for G in loader:
+            assert loader.ring.registered  # page-locked after the workers forked (hipHostRegister)
             got.append(G)
             if stop is not None and len(got) == stop:
                 break

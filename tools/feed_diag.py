@@ -18,7 +18,7 @@ def main():
     p.add_argument("--pin-threads", type=int, default=0)
     p.add_argument("--ring-slots", type=int, default=3)
     p.add_argument("--profile", action="store_true")
-    p.add_argument("--inline", action="store_true", help="issue H2D on the consumer thread")
+    p.add_argument("--background", action="store_true", help="issue H2D on the prefetcher's own thread")
     a = p.parse_args()
     import torch
 
@@ -37,11 +37,11 @@ def main():
     graphs = make_batch("qm9", 4096, seed=1000).to_graphs()
     W = a.workers
     warm, n = W * 3 + 4, 3 * W
-    out = {"workers": W, "pin_threads": a.pin_threads, "ring_slots": a.ring_slots, "background": not a.inline}
+    out = {"workers": W, "pin_threads": a.pin_threads, "ring_slots": a.ring_slots, "background": a.background}
 
     def run_loader(model: bool):
         loader = graph_loader(graphs * (warm + n), 4096, dev, num_workers=W, pin_threads=a.pin_threads,
-                              ring_slots=a.ring_slots, background=not a.inline)
+                              ring_slots=a.ring_slots, background=a.background)
         it = iter(loader)
         with torch.no_grad():
             for _ in range(warm):
