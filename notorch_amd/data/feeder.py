@@ -103,6 +103,9 @@ class GraphFeeder:
         self.epoch = 0
         self.procs: list = []
         self.conns: list = []
+        # called while the consumer polls for a batch: DevicePrefetcher frees the slots whose copies
+        # finished (a worker may be waiting for one of them to write the very batch polled for)
+        self.on_wait = None
 
     def __len__(self) -> int:
         n = len(self.dataset)
@@ -172,6 +175,8 @@ class GraphFeeder:
                     yield payload
                     break
                 spins += 1
+                if self.on_wait is not None:
+                    self.on_wait()
                 if spins % 4096 == 0 and not self.procs[w].is_alive():
                     raise RuntimeError(f"GraphFeeder worker {w} died (exit code {self.procs[w].exitcode})")
                 time.sleep(1e-5)

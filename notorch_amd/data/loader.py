@@ -248,6 +248,8 @@ class DevicePrefetcher:
         self.ring = ring
         self.background = background
         self._held: list = []  # (event, slot): ring slots whose device copy may still be running
+        if ring is not None and hasattr(batches, "on_wait"):
+            batches.on_wait = self._release_done
 
     def _release_done(self, wait: bool = False) -> None:
         keep = []
