@@ -174,7 +174,7 @@ __device__ __forceinline__ void fw_split(St<NCT, PREC>& st, const Args& a, int s
       asm volatile("" : "+v"(x));
       const _Float16 t0 = (_Float16)x;
       h0[4 * uu + c] = t0;
-      h1[4 * uu + c] = (_Float16)(x - (float)t0);
+      h1[4 * uu + c] = fk::lo_part(x, t0);
     }
   }
   *reinterpret_cast<f16x8*>(base) = h0;

@@ -81,6 +81,10 @@
 #ifndef FK_EPI4
 #define FK_EPI4 0
 #endif
+// FK_PRIO2 (A/B builds): 1 = s_setprio 1 for the second workgroup of each CU in the two-workgroup walk
+#ifndef FK_PRIO2
+#define FK_PRIO2 0
+#endif
 // FK_GATHER2 (A/B builds): 1 = 64-B contiguous row reads per gather instruction (fp32, 128-row tiles)
 #ifndef FK_GATHER2
 #define FK_GATHER2 0
@@ -187,6 +191,16 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 __device__ __forceinline__ f16x8 as_f16x8(uint4 v) { return __builtin_bit_cast(f16x8, v); }
+
+// Low fp16 part of the split x = x0 + x1 (x0 = fp16(x)), stored as x1 x 2^11 so that it stays a
+// normal fp16 for every x down to fp16's normal range (|x| >= 2^-14, 2^-28 of the scaled max 2^14):
+// unscaled, x1 ~ 2^-11 x fell into fp16's subnormals for |x| < 2^-3, so rows far below the tensor's
+// max (one split scale per tensor) lost their low part.  x - x0 and the x 2^11 are exact in fp32.
+#ifndef FK_LOSCALE
+#define FK_LOSCALE 1  // A/B: 0 = the rounds 1-5 unscaled low part (x - x0, W0 on its product)
+#endif
+constexpr float kLoScale = FK_LOSCALE ? 2048.f : 1.f;
+__device__ __forceinline__ _Float16 lo_part(float x, _Float16 x0) { return (_Float16)((x - (float)x0) * kLoScale); }
 
 // compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>), so register
 // arrays are only ever indexed by constants (a dynamic index would put them in scratch)
@@ -366,7 +380,7 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC, NW>& st, const 
       for (int c = 0; c < 4; ++c) {
         const _Float16 t0 = (_Float16)x[4 * u + c];
         h0[c] = t0;
-        h1[c] = (_Float16)(x[4 * u + c] - (float)t0);
+        h1[c] = lo_part(x[4 * u + c], t0);
       }
       char* dst = tb + (2 * u + (st.g16 >> 1)) * 256;
       *reinterpret_cast<f16x4*>(dst) = h0;
@@ -381,7 +395,7 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC, NW>& st, const 
     for (int c = 0; c < 8; ++c) {
       const _Float16 t0 = (_Float16)x[c];
       h0[c] = t0;
-      h1[c] = (_Float16)(x[c] - (float)t0);
+      h1[c] = lo_part(x[c], t0);
     }
     *reinterpret_cast<f16x8*>(base) = h0;
     *reinterpret_cast<f16x8*>(base + St::kPartB) = h1;
@@ -391,7 +405,7 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC, NW>& st, const 
     for (int c = 0; c < 4; ++c) {
       const _Float16 t0 = (_Float16)x[c];
       h0[c] = t0;
-      h1[c] = (_Float16)(x[c] - (float)t0);
+      h1[c] = lo_part(x[c], t0);
     }
     *reinterpret_cast<f16x4*>(base) = h0;
     *reinterpret_cast<f16x4*>(base + St::kPartB) = h1;
@@ -419,7 +433,22 @@ __device__ __forceinline__ void fk_load_w(State<RT, CT, GD, PREC, NW>& st, int c
   }
 }
 
-// one (row tile, column tile) k-step: fp32 = the three split products, bf16 = one bf16 MFMA
+// W0 x 2^-11 in fp16 (exact unless the product is subnormal, i.e. |W0| < 2^-17 of the scaled max:
+// such a weight's error term is below 2^-36 of the row's own scale): the operand of the scaled low
+// part of A.  Volatile asm: one copy per use, so the compiler neither merges the (row tile, column
+// tile) copies nor keeps 4 more registers per column tile live across the row tiles.
+__device__ __forceinline__ f16x8 w0_lo_scaled(uint4 w) {
+  const unsigned k = 0x10001000u;  // two fp16 2^-11
+  uint4 r;
+  asm volatile("v_pk_mul_f16 %0, %1, %2" : "=v"(r.x) : "v"(w.x), "s"(k));
+  asm volatile("v_pk_mul_f16 %0, %1, %2" : "=v"(r.y) : "v"(w.y), "s"(k));
+  asm volatile("v_pk_mul_f16 %0, %1, %2" : "=v"(r.z) : "v"(w.z), "s"(k));
+  asm volatile("v_pk_mul_f16 %0, %1, %2" : "=v"(r.w) : "v"(w.w), "s"(k));
+  return as_f16x8(r);
+}
+
+// one (row tile, column tile) k-step: fp32 = the three split products, bf16 = one bf16 MFMA.  a1 is
+// the scaled low part A1 x 2^11 (lo_part), so its product takes W0 x 2^-11: W1 A0 + W0 A1 + W0 A0.
 template <int PREC>
 __device__ __forceinline__ f32x4 fk_mac(uint4 w0r, uint4 w1r, f16x8 a0, f16x8 a1, f32x4 t) {
   if constexpr (PREC == 1) {
@@ -428,7 +457,7 @@ __device__ __forceinline__ f32x4 fk_mac(uint4 w0r, uint4 w1r, f16x8 a0, f16x8 a1
   } else {
     const f16x8 w0 = as_f16x8(w0r), w1 = as_f16x8(w1r);
     t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, a0, t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a1, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(FK_LOSCALE ? w0_lo_scaled(w0r) : w0, a1, t, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a0, t, 0, 0, 0);
   }
 }
@@ -1032,6 +1061,10 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   if (ntl <= 0) return;
   auto tile = [&](int i) __attribute__((always_inline)) { return t0 + (i < ntl ? i : ntl - 1) * tstride; };
   if constexpr (NW == 4) {
+#if FK_PRIO2
+    // A/B: static priority 1 for the second half of the grid (the second workgroup of each CU)
+    if ((int)blockIdx.x >= (int)gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
+#endif
     // two workgroups per CU: the second half of the grid (the second workgroup of each CU, which the
     // XCD walk also gives the smaller tile count) starts `stagger` x 8k cycles late, so the pair's
     // K loops and epilogues start out of phase (A/B: NT_FK_STAGGER)

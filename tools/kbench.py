@@ -48,6 +48,7 @@ def main():
     out = torch.empty_like(H)
     H2 = torch.randn(E, h, device="cuda", generator=gen)
     S2 = torch.empty_like(S)
+    R = torch.empty(len(G), h, device="cuda")
     relu = K.act_code(torch.nn.ReLU())
     amax = torch.zeros(2, device="cuda")
     K.absmax(H, amax[0:1])
@@ -98,6 +99,7 @@ def main():
                                                   row_table=plans[128][1], out=out, S_out=S2),
         "init_only": lambda: K.dmpnn_init(Xv, H, src, act=relu, amax=amax_out),
         # bandwidth ceilings of the init's traffic: E-row copy (2 rows / edge), E-row add (3 rows / edge)
+        "readout": lambda: K.segment_reduce(S, lay.mol_ptr, None, len(G), out=R),
         "copy": lambda: out.copy_(H),
         "add": lambda: torch.add(H, H2, out=out),
         "absmax": lambda: K.absmax(H, amax_out[0:1]),
