@@ -50,52 +50,8 @@ __global__ void __launch_bounds__(256) segment_reduce_vec4(
 }
 
 // One wave per segment (rows of >= 32 pieces): the segment bounds and the row indices are
-// wave-uniform scalar loads, lane l takes row pieces l + 64 q (q < PPL).  The rows go in batches of 8
-// (or 4 when at most 4 are left) with all their loads in flight and every load unconditional (rows
-// past the segment re-read its last row, pieces past the row read piece 0, both unused), so the
-// compiler's vmcnt waits stay counted and a segment of up to 8 rows -- a QM9 molecule's nodes in the
-// Sum readout, 4 and 8 in the round-5 kernel -- costs one round trip; pushed in ascending order: the
-// same bits as segment_reduce_vec4.
-template <int N, bool PERM, int R, int ACT, int PPL>
-__device__ __forceinline__ void seg_wave_batch(const float4* __restrict__ X, const int32_t* __restrict__ perm,
-                                               int32_t j, int32_t cnt, int64_t hv, const int64_t (&cc)[PPL],
-                                               int act, float alpha, Reducer4<R> (&r)[PPL]) {
-  float4 x[N][PPL];
-#pragma unroll
-  for (int u = 0; u < N; ++u) {
-    const int32_t ju = j + (u < cnt ? u : cnt - 1);
-    const int64_t row = PERM ? (int64_t)perm[ju] : (int64_t)ju;
-#pragma unroll
-    for (int q = 0; q < PPL; ++q) x[u][q] = X[row * hv + cc[q]];
-  }
-#pragma unroll
-  for (int u = 0; u < N; ++u)
-    if (u < cnt) {
-#pragma unroll
-      for (int q = 0; q < PPL; ++q) r[q].push(act4_t<ACT>(x[u][q], act, alpha));
-    }
-}
-
-#ifndef NT_SEG_RB8
-#define NT_SEG_RB8 1  // A/B: 0 = batches of 4 rows only (the round-5 kernel's round trips)
-#endif
-template <bool PERM, int R, int ACT, int PPL>
-__device__ __forceinline__ void seg_wave_rows(const float4* __restrict__ X, const int32_t* __restrict__ perm,
-                                              int32_t b, int32_t e, int64_t hv, const int64_t (&cc)[PPL], int act,
-                                              float alpha, Reducer4<R> (&r)[PPL]) {
-  for (int32_t j = b; j < e;) {
-    const int32_t left = e - j;  // wave-uniform
-    if (NT_SEG_RB8 && left > 4) {
-      const int32_t cnt = left < 8 ? left : 8;
-      seg_wave_batch<8, PERM, R, ACT, PPL>(X, perm, j, cnt, hv, cc, act, alpha, r);
-      j += cnt;
-    } else {
-      seg_wave_batch<4, PERM, R, ACT, PPL>(X, perm, j, left, hv, cc, act, alpha, r);
-      j += left;
-    }
-  }
-}
-
+// wave-uniform scalar loads, lane l takes row pieces l + 64 q (q < PPL), four rows in flight, pushed
+// in ascending order -- the same bits as segment_reduce_vec4.  Pieces past the row load nothing.
 template <int R, int ACT, int PPL>
 __global__ void __launch_bounds__(256) segment_reduce_wave(
     const float4* __restrict__ X, const int32_t* __restrict__ seg_ptr, const int32_t* __restrict__ perm,
@@ -116,8 +72,28 @@ __global__ void __launch_bounds__(256) segment_reduce_wave(
         cc[q] = ok[q] ? c : 0;
         r[q].init();
       }
-      if (perm) seg_wave_rows<true, R, ACT, PPL>(X, perm, b, e, hv, cc, act, alpha, r);
-      else seg_wave_rows<false, R, ACT, PPL>(X, perm, b, e, hv, cc, act, alpha, r);
+      int32_t j = b;
+      for (; j + 4 <= e; j += 4) {
+        int64_t row[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) row[u] = perm ? (int64_t)perm[j + u] : (int64_t)(j + u);
+        float4 x[4][PPL];
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < PPL; ++q)
+            x[u][q] = ok[q] ? X[row[u] * hv + cc[q]] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int q = 0; q < PPL; ++q) r[q].push(act4_t<ACT>(x[u][q], act, alpha));
+      }
+      for (; j < e; ++j) {
+        const int64_t row = perm ? (int64_t)perm[j] : (int64_t)j;
+#pragma unroll
+        for (int q = 0; q < PPL; ++q)
+          r[q].push(act4_t<ACT>(ok[q] ? X[row * hv + cc[q]] : make_float4(0.f, 0.f, 0.f, 0.f), act, alpha));
+      }
 #pragma unroll
       for (int q = 0; q < PPL; ++q)
         if (ok[q]) out[s * hv + cc[q]] = r[q].result();

@@ -81,10 +81,6 @@
 #ifndef FK_EPI4
 #define FK_EPI4 0
 #endif
-// FK_PRIO2 (A/B builds): 1 = s_setprio 1 for the second workgroup of each CU in the two-workgroup walk
-#ifndef FK_PRIO2
-#define FK_PRIO2 0
-#endif
 // FK_GATHER2 (A/B builds): 1 = 64-B contiguous row reads per gather instruction (fp32, 128-row tiles)
 #ifndef FK_GATHER2
 #define FK_GATHER2 0
@@ -1061,10 +1057,6 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   if (ntl <= 0) return;
   auto tile = [&](int i) __attribute__((always_inline)) { return t0 + (i < ntl ? i : ntl - 1) * tstride; };
   if constexpr (NW == 4) {
-#if FK_PRIO2
-    // A/B: static priority 1 for the second half of the grid (the second workgroup of each CU)
-    if ((int)blockIdx.x >= (int)gridDim.x / 2) __builtin_amdgcn_s_setprio(1);
-#endif
     // two workgroups per CU: the second half of the grid (the second workgroup of each CU, which the
     // XCD walk also gives the smaller tile count) starts `stagger` x 8k cycles late, so the pair's
     // K loops and epilogues start out of phase (A/B: NT_FK_STAGGER)

@@ -167,3 +167,21 @@ def test_extreme_magnitude_operands_stay_finite():
     assert torch.isfinite(Hn).all() and torch.isfinite(Sn).all()
     assert_parity(Hn, rH, FP32_NORM_TOL, "H 1e36")
     assert_parity(Sn, rS, FP32_NORM_TOL, "S 1e36")
+
+
+@pytest.mark.parametrize("small", [1e-6, 1e-8])
+def test_dense_matmul_mixed_magnitude_rows(small):
+    """The backward's dA = G W (the layer kernel's dense mode, one per-tensor split scale for G): rows
+    of G `small` x the largest keep per-row fp32 accuracy (the scaled low part, update_fk.hpp
+    lo_part)."""
+    K = _K()
+    h, M = 300, 4096
+    g = torch.Generator().manual_seed(31)
+    rs = torch.where(torch.arange(M) % 2 == 0, torch.tensor(1.0), torch.tensor(small)).unsqueeze(1)
+    X = torch.randn(M, h, generator=g) * rs
+    W = torch.randn(h, h, generator=g) / h ** 0.5
+    out = K.dense_matmul(X.to(DEV), K.pack_weights(W.to(DEV))).cpu()
+    ref = X.double() @ W.double().t()
+    e = _row_rel_err(out, ref)
+    print(f"dense rows x{small:g}: per-row rel err max {e[1::2].max():.3e} (unit rows {e[0::2].max():.3e})")
+    assert e.max().item() <= 1e-5, f"per-row relative error {e.max():.3e}"
