@@ -14,8 +14,9 @@
 // kernels that produced them), W by s_W (stored in the image header by the pack kernel).  Three
 // v_mfma_f32_16x16x32_f16 products per k-step, W1 A0 + W0 A1 + W0 A0, accumulate in fp32; the
 // dropped W1 A1 term and the two split roundings are ~2^-22 relative: 8.6e-7 normalised from fp64 at
-// config 2, 2.7x the fp32 CPU oracle's 3.2e-7 (tests/test_gpu_numerics.py).  The scale is per tensor:
-// rows far below the tensor's max (< 1e-4 of it) lose the low part to fp16 subnormals.  Half the MFMA work of a bf16x6 split and
+// config 2, 2.7x the fp32 CPU oracle's 3.2e-7 (tests/test_gpu_numerics.py).  The scale is per tensor,
+// but the low part is stored x 2^11 (lo_part; its product takes W0 x 2^-11), so rows down to 2^-28 of
+// the scaled max keep both parts normal: per-row fp32 accuracy.  Half the MFMA work of a bf16x6 split and
 // two thirds of its operand bytes.  The residual row enters the accumulator scaled by s_A s_W while
 // the K loop runs; the epilogue multiplies by the exact inverse and adds the bias.
 //
