@@ -43,7 +43,7 @@ endif
 
 $(PYEXT): $(SRC_DIR)/host/collate_py.cpp
 	@mkdir -p $(dir $@)
-	g++ -O2 -std=c++17 -shared -fPIC -Wall $(TORCH_FLAGS) $< -o $@ -ltorch_python -ltorch_cpu -lc10
+	g++ -O3 -std=c++17 -shared -fPIC -Wall $(TORCH_FLAGS) $< -o $@ -ltorch_python -ltorch_cpu -lc10
 
 $(BDIR)/%.o: $(SRC_DIR)/%.hip $(HDRS)
 	@mkdir -p $(dir $@)

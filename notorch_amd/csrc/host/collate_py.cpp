@@ -19,6 +19,8 @@
 // The caller raises the reference's errors for 2-4 (graph.py _native_collate).
 #include <Python.h>
 
+#include <stdint.h>
+
 #include <ATen/ops/empty.h>
 #include <torch/csrc/autograd/python_variable.h>
 
@@ -55,7 +57,19 @@ PyObject* graph_arrays(PyObject*, PyObject* arg) {
   for (Py_ssize_t i = 0; i < B && status == 0; ++i) {
     PyObject* obj[4];
     int got = 0;
+    // dataclass graphs keep their fields in the instance dict: four dict lookups on interned names
+    // (attribute lookup first walks the type's MRO for descriptors); anything else, or a miss, takes
+    // the generic attribute lookup
+    PyObject** dictp = _PyObject_GetDictPtr(items[i]);
+    PyObject* dict = dictp ? *dictp : nullptr;
     for (; got < 4; ++got) {
+      PyObject* v = dict ? PyDict_GetItemWithError(dict, g_names[got]) : nullptr;
+      if (v) {
+        Py_INCREF(v);
+        obj[got] = v;
+        continue;
+      }
+      if (PyErr_Occurred()) PyErr_Clear();
       obj[got] = PyObject_GetAttr(items[i], g_names[got]);
       if (!obj[got]) break;
     }
@@ -111,9 +125,49 @@ PyObject* graph_arrays(PyObject*, PyObject* arg) {
   return r;
 }
 
+// The layout's dst-sorted node ids and degree range (graph.py host_stats) in one pass instead of
+// numpy's diff / repeat / max / min chain.
+bool cpu_contig(PyObject* arg, at::ScalarType st, const at::Tensor** out) {
+  if (!THPVariable_Check(arg)) return false;
+  const at::Tensor& t = THPVariable_Unpack(arg);
+  if (!t.device().is_cpu() || !t.is_contiguous() || t.scalar_type() != st) return false;
+  *out = &t;
+  return true;
+}
+
+// segment_ids(seg_ptr: int32[n + 1] CPU) -> (ids int32[seg_ptr[n]], max count, min count): ids[p] = the
+// segment holding position p (np.repeat(arange(n), diff(seg_ptr))); None for a non-monotone pointer
+PyObject* segment_ids(PyObject*, PyObject* arg) {
+  const at::Tensor* t;
+  if (!cpu_contig(arg, at::kInt, &t) || t->dim() != 1 || t->numel() < 1) {
+    PyErr_SetString(PyExc_TypeError, "segment_ids expects a contiguous int32 CPU tensor of n + 1 >= 1 offsets");
+    return nullptr;
+  }
+  const int32_t* sp = t->data_ptr<int32_t>();
+  const int64_t n = t->numel() - 1;
+  if (sp[0] != 0) Py_RETURN_NONE;
+  for (int64_t v = 0; v < n; ++v)
+    if (sp[v + 1] < sp[v]) Py_RETURN_NONE;
+  at::Tensor ids = at::empty({(int64_t)sp[n]}, at::kInt);
+  int32_t* __restrict__ o = ids.data_ptr<int32_t>();
+  int64_t mx = 0, mn = n > 0 ? INT64_MAX : 0;
+  int32_t b = sp[0];
+  for (int64_t v = 0; v < n; ++v) {
+    const int32_t e = sp[v + 1];
+    const int64_t c = e - b;
+    mx = c > mx ? c : mx;
+    mn = c < mn ? c : mn;
+    for (int32_t p = b; p < e; ++p) o[p] = (int32_t)v;
+    b = e;
+  }
+  return Py_BuildValue("(NLL)", THPVariable_Wrap(ids), (long long)mx, (long long)mn);
+}
+
 PyMethodDef kMethods[] = {
     {"graph_arrays", graph_arrays, METH_O,
      "graph_arrays(graphs) -> (status, n_nodes, n_edges, ptrs, V, E): the native collate's per-graph inputs"},
+    {"segment_ids", segment_ids, METH_O,
+     "segment_ids(seg_ptr int32) -> (ids int32, max count, min count), or None if seg_ptr is not monotone"},
     {nullptr, nullptr, 0, nullptr}};
 
 PyModuleDef kModule = {PyModuleDef_HEAD_INIT, "_collate_py", "host helper of the native collate", -1, kMethods};

@@ -658,15 +658,34 @@ def host_tile_ptr(dst_ptr: np.ndarray, E: int, stride: int, hub_degree: int = 0,
 
 
 def host_tile_plan(dst_ptr: np.ndarray, E: int, max_in_degree: int, rows: int = 64, ncu: int = 0,
-                   hub_degree: int = 0):
+                   hub_degree: int = 0, dsts: Optional[Tensor] = None):
     """(tile_ptr[ntiles+1], ntiles, dst_sorted[E]) exactly as nt_dmpnn_tile_plan (hub_degree > 0:
     nt_dmpnn_tile_plan_hubs) builds them with the stride of nt_dmpnn_tile_stride(E, max_in_degree,
     rows, ncu)."""
     stride = host_tile_stride(E, max_in_degree, rows, ncu) if E > 0 else 1
     tile_ptr, ntiles = host_tile_ptr(dst_ptr, E, stride, hub_degree, rows)
-    counts = np.diff(dst_ptr.astype(np.int64))
-    dsts = np.repeat(np.arange(len(counts), dtype=np.int32), counts)
-    return tile_ptr, ntiles, torch.from_numpy(dsts)
+    return tile_ptr, ntiles, _segment_ids(dst_ptr)[0] if dsts is None else dsts
+
+
+def _segment_ids(seg_ptr: np.ndarray) -> tuple:
+    """(ids int32 tensor: position -> segment, max count, min count) of a CSR offset array: one C++ pass
+    through the collate helper when it is built and seg_ptr is int32, else numpy."""
+    fast = _collate_py()
+    if fast is not None and seg_ptr.dtype == np.int32 and seg_ptr.flags.c_contiguous:
+        r = fast.segment_ids(torch.from_numpy(seg_ptr))
+        if r is not None:
+            return r
+    counts = np.diff(seg_ptr.astype(np.int64))
+    ids = np.repeat(np.arange(len(counts), dtype=np.int32), counts)
+    return torch.from_numpy(ids), (int(counts.max()) if counts.size else 0), (int(counts.min()) if counts.size else 0)
+
+
+def _minmax(X: Tensor) -> Optional[tuple]:
+    """(min, max) of a CPU int64 tensor (None when empty; numpy's vectorised reductions)."""
+    if X.numel() == 0:
+        return None
+    xn = X.numpy()
+    return int(xn.min()), int(xn.max())
 
 
 def host_chunk_plan(seg_ptr: np.ndarray, chunk: int = CHUNK_ROWS):
@@ -693,20 +712,22 @@ def host_chunk_plan(seg_ptr: np.ndarray, chunk: int = CHUNK_ROWS):
 def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional[np.ndarray],
                node_feats: Optional[Tensor] = None, edge_feats: Optional[Tensor] = None) -> None:
     """Fill the layout's host statistics and plans from the host CSR (one O(V + E) pass)."""
-    deg = np.diff(dst_ptr.astype(np.int64))
-    lay.deg_range = (int(deg.max()), int(deg.min())) if deg.size else (0, 0)
-    V = len(deg)
+    V = len(dst_ptr) - 1
+    dsts, dmax, dmin = _segment_ids(dst_ptr)  # dst node of every dst-sorted position, degree range
+    lay.deg_range = (dmax, dmin) if V > 0 else (0, 0)
     maxdeg, mindeg = lay.deg_range
     hub = 0
     lay.hubs = False
     if E > 0 and V > 0 and maxdeg > MAX_FUSED_IN_DEGREE:  # hubs: cut at the stride (fp32 plans)
+        deg = np.diff(dst_ptr.astype(np.int64))
         is_hub = deg > HUB_CUT_DEGREE
         ids = np.nonzero(is_hub)[0].astype(np.int32)
         rest = deg[~is_hub]
         lay.hubs = (torch.from_numpy(ids), int(ids.size), int(rest.max()) if rest.size else 0)
         hub, maxdeg = HUB_CUT_DEGREE, lay.hubs[2]
     if E > 0 and V > 0:
-        tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg, rows=64, ncu=PLAN_SLOTS64, hub_degree=hub)
+        tile_ptr, ntiles, dsts = host_tile_plan(dst_ptr, E, maxdeg, rows=64, ncu=PLAN_SLOTS64, hub_degree=hub,
+                                                dsts=dsts)
         lay.plan = (tile_ptr, ntiles, dsts, mindeg == 0)
         lay.plan_wide = host_tile_ptr(dst_ptr, E, host_tile_stride(E, maxdeg, WIDE_TILE_ROWS, PLAN_NCU), hub,
                                       WIDE_TILE_ROWS)
@@ -721,8 +742,8 @@ def host_stats(lay: DeviceLayout, dst_ptr: np.ndarray, E: int, mol_ptr: Optional
     tr = []
     for X in (node_feats, edge_feats):
         if X is not None and X.dim() == 2 and X.dtype == torch.int64 and X.device.type == "cpu":
-            xn = X.numpy()
-            tr.append((int(xn.min()), int(xn.max())) if X.numel() else (0, -1))
+            r = _minmax(X)
+            tr.append(r if r is not None else (0, -1))
         else:
             tr.append(None)
     lay.type_range = tuple(tr)

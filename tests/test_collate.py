@@ -261,3 +261,26 @@ def test_collate_helper_walk_matches_python_walk():
             BatchedGraph.from_graphs(case)
     with pytest.raises(TypeError):
         fast.graph_arrays(3)
+
+
+def test_segment_ids_helper_matches_numpy():
+    """The collate helper's segment_ids (dst-sorted node ids + degree range, graph.py host_stats) equals
+    numpy's repeat / diff, with empty segments, an empty pointer and a non-monotone pointer (None)."""
+    import numpy as np
+
+    from notorch_amd.data.models import graph as gm
+
+    fast = gm._collate_py()
+    if fast is None:
+        pytest.skip("collate helper not built")
+    rng = np.random.default_rng(5)
+    for counts in (rng.integers(0, 5, 1000), np.zeros(7, dtype=np.int64), np.array([3]), np.array([], dtype=np.int64)):
+        sp = np.zeros(len(counts) + 1, dtype=np.int32)
+        np.cumsum(counts, out=sp[1:])
+        ids, mx, mn = fast.segment_ids(torch.from_numpy(sp))
+        assert ids.dtype == torch.int32
+        assert np.array_equal(ids.numpy(), np.repeat(np.arange(len(counts), dtype=np.int32), counts))
+        assert (mx, mn) == ((int(counts.max()), int(counts.min())) if len(counts) else (0, 0))
+    assert fast.segment_ids(torch.tensor([0, 3, 2], dtype=torch.int32)) is None
+    ids, mx, mn = gm._segment_ids(np.array([0, 2, 2, 5], dtype=np.int32))
+    assert ids.tolist() == [0, 0, 2, 2, 2] and (mx, mn) == (3, 0)
