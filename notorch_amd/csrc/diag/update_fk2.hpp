@@ -273,7 +273,6 @@ __global__ void __launch_bounds__(kThreads, 2) update_fk2_kernel(Args a) {
   st.kp0 = tid & 7;    // its 16-B piece of the 32-deep k-step
   st.hv = a.hv;
   st.hc = a.hv;
-  st.rtabl = 0;
   st.NT = a.NT;
   st.CTC = 8 * CT;
   st.KS = a.KS;

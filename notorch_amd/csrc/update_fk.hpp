@@ -41,52 +41,6 @@
 
 #include "common.hpp"
 
-// FK_MFMA_MODE (A/B builds): 0 = per-(row tile, column tile) guarded MFMAs; 1 = branch-free steps
-// (column-tile count switched once per step, every row tile computed); 2 = every wave computes all
-// CT column tiles and all row tiles (no branch at all)
-#ifndef FK_MFMA_MODE
-#define FK_MFMA_MODE 0
-#endif
-// FK_EPI2 (A/B builds): 1 = the sum-only aggregation scan with bound-control DPP and fma selects
-#ifndef FK_EPI2
-#define FK_EPI2 0
-#endif
-// FK_PRIO (A/B builds): 1 = s_setprio 1 for waves 4-7 for the whole loop
-#ifndef FK_PRIO
-#define FK_PRIO 0
-#endif
-#ifndef FK_RTABL
-#define FK_RTABL 0
-#endif
-// FK_DEPHASE (A/B builds): 1 = waves 4-7 run each k-step's split before its MFMAs
-#ifndef FK_DEPHASE
-#define FK_DEPHASE 0
-#endif
-#ifndef FK_AMAX_BLOCK
-#define FK_AMAX_BLOCK 1  // A/B: 0 = one atomic pair per wave for the amax chain
-#endif
-// FK_EPI3: the epilogue of 128-row tiles staged through LDS (see fk_epilogue3)
-#ifndef FK_EPI3
-#define FK_EPI3 0
-#endif
-// FK_STAMP (A/B builds): coarse s_memtime stamps (each right after a barrier or around the epilogue,
-// where no LDS / SMEM op is outstanding, so they cost little): per wave and launch the K-loop cycles,
-// the epilogue cycles and the first two k-steps of each unit (the tile-boundary drain), summed into
-// g_pk_stamps[0..3] (+ wave count at [4]); read by nt_debug_fk_stamps
-#ifndef FK_STAMP
-#define FK_STAMP 0
-#endif
-// FK_EPI4 (A/B): the node sums of the two-workgroup 64-row walk from a per-wave LDS stage
-// (fk_epilogue4) instead of the DPP scan -- bit-identical, measured slower (124.0 vs 118.3 us at
-// config 2: the node pass diverges and the scan's VALU is not what binds this walk)
-#ifndef FK_EPI4
-#define FK_EPI4 0
-#endif
-// FK_GATHER2 (A/B builds): 1 = 64-B contiguous row reads per gather instruction (fp32, 128-row tiles)
-#ifndef FK_GATHER2
-#define FK_GATHER2 0
-#endif
-
 namespace nt {
 namespace fk {
 
@@ -151,8 +105,9 @@ struct Args {
   float* SP = nullptr;  // hub partial rows (slots x h fp32), written at the end rows of kFlagPart sub-runs
   int nxcd;
   int stagger;  // diagnostic: start delay of workgroup b = stagger * ((b / nxcd) % 4) x 8k cycles (0)
-  int rtabl;    // FK_RTABL builds only (timing ablations, results invalid): 1 gathers read row 0, 2 W reads
-                // block 0, 4 no H_out / S_out stores, 8 residual reads row 0, 32 no aggregation scan
+#ifdef NT_DIAG
+  int rtabl = 0;  // diagnostic library: the fw walk's timing ablations (NT_FK_RTABL, results invalid)
+#endif
 };
 
 // power-of-two scale that maps a magnitude bound to < 2^14 (exponent at most 24; every finite
@@ -193,10 +148,7 @@ __device__ __forceinline__ f16x8 as_f16x8(uint4 v) { return __builtin_bit_cast(f
 // normal fp16 for every x down to fp16's normal range (|x| >= 2^-14, 2^-28 of the scaled max 2^14):
 // unscaled, x1 ~ 2^-11 x fell into fp16's subnormals for |x| < 2^-3, so rows far below the tensor's
 // max (one split scale per tensor) lost their low part.  x - x0 and the x 2^11 are exact in fp32.
-#ifndef FK_LOSCALE
-#define FK_LOSCALE 1  // A/B: 0 = the rounds 1-5 unscaled low part (x - x0, W0 on its product)
-#endif
-constexpr float kLoScale = FK_LOSCALE ? 2048.f : 1.f;
+constexpr float kLoScale = 2048.f;
 __device__ __forceinline__ _Float16 lo_part(float x, _Float16 x0) { return (_Float16)((x - (float)x0) * kLoScale); }
 
 // compile-time loop: f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>), so register
@@ -288,13 +240,8 @@ struct State {
                                                            // hc: 4-column output pieces per row
   int li, lo;  // row pitches in 4-column pieces: input (residual H), output (H_out, S_out)
   float sA, sAW, inv;
-  int rtabl;  // FK_RTABL builds: Args::rtabl
   char* abuf;
-  float* stage;  // FK_EPI3: 128-row x 128-column output staging (pitch kSP floats); FK_EPI4: this wave's
-                 // column-tile stage (RT x 16 rows x 16 columns, pitch kSP4)
-  float* lbias;  // FK_EPI3: the bias in fp32 (h floats), loaded once
-  int* nlist;    // FK_EPI3: node segments of the current tile (start rows, count at [kNlistN]); FK_EPI4:
-                 // this wave's copy
+  float* lbias;  // 4-wave workgroups: the bias in fp32 (h floats) in LDS, loaded once
   int4* emap;
   __amdgpu_buffer_rsrc_t wrsrc;
 };
@@ -312,13 +259,7 @@ __device__ __forceinline__ void fk_gather(State<RT, CT, GD, PREC, NW>& st, const
   constexpr int NP = PREC ? 1 : State<RT, CT, GD, PREC, NW>::PPT;
 #pragma unroll
   for (int u = 0; u < NP; ++u) {
-#if FK_GATHER2
-    // fp32 128-row tiles: lanes g16 = 0..3 of a row read 64 contiguous bytes per instruction
-    // (pieces g16 and g16 + 4) instead of 16-B pieces at a 32-B stride
-    int p = PREC ? 4 * s + st.g16 : (RT == 8 ? 8 * s + st.g16 + 4 * u : 8 * s + st.kp0 + u);
-#else
     int p = PREC ? 4 * s + st.g16 : 8 * s + st.kp0 + u;
-#endif
     p = p < st.hv ? p : 0;
     st.gs[P][u] = S4[sb + p];
     st.gq[P][u] = H4[qb + p];
@@ -350,11 +291,7 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC, NW>& st, const 
   float x[4 * St::PPT];
 #pragma unroll
   for (int u = 0; u < St::PPT; ++u) {
-#if FK_GATHER2
-    const bool in = (RT == 8 ? 8 * s + st.g16 + 4 * u : 8 * s + st.kp0 + u) < st.hv;
-#else
     const bool in = 8 * s + st.kp0 + u < st.hv;
-#endif
     const f32x4 sv = st.gs[P][u];
     const f32x4 qv = st.gq[P][u];
 #pragma unroll
@@ -366,26 +303,6 @@ __device__ __forceinline__ void fk_split(State<RT, CT, GD, PREC, NW>& st, const 
   }
   char* base = st.abuf + BUF * St::kBufB + st.grt * 1024 + st.lane * 16 +
                (RT == NW ? 0 : 8 * (st.wave >> 2));
-#if FK_GATHER2
-  if constexpr (RT == 8) {
-    // piece u holds k = 16 u + 4 g16 .. + 3: fragment k-group 2 u + (g16 >> 1), half g16 & 1
-    char* tb = st.abuf + BUF * St::kBufB + st.grt * 1024 + st.fr * 16 + 8 * (st.g16 & 1);
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      f16x4 h0, h1;
-#pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        const _Float16 t0 = (_Float16)x[4 * u + c];
-        h0[c] = t0;
-        h1[c] = lo_part(x[4 * u + c], t0);
-      }
-      char* dst = tb + (2 * u + (st.g16 >> 1)) * 256;
-      *reinterpret_cast<f16x4*>(dst) = h0;
-      *reinterpret_cast<f16x4*>(dst + St::kPartB) = h1;
-    }
-    return;
-  }
-#endif
   if constexpr (St::PPT == 2) {
     f16x8 h0, h1;
 #pragma unroll
@@ -418,10 +335,7 @@ __device__ __forceinline__ void fk_load_w(State<RT, CT, GD, PREC, NW>& st, int c
     const int ct = c * st.CTC + st.wave + NW * j;
     // fp32: two parts per block behind the scale header; bf16: the plain bf16 image (one part)
     const int blk = PREC ? (s * st.NT + ct) * 1024 : kImgHdr + ((s * st.NT + ct) * 2) * 1024;
-    int soff = __builtin_amdgcn_readfirstlane(ct < st.NT ? blk : 0x7fff0000);
-#if FK_RTABL
-    if (st.rtabl & 2) soff = ct < st.NT ? (PREC ? 0 : kImgHdr) : 0x7fff0000;
-#endif
+    const int soff = __builtin_amdgcn_readfirstlane(ct < st.NT ? blk : 0x7fff0000);
     st.wb[P][j][0] = __builtin_bit_cast(
         uint4, __builtin_amdgcn_raw_buffer_load_b128(st.wrsrc, st.lane * 16, soff, 0));
     if constexpr (PREC == 0)
@@ -454,7 +368,7 @@ __device__ __forceinline__ f32x4 fk_mac(uint4 w0r, uint4 w1r, f16x8 a0, f16x8 a1
   } else {
     const f16x8 w0 = as_f16x8(w0r), w1 = as_f16x8(w1r);
     t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w1, a0, t, 0, 0, 0);
-    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(FK_LOSCALE ? w0_lo_scaled(w0r) : w0, a1, t, 0, 0, 0);
+    t = __builtin_amdgcn_mfma_f32_16x16x32_f16(w0_lo_scaled(w0r), a1, t, 0, 0, 0);
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(w0, a0, t, 0, 0, 0);
   }
 }
@@ -488,59 +402,6 @@ __device__ __forceinline__ void fk_mfma(State<RT, CT, GD, PREC, NW>& st, int c, 
   }
 }
 
-// Branch-free MFMA step: NCT (compile time) active column tiles for this wave, and every row tile
-// of the tile computed (rows past the tile hold zeros in the A buffer, so their accumulators keep
-// whatever they held and are never stored).  One scalar branch per step (the NCT switch) instead of
-// one per (row tile, column tile).
-template <int RT, int CT, int P, int GD, int NCT, int PREC, int NW>
-__device__ __forceinline__ void fk_mfma_nb(State<RT, CT, GD, PREC, NW>& st) {
-  using St = State<RT, CT, GD, PREC, NW>;
-  const char* bb = st.abuf + P * St::kBufB + st.lane * 16;
-  f16x8 a0 = *reinterpret_cast<const f16x8*>(bb);
-  f16x8 a1 = PREC ? a0 : *reinterpret_cast<const f16x8*>(bb + St::kPartB);
-#pragma unroll
-  for (int rt = 0; rt < RT; ++rt) {
-    f16x8 n0 = a0, n1 = a1;
-    if (rt + 1 < RT) {
-      n0 = *reinterpret_cast<const f16x8*>(bb + (rt + 1) * 1024);
-      n1 = PREC ? n0 : *reinterpret_cast<const f16x8*>(bb + St::kPartB + (rt + 1) * 1024);
-    }
-#pragma unroll
-    for (int j = 0; j < NCT; ++j) {
-      st.acc[rt][j] = fk_mac<PREC>(st.wb[P][j][0], st.wb[P][j][1], a0, a1, st.acc[rt][j]);
-    }
-    a0 = n0;
-    a1 = n1;
-    __builtin_amdgcn_sched_barrier(0);
-  }
-}
-
-template <int RT, int CT, int P, int GD, int PREC, int NW>
-__device__ __forceinline__ void fk_mfma_sw(State<RT, CT, GD, PREC, NW>& st, int c, int nrt) {
-#if FK_MFMA_MODE == 2
-  // every wave runs all CT column tiles (past NT the W fragments read zeros): one straight-line
-  // MFMA block per step, no per-wave branch
-  (void)c;
-  (void)nrt;
-  fk_mfma_nb<RT, CT, P, GD, CT>(st);
-#elif FK_MFMA_MODE == 1
-  // active column tiles of this wave in chunk c (wave-uniform)
-  const int first = c * st.CTC + st.wave;
-  const int nct = first >= st.NT ? 0 : min(CT, (st.NT - first + NW - 1) / NW);
-  if constexpr (CT >= 4) {
-    if (nct == 4) { fk_mfma_nb<RT, CT, P, GD, 4>(st); return; }
-  }
-  if constexpr (CT >= 3) {
-    if (nct == 3) { fk_mfma_nb<RT, CT, P, GD, 3>(st); return; }
-  }
-  if (nct == 2) { fk_mfma_nb<RT, CT, P, GD, 2>(st); return; }
-  if (nct == 1) { fk_mfma_nb<RT, CT, P, GD, 1>(st); return; }
-  (void)nrt;
-#else
-  fk_mfma<RT, CT, P, GD>(st, c, nrt);
-#endif
-}
-
 // Residual rows H[e] of (tile i, chunk c), column tile j, loaded straight into the accumulators:
 // issued by the epilogue of the previous (tile, chunk) as soon as it has stored column tile j, so
 // they land during the rest of that epilogue; fk_resid_scale multiplies them by s_A s_W before the
@@ -552,10 +413,7 @@ __device__ __forceinline__ void fk_resid_load(State<RT, CT, GD, PREC, NW>& st, c
   pc = pc < st.hc ? pc : 0;
 #pragma unroll
   for (int rt = 0; rt < RT; ++rt) {
-    int e = st.emap[(i % kEmaps) * St::ROWS + 16 * rt + st.fr].x;
-#if FK_RTABL
-    if (st.rtabl & 8) e = 0;
-#endif
+    const int e = st.emap[(i % kEmaps) * St::ROWS + 16 * rt + st.fr].x;
     const int64_t r = (int64_t)(e >= 0 ? e : 0) * st.li + pc;
     if constexpr (PREC == 1) {  // 4 bf16 (8 B), widened by fk_resid_scale once they have landed
       const uint2 v = reinterpret_cast<const uint2*>(a.H)[r];
@@ -607,11 +465,7 @@ __device__ __forceinline__ void fk_resid_scale(State<RT, CT, GD, PREC, NW>& st) 
 // scratch).
 // 4-wave workgroups keep the bias in LDS instead of CT registers per thread (their 5 column tiles
 // per wave leave no registers for it)
-// (FK_LB8 A/B: also the 8-wave 128-row fp32 walk, h <= 384 there)
-#ifndef FK_LB8
-#define FK_LB8 0
-#endif
-constexpr bool fk_lds_bias(int NW, int RT, int PREC) { return NW == 4 || (FK_LB8 && RT == 8 && PREC == 0); }
+constexpr bool fk_lds_bias(int NW) { return NW == 4; }
 
 struct EpiCtx {
   const f32x4* b4;
@@ -639,10 +493,7 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC, NW>& st, cons
 #pragma unroll
       for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[RTI][J][q], st.inv, bj[q]);
     }
-    bool rok = ri.x >= 0 && pok;
-#if FK_RTABL
-    if (st.rtabl & 4) rok = false;
-#endif
+    const bool rok = ri.x >= 0 && pok;
     if (rok && (ABL & 64) == 0) {
       if constexpr (PREC == 1) {
         reinterpret_cast<uint2*>(x0.O4)[(int64_t)ri.x * lo + pc] = ob;
@@ -651,11 +502,7 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC, NW>& st, cons
         st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
       }
     }
-#if FK_RTABL
-    if (x0.SO4 != nullptr && !(st.rtabl & 32)) {
-#else
     if (x0.SO4 != nullptr) {
-#endif
       // MAXL rounds of x[r] = start[r] ? m[r] : x[r - 1] + m[r] (the carry enters at row 0): a
       // row's value is final once the rounds cover its distance from its node's first row, at
       // most max in-degree - 1 (<= 16 within a row tile); extra rounds leave converged rows as they
@@ -669,25 +516,6 @@ __device__ __forceinline__ void fk_epi_row(State<RT, CT, GD, PREC, NW>& st, cons
       for (int q = 0; q < 4; ++q) cin[q] = dpp_ror1(carry[q]);
       float cnt = 1.f;
       const float cinc = SUMONLY ? 0.f : dpp_ror1(ccnt);
-#if FK_EPI2
-      if constexpr (SUMONLY) {
-        // the same left-to-right sums with fewer instructions: the carry enters lane 0's own term
-        // once (m0 = cin + m at a continuing lane 0), then every round is one bound-control DPP
-        // shift (lane 0 reads 0: no copy of an `old` operand) and one fma with keep = !start
-        // (fma(y, 1, m) = y + m and fma(y, 0, m) = m for finite y: the sums are bit-identical)
-        const float keep = start ? 0.f : 1.f;
-        const bool lane0 = st.fr == 0;
-        f32x4 mp;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) mp[q] = lane0 ? fmaf(cin[q], keep, m[q]) : m[q];
-        x = mp;
-#pragma unroll
-        for (int it = 0; it < MAXL; ++it) {
-#pragma unroll
-          for (int q = 0; q < 4; ++q) x[q] = fmaf(dpp_shr1_bc(x[q]), keep, mp[q]);
-        }
-      } else
-#endif
 #pragma unroll
       for (int it = 0; it < MAXL; ++it) {
         f32x4 y;
@@ -735,12 +563,12 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC, NW>& st, cons
     const int pc = 4 * ct + st.g16;
     const bool pok = pc < st.hc;
     f32x4 bj = f32x4{0.f, 0.f, 0.f, 0.f};
-    if constexpr (fk_lds_bias(NW, RT, PREC)) {  // the bias from LDS (copied once per workgroup): no registers
+    if constexpr (fk_lds_bias(NW)) {  // the bias from LDS (copied once per workgroup): no registers
       if (x0.b4 && pok) bj = *reinterpret_cast<const f32x4*>(st.lbias + 4 * pc);
     } else {
       if (x0.b4 && pok) bj = st.bias[J];
     }
-    if constexpr (PREC == 1 && !fk_lds_bias(NW, RT, PREC)) {  // the raw bf16 bias piece (zero bits stay zero)
+    if constexpr (PREC == 1 && !fk_lds_bias(NW)) {  // the raw bf16 bias piece (zero bits stay zero)
       const float4 w = bf4_widen(__builtin_bit_cast(uint4, bj));
       bj = f32x4{w.x, w.y, w.z, w.w};
     }
@@ -750,7 +578,7 @@ __device__ __forceinline__ void fk_epi_col(State<RT, CT, GD, PREC, NW>& st, cons
   }
   // column tile J is stored: its accumulators start the next (tile, chunk) (after the last tile the
   // loads re-read this tile's rows and go unused)
-  if (!fk_lds_bias(NW, RT, PREC) && c_next != c) fk_bias_load(st, a, c_next, J);  // column chunks: the next chunk's bias
+  if (!fk_lds_bias(NW) && c_next != c) fk_bias_load(st, a, c_next, J);  // column chunks: the next chunk's bias
   if (load_next) {
     fk_resid_load(st, a, i_next, c_next, J);
   } else {
@@ -773,248 +601,7 @@ __device__ __forceinline__ void fk_epilogue(State<RT, CT, GD, PREC, NW>& st, con
   fk_epi_col<0, RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, x0, i, c, load_next, i_next, c_next);
 }
 
-// --------------------------------------------------------------------------- LDS-staged epilogue
-// FK_EPI3 (128-row tiles): per group of 8 output column tiles (128 columns, one tile per wave) the
-// waves write their accumulators into a row-major LDS stage; then every thread takes whole 16-B row
-// pieces (piece p = tid & 31 of rows tid / 32 + 16 m): H_out = acc / s_A s_W + bias + H (the
-// residual read here as contiguous row pieces, so the accumulators start every tile at zero and no
-// load is pending across the tile boundary), stored as full 512-B row segments; the aggregated value
-// aact(H_out) goes back into the stage; then (node, piece) items reduce each node's consecutive
-// rows in order (bit-identical to the CPU scatter) and store S_out.  Three barriers per group.
-constexpr int kSP = 132;     // stage pitch in floats (128 + 4: conflict-free 16-B writes of 16 rows)
-constexpr int kNlistN = 132;  // node list: start rows [0, nseg], nseg at [kNlistN]
-constexpr int kStageB = 128 * kSP * 4;
-constexpr int kLbiasB = 512 * 4;
-constexpr int kNlistB = (kNlistN + 4) * 4;
-
-// residual pieces of group J for this thread's rows (piece tid & 31 of rows tid / 32 + 16 m)
-template <int J, int RT, int CT, int GD, int PREC, int NW>
-__device__ __forceinline__ void fk_epi3_resid(State<RT, CT, GD, PREC, NW>& st, const Args& a, const int4* em, int c,
-                                              f32x4 (&rr)[RT]) {
-  const int tid = threadIdx.x, p = tid & 31, rg = tid >> 5;
-  const int col = 16 * (c * st.CTC + 8 * J) + 4 * p;
-  const int pc = col < a.h ? col >> 2 : 0;
-#pragma unroll
-  for (int m = 0; m < RT; ++m) {
-    const int e = em[rg + 16 * m].x;
-    const int64_t r = (int64_t)(e >= 0 ? e : 0) * st.li + pc;
-    if constexpr (PREC == 1) {
-      const uint2 v = reinterpret_cast<const uint2*>(a.H)[r];
-      rr[m] = __builtin_bit_cast(f32x4, uint4{v.x, v.y, 0u, 0u});
-    } else {
-      rr[m] = reinterpret_cast<const f32x4*>(a.H)[r];
-    }
-  }
-}
-
-template <int J, int RT, int CT, int AACT, int GD, int PREC, int NW>
-__device__ __forceinline__ void fk_epi3_group(State<RT, CT, GD, PREC, NW>& st, const Args& a, const int4* em, int c, int n,
-                                              bool resid, f32x4 (&rr)[RT]) {
-  if constexpr (J < CT) {
-    const int cb = 16 * (c * st.CTC + 8 * J);  // first column of the group
-    if (cb < a.h) {
-      const int tid = threadIdx.x, p = tid & 31, rg = tid >> 5;
-      const int col = cb + 4 * p;
-      const bool pok = col < a.h;
-      const int pc = pok ? col >> 2 : 0;  // 4-column piece index in the row
-      // (A) this wave's column tile of the group into the stage
-      if (c * st.CTC + 8 * J + st.wave < st.NT) {
-#pragma unroll
-        for (int rt = 0; rt < RT; ++rt)
-          *reinterpret_cast<f32x4*>(st.stage + (16 * rt + st.fr) * kSP + 16 * st.wave + 4 * st.g16) = st.acc[rt][J];
-      }
-      // group 0's residual pieces now (its accumulators are dead); later groups' were issued during
-      // the previous group
-      if (J == 0 && resid) fk_epi3_resid<0>(st, a, em, c, rr);
-      __syncthreads();
-      if (J == 0 && a.SO != nullptr && st.wave == 0) {  // the tile's node segments (start rows)
-        const int l = st.lane;
-        const bool s0 = l < n && (em[l].z & kFlagStart), s1 = l + 64 < n && (em[l + 64].z & kFlagStart);
-        const unsigned long long m0 = __ballot(s0), m1 = __ballot(s1);
-        const unsigned long long below = (1ull << l) - 1ull;
-        const int c0 = __popcll(m0);
-        if (s0) st.nlist[__popcll(m0 & below)] = l;
-        if (s1) st.nlist[c0 + __popcll(m1 & below)] = l + 64;
-        if (l == 0) {
-          const int ns = c0 + __popcll(m1);
-          st.nlist[ns] = n;
-          st.nlist[kNlistN] = ns;
-        }
-      }
-      // (B) rows: H_out, and aact(H_out) back into the stage
-      const f32x4 b4 = (a.bias && pok) ? *reinterpret_cast<const f32x4*>(st.lbias + col) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int m = 0; m < RT; ++m) {
-        const int r = rg + 16 * m;
-        if (r < n && pok) {
-          const int e = em[r].x;
-          float* sp = st.stage + r * kSP + 4 * p;
-          const f32x4 v = *reinterpret_cast<const f32x4*>(sp);
-          f32x4 o;
-          if constexpr (PREC == 1) {
-            const float4 w = bf4_widen(__builtin_bit_cast(uint4, rr[m]));
-            const f32x4 h4 = resid ? f32x4{w.x, w.y, w.z, w.w} : f32x4{0.f, 0.f, 0.f, 0.f};
-            const uint2 ob = bf4_pack((v[0] + b4[0]) + h4[0], (v[1] + b4[1]) + h4[1], (v[2] + b4[2]) + h4[2],
-                                      (v[3] + b4[3]) + h4[3]);
-            reinterpret_cast<uint2*>(a.O)[(int64_t)e * st.lo + pc] = ob;
-            const float4 s4 = bf4_widen(uint4{ob.x, ob.y, 0u, 0u});
-            o = f32x4{s4.x, s4.y, s4.z, s4.w};
-          } else {
-#pragma unroll
-            for (int q = 0; q < 4; ++q) o[q] = fmaf(v[q], st.inv, b4[q]) + (resid ? rr[m][q] : 0.f);
-            reinterpret_cast<f32x4*>(a.O)[(int64_t)e * st.lo + pc] = o;
-            st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
-          }
-          if (a.SO != nullptr) {
-            f32x4 ag;
-#pragma unroll
-            for (int q = 0; q < 4; ++q) ag[q] = act_t<AACT>(o[q], a.aact, a.aalpha);
-            *reinterpret_cast<f32x4*>(sp) = ag;
-          }
-        }
-      }
-      // the next group's residual pieces, in flight across (C) and the next staging round trip
-      if constexpr (J + 1 < CT) {
-        if (resid && 16 * (c * st.CTC + 8 * (J + 1)) < a.h) fk_epi3_resid<J + 1>(st, a, em, c, rr);
-      }
-      if (a.SO != nullptr) {
-        __syncthreads();
-        // (C) nodes: each node's rows are consecutive in the tile; reduce them in order
-        const int ns = st.nlist[kNlistN];
-        for (int k = rg; k < ns; k += 16) {
-          const int r0 = st.nlist[k], r1 = st.nlist[k + 1];
-          if (pok && (em[r1 - 1].z & (kFlagEnd | kFlagPart)) == kFlagEnd) {  // (no hub partials here)
-            f32x4 x = *reinterpret_cast<const f32x4*>(st.stage + r0 * kSP + 4 * p);
-            for (int r = r0 + 1; r < r1; ++r) {
-              const f32x4 y = *reinterpret_cast<const f32x4*>(st.stage + r * kSP + 4 * p);
-              if (a.reduce == NT_MAX) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], y[q]);
-              } else if (a.reduce == NT_MIN) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) x[q] = fminf(x[q], y[q]);
-              } else {
-                x = x + y;
-              }
-            }
-            if (a.reduce == NT_MEAN) {
-              const float inv_n = 1.f / (float)(r1 - r0);
-              x = x * f32x4{inv_n, inv_n, inv_n, inv_n};
-            }
-            const int node = em[r0].y;
-            if constexpr (PREC == 1) {
-              reinterpret_cast<uint2*>(a.SO)[(int64_t)node * st.lo + pc] = bf4_pack(x[0], x[1], x[2], x[3]);
-            } else {
-              reinterpret_cast<f32x4*>(a.SO)[(int64_t)node * st.lo + pc] = x;
-              st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
-            }
-          }
-        }
-      }
-      if constexpr (J + 1 < CT) __syncthreads();  // the next group overwrites the stage
-    }
-    fk_epi3_group<J + 1, RT, CT, AACT, GD, PREC>(st, a, em, c, n, resid, rr);
-  }
-}
-
-template <int RT, int CT, int AACT, int GD, int PREC, int NW>
-__device__ __forceinline__ void fk_epilogue3(State<RT, CT, GD, PREC, NW>& st, const Args& a, int i, int c, int n,
-                                             bool resid) {
-  const int4* em = st.emap + (i % kEmaps) * State<RT, CT, GD, PREC, NW>::ROWS;
-  f32x4 rr[RT];
-  fk_epi3_group<0, RT, CT, AACT, GD, PREC>(st, a, em, c, n, resid, rr);
-}
-
-// --------------------------------------------------------------------------- LDS node reduction
-// FK_EPI4 (the two-workgroup 64-row walk, sum aggregation): per column tile J of the wave, the row
-// tiles' units store H_out and write aact(H_out) into the wave's own stage; then lanes take (node,
-// 4-column piece) items, 16 nodes x 4 pieces per round, and sum each node's consecutive rows left to
-// right (CPU scatter_add_ order: the same bits as the DPP scan), S_out as 16-B pieces.  No barrier:
-// each wave owns its stage and its copy of the tile's node list.  ~12 VALU + one ds_write per unit
-// against the scan's ~40 VALU.
-constexpr int kSP4 = 20;  // stage pitch (floats): conflict-free 16-B row writes
-constexpr int kNl4 = 68;  // node list ints per wave: start rows [0, ns], ns at [66]
-
-template <int J, int RT, int CT, int AACT, int GD, int PREC, int NW>
-__device__ __forceinline__ void fk_epi4_col(State<RT, CT, GD, PREC, NW>& st, const Args& a, const int4* em, int c,
-                                            int n, int ns, bool load_next, int i_next, int c_next) {
-  const int ct = c * st.CTC + st.wave + NW * J;
-  const int hc = st.hc;
-  if (ct < st.NT) {
-    const int pc = 4 * ct + st.g16;
-    const bool pok = pc < hc;
-    const f32x4 bj = (a.bias && pok) ? *reinterpret_cast<const f32x4*>(st.lbias + 4 * pc) : f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) {
-      if (16 * rt < n) {
-        f32x4 o;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) o[q] = fmaf(st.acc[rt][J][q], st.inv, bj[q]);
-        const int e = em[16 * rt + st.fr].x;
-        if (e >= 0 && pok) {
-          reinterpret_cast<f32x4*>(a.O)[(int64_t)e * st.lo + pc] = o;
-          st.mxH = fmaxf(st.mxH, fmaxf(fmaxf(fabsf(o[0]), fabsf(o[1])), fmaxf(fabsf(o[2]), fabsf(o[3]))));
-        }
-        f32x4 m;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) m[q] = act_t<AACT>(o[q], a.aact, a.aalpha);
-        *reinterpret_cast<f32x4*>(st.stage + (16 * rt + st.fr) * kSP4 + 4 * st.g16) = m;
-      }
-    }
-  }
-  // column tile J is out: its accumulators take the next (tile, chunk)'s residual rows, in flight
-  // across the node pass below
-  if (load_next) {
-    fk_resid_load(st, a, i_next, c_next, J);
-  } else {
-#pragma unroll
-    for (int rt = 0; rt < RT; ++rt) st.acc[rt][J] = f32x4{0.f, 0.f, 0.f, 0.f};
-  }
-  if (ct < st.NT) {
-    __builtin_amdgcn_wave_barrier();  // the stage rows come from other lanes of this wave (LDS keeps order)
-    const int p4 = st.lane & 3;
-    const int pcn = 4 * ct + p4;
-    for (int k = st.lane >> 2; k < ns; k += 16) {
-      const int r0 = st.nlist[k], r1 = st.nlist[k + 1];
-      f32x4 x = *reinterpret_cast<const f32x4*>(st.stage + r0 * kSP4 + 4 * p4);
-      for (int r = r0 + 1; r < r1; ++r) x = x + *reinterpret_cast<const f32x4*>(st.stage + r * kSP4 + 4 * p4);
-      const int4 re = em[r1 - 1];  // the node's last row: its id and end flag (hub rows carry none)
-      if ((re.z & (kFlagEnd | kFlagPart)) == kFlagEnd && re.x >= 0 && pcn < hc) {  // (no hub partials here)
-        reinterpret_cast<f32x4*>(a.SO)[(int64_t)re.y * st.lo + pcn] = x;
-        st.mxS = fmaxf(st.mxS, fmaxf(fmaxf(fabsf(x[0]), fabsf(x[1])), fmaxf(fabsf(x[2]), fabsf(x[3]))));
-      }
-    }
-    __builtin_amdgcn_wave_barrier();  // the next column tile rewrites the stage
-  }
-  if constexpr (J + 1 < CT)
-    fk_epi4_col<J + 1, RT, CT, AACT, GD, PREC, NW>(st, a, em, c, n, ns, load_next, i_next, c_next);
-}
-
-template <int RT, int CT, int AACT, int GD, int PREC, int NW>
-__device__ __forceinline__ void fk_epilogue4(State<RT, CT, GD, PREC, NW>& st, const Args& a, int i, int c, int n,
-                                             bool load_next, int i_next, int c_next) {
-  static_assert(RT * 16 <= 64, "FK_EPI4: tiles of at most 64 rows (one ballot)");
-  using St = State<RT, CT, GD, PREC, NW>;
-  const int4* em = st.emap + (i % kEmaps) * St::ROWS;
-  // the wave's stage and node list behind the bias (wave-uniform addresses)
-  char* e4 = st.abuf + 2 * St::kBufB + kEmaps * St::ROWS * 16 + kLbiasB;
-  st.stage = reinterpret_cast<float*>(e4 + st.wave * (16 * RT * kSP4 * 4));
-  st.nlist = reinterpret_cast<int*>(e4 + NW * (16 * RT * kSP4 * 4)) + st.wave * kNl4;
-  {  // the tile's node list: start rows of its nodes (ascending), ns = count, start[ns] = n
-    const int l = st.lane;
-    const bool s0 = l < n && (em[l].z & kFlagStart);
-    const unsigned long long m0 = __ballot(s0);
-    if (s0) st.nlist[__popcll(m0 & ((1ull << l) - 1ull))] = l;
-    if (l == 0) {
-      const int ns = __popcll(m0);
-      st.nlist[ns] = n;
-      st.nlist[66] = ns;
-    }
-  }
-  __builtin_amdgcn_wave_barrier();
-  const int ns = st.nlist[66];
-  fk_epi4_col<0, RT, CT, AACT, GD, PREC, NW>(st, a, em, c, n, ns, load_next, i_next, c_next);
-}
+constexpr int kLbiasB = 512 * 4;  // the bias in LDS (4-wave workgroups, h <= 512)
 
 __device__ __forceinline__ void fk_barrier() {
   // LDS writes of this step retired, then the workgroup barrier (vector-memory loads stay in flight)
@@ -1035,12 +622,8 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   constexpr int ROWS = St::ROWS;
   constexpr int kEmapB = kEmaps * ROWS * 16;
   static_assert(RT == NW || (RT == 4 && NW == 8), "row tiles per wave mapping");
-  constexpr bool EPI3 = FK_EPI3 && RT == 8 && NW == 8;
-  // FK_EPI4: the LDS node reduction on the two-workgroup 64-row walk (fp32, sum)
-  constexpr bool EPI4 = FK_EPI4 && NW == 4 && RT == 4 && PREC == 0 && SUMONLY && MAXL > 1;
-  constexpr bool LB = fk_lds_bias(NW, RT, PREC);
-  constexpr int kEpi4B = EPI4 ? NW * (16 * RT * kSP4 * 4 + kNl4 * 4) : 0;
-  constexpr int kExtraB = (EPI3 ? kStageB + kLbiasB + kNlistB : (LB ? kLbiasB : 0)) + kEpi4B;
+  constexpr bool LB = fk_lds_bias(NW);
+  constexpr int kExtraB = LB ? kLbiasB : 0;
   __shared__ __attribute__((aligned(16))) uint4 smem[(2 * St::kBufB + kEmapB + kExtraB) / 16];
 
   // XCD-aware persistent walk (blocks b and b + nxcd share an L2): each XCD one contiguous chunk
@@ -1081,16 +664,13 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   st.hc = a.h / 4;    // 4-column output pieces per row
   st.li = a.ldic;
   st.lo = a.ldoc;
-  st.rtabl = a.rtabl;
   st.NT = a.NT;
   st.CTC = NW * CT;
   st.abuf = reinterpret_cast<char*>(smem);
   st.emap = reinterpret_cast<int4*>(st.abuf + 2 * St::kBufB);
-  st.stage = reinterpret_cast<float*>(st.abuf + 2 * St::kBufB + kEmapB);
-  st.lbias = st.stage + (EPI3 ? kStageB / 4 : 0);
-  st.nlist = reinterpret_cast<int*>(st.lbias + (EPI3 ? kLbiasB / 4 : 0));
+  st.lbias = reinterpret_cast<float*>(st.abuf + 2 * St::kBufB + kEmapB);
 
-  if constexpr (EPI3 || LB) {  // the bias in fp32, once (h <= 512)
+  if constexpr (LB) {  // the bias in fp32, once (h <= 512)
     for (int q = tid; q < a.h; q += 64 * NW) {
       float b = 0.f;
       if (a.bias) {
@@ -1149,7 +729,7 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
 
   // ---- prologue: steps 0 and 1 staged, W of step 0, slice 0 split into buffer 0
   __syncthreads();  // emap of tiles 0 and 1
-  if (resid && !EPI3) {  // EPI3 reads the residual in the epilogue: the accumulators start at zero
+  if (resid) {
 #pragma unroll
     for (int j = 0; j < CT; ++j) fk_resid_load(st, a, 0, 0, j);
   }
@@ -1181,11 +761,6 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
   // gathers each step really needs: W two steps ahead and gathers three steps ahead stay in flight
   // across the MFMAs.  Every vector-memory op is unconditional.
   int i = 0, c = 0;  // tile-local index, column chunk
-#if FK_PRIO
-  // static priority for the second-dispatched half (waves 4-7: each SIMD's younger wave), which
-  // otherwise loses every issue arbitration against its partner (MI355X_MICROARCH, two waves per SIMD)
-  if (st.wave >= 4) __builtin_amdgcn_s_setprio(1);
-#endif
   const int U = ntl * a.nchunks;
   [[maybe_unused]] unsigned long long tacc[5] = {0, 0, 0, 0, 0}, tp = 0, tb = 0;
   if constexpr ((ABL & 256) != 0) tb = tp = __builtin_amdgcn_s_memtime();
@@ -1196,22 +771,11 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
       tp = t;
     }
   };
-  [[maybe_unused]] unsigned long long fs_k = 0, fs_e = 0, fs_f = 0, fs_t0 = 0, fs_t1 = 0;
   for (int u = 0; u < U; ++u) {
-#if FK_STAMP
-    fs_t0 = __builtin_amdgcn_s_memtime();
-#endif
     // (1) residual rows (loaded by the previous epilogue) into the accumulators' scale; without a
     // residual the accumulators are zero and the scale leaves them so.  Unconditional, so that no
     // path into the inner loop carries an accumulator load still pending.
-    if constexpr (EPI3) {  // accumulators restart at zero (dead across the staged epilogue)
-#pragma unroll
-      for (int rt = 0; rt < RT; ++rt)
-#pragma unroll
-        for (int j = 0; j < CT; ++j) st.acc[rt][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    } else {
-      fk_resid_scale(st);
-    }
+    fk_resid_scale(st);
     const int nrt = (n_cur + 15) >> 4;
     const int kb = c * a.KS;
     for (int s0 = 0; s0 < a.KS; s0 += 2) {
@@ -1221,8 +785,8 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
         auto phase_mfma = [&]() __attribute__((always_inline)) {
           // (2) MFMAs of step k
           if constexpr ((ABL & 2) == 0) {
-            if (P == 0) fk_mfma_sw<RT, CT, 0>(st, c, nrt);
-            else fk_mfma_sw<RT, CT, 1>(st, c, nrt);
+            if (P == 0) fk_mfma<RT, CT, 0>(st, c, nrt);
+            else fk_mfma<RT, CT, 1>(st, c, nrt);
           }
           stamp(0);
           // (3) W fragments of step k + 2 into the registers step k used
@@ -1248,51 +812,23 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
           const int s3 = (k3 - adv * SPT) % a.KS;
           int so = adv == 0 ? cur.x : nxt.x, qo = adv == 0 ? cur.y : nxt.y;
           if constexpr ((ABL & 1) != 0) so = qo = 0;
-#if FK_RTABL
-          if (st.rtabl & 1) so = qo = 0;
-#endif
           if (P == 0) fk_gather<RT, CT, ACT, 1>(st, a, so, qo, s3);
           else fk_gather<RT, CT, ACT, 0>(st, a, so, qo, s3);
           stamp(2);
         };
-#if FK_DEPHASE
-        // the two waves of a SIMD (w, w + 4) run the step's phases in opposite orders, so one
-        // wave's split VALU runs beside its partner's MFMAs instead of both contending for the
-        // matrix pipe and then both for the VALU
-        if (st.wave < 4) {
-          phase_mfma();
-          phase_split();
-        } else {
-          phase_split();
-          phase_mfma();
-        }
-#else
         phase_mfma();
         phase_split();
-#endif
         if constexpr ((ABL & 16) == 0) fk_barrier();
         stamp(3);
-#if FK_STAMP
-        if (s0 == 0 && P == 1) fs_f += __builtin_amdgcn_s_memtime() - fs_t0;
-#endif
       }
     }
     // (5) epilogue of the unit; it starts the next (tile, chunk)'s residual loads
-#if FK_STAMP
-    fs_t1 = __builtin_amdgcn_s_memtime();
-    fs_k += fs_t1 - fs_t0;
-#endif
     const bool last_c = c + 1 == a.nchunks;
     const int i_next = last_c ? (i + 1 < ntl ? i + 1 : i) : i, c_next = last_c ? 0 : c + 1;
     if constexpr ((ABL & 8) == 0) {
-      if constexpr (EPI3) fk_epilogue3<RT, CT, AACT, GD>(st, a, i, c, n_cur, resid);
-      else if constexpr (EPI4) fk_epilogue4<RT, CT, AACT, GD>(st, a, i, c, n_cur, resid, i_next, c_next);
-      else fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
+      fk_epilogue<RT, CT, AACT, SUMONLY, MAXL, GD, ABL>(st, a, i, c, n_cur, resid, i_next, c_next);
       stamp(4);
     }
-#if FK_STAMP
-    fs_e += __builtin_amdgcn_s_memtime() - fs_t1;
-#endif
     // (6) advance: tile i + 1 becomes current, tile i + 2's row (loaded a tile ago) is published
     c = c_next;
     if (last_c) {
@@ -1308,18 +844,8 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
       h3 = tile_head<RT, TABLE>(a, tile(i + 3));
     }
   }
-#if FK_STAMP
-  if (st.lane == 0) {
-    atomicAdd(&g_pk_stamps[0], fs_k);
-    atomicAdd(&g_pk_stamps[1], fs_e);
-    atomicAdd(&g_pk_stamps[2], fs_f);
-    atomicAdd(&g_pk_stamps[3], (unsigned long long)U);
-    atomicAdd(&g_pk_stamps[4], 1ull);
-  }
-#endif
   if (a.amax_out) {
     const float mh = wave_max(st.mxH), ms = wave_max(st.mxS);
-#if FK_AMAX_BLOCK
     // one atomic pair per workgroup (the waves' maxima through LDS): every wave of the workgroup ran
     // the same persistent loop, so all reach this barrier
     __shared__ float amx[2][NW];
@@ -1338,12 +864,6 @@ __global__ void __launch_bounds__(64 * NW, 2) update_fk_kernel(Args a) {
       atomic_max_abs(a.amax_out, bh);
       if (a.SO) atomic_max_abs(a.amax_out + 1, bs);
     }
-#else
-    if (st.lane == 0) {
-      atomic_max_abs(a.amax_out, mh);
-      if (a.SO) atomic_max_abs(a.amax_out + 1, ms);
-    }
-#endif
   }
 #ifdef NT_DIAG
   if constexpr ((ABL & 256) != 0) {

@@ -20,9 +20,9 @@
 
 namespace nt {
 
-#if defined(NT_DIAG) || FK_STAMP
-// diagnostic / stamp builds only (the shipping library holds no device state): stamp sums of the fk
-// (FK_STAMP, ABL 256) and fw (FW_STAMP) walks, read by nt_debug_fk_stamps / nt_debug_fw_stamps
+#ifdef NT_DIAG
+// diagnostic builds only (the shipping library holds no device state): stamp sums of the fk (ABL 256)
+// and fw (FW_STAMP) walks, read by nt_debug_fw_stamps
 __device__ unsigned long long g_pk_stamps[10];
 #endif
 
@@ -298,8 +298,6 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
              "tile plan rows exceed nt_dmpnn_fused_tile_rows for this layer");
   NT_REQUIRE(!fused || (max_in_degree >= 0 && max_in_degree <= 32), NT_EUNSUPPORTED,
              "fused aggregation needs max_in_degree <= 32");
-  NT_REQUIRE(u.S_part == nullptr || !(FK_EPI3 || FK_EPI4), NT_EUNSUPPORTED,
-             "FK_EPI3 / FK_EPI4 variant builds write no hub partials (S_part)");
   fk::Args a;
   a.H = u.H;
   a.S = u.S;
@@ -346,18 +344,19 @@ int launch_update_fk(const UpdateArgs& u, const void* Wimg, const float* amax_in
   a.SP = u.S_part;
   a.nxcd = xcd_count();
   {
-    // timing experiments only, read once per process: NT_FK_STAGGER (start delay of half the grid),
-    // NT_FK_RTABL (FK_RTABL builds: ablations)
+    // timing experiments only, read once per process: NT_FK_STAGGER (start delay of half the grid)
     static const int stagger = [] {
       const char* e = getenv("NT_FK_STAGGER");
       return e ? atoi(e) : 0;
     }();
+    a.stagger = stagger;
+#ifdef NT_DIAG
     static const int rtabl = [] {
       const char* e = getenv("NT_FK_RTABL");
       return e ? atoi(e) : 0;
     }();
-    a.stagger = stagger;
     a.rtabl = rtabl;
+#endif
   }
   a.ntiles = fused ? (int)ntiles : (int)((u.E + cap - 1) / cap);
   if (a.ntiles == 0) return NT_OK;
@@ -471,7 +470,6 @@ int launch_update_fk_bf16(const UpdateArgs& u, const void* Wimg, const int32_t* 
   a.SO = (float*)S_out;
   a.nxcd = xcd_count();
   a.stagger = 0;
-  a.rtabl = 0;
   a.ntiles = fused ? (int)ntiles : (int)((u.E + 127) / 128);
   if (a.ntiles == 0) return NT_OK;
   const int grid = a.ntiles < cu_count() ? a.ntiles : cu_count();
@@ -568,17 +566,6 @@ int amax_fill(float* ws, const float* H, int64_t nh, const float* S, int64_t ns,
 // A/B builds only (FW_STAMP): read and reset the fw kernel's stamp sums (6 values)
 extern "C" __attribute__((visibility("default"))) int nt_debug_fw_stamps(unsigned long long* out6) {
   if (hipMemcpyFromSymbol(out6, HIP_SYMBOL(nt::g_pk_stamps), 6 * sizeof(unsigned long long), 0,
-                          hipMemcpyDeviceToHost) != hipSuccess)
-    return 2;
-  unsigned long long z[10] = {0};
-  return hipMemcpyToSymbol(HIP_SYMBOL(nt::g_pk_stamps), z, sizeof(z), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : 2;
-}
-#endif
-
-#if FK_STAMP
-// A/B builds only (FK_STAMP): read and reset the fk kernel's coarse stamp sums
-extern "C" __attribute__((visibility("default"))) int nt_debug_fk_stamps(unsigned long long* out5) {
-  if (hipMemcpyFromSymbol(out5, HIP_SYMBOL(nt::g_pk_stamps), 5 * sizeof(unsigned long long), 0,
                           hipMemcpyDeviceToHost) != hipSuccess)
     return 2;
   unsigned long long z[10] = {0};
