@@ -284,3 +284,42 @@ def test_segment_ids_helper_matches_numpy():
     assert fast.segment_ids(torch.tensor([0, 3, 2], dtype=torch.int32)) is None
     ids, mx, mn = gm._segment_ids(np.array([0, 2, 2, 5], dtype=np.int32))
     assert ids.tolist() == [0, 0, 2, 2, 2] and (mx, mn) == (3, 0)
+
+
+def test_collate_helper_reads_fields_without_an_instance_dict():
+    """graph_arrays reads dataclass fields from the instance dict; objects whose fields are slots or
+    properties (duck-typed reference graphs) take the generic attribute lookup with the same result."""
+    from notorch_amd.data.models import graph as gm
+
+    fast = gm._collate_py()
+    if fast is None:
+        pytest.skip("collate helper not built")
+
+    class Slotted:
+        __slots__ = ("node_feats", "edge_feats", "edge_index", "rev_index")
+
+        def __init__(self, G):
+            self.node_feats, self.edge_feats, self.edge_index, self.rev_index = (
+                G.node_feats, G.edge_feats, G.edge_index, G.rev_index)
+
+    class Props:
+        def __init__(self, G):
+            self._g = G
+
+        node_feats = property(lambda self: self._g.node_feats)
+        edge_feats = property(lambda self: self._g.edge_feats)
+        edge_index = property(lambda self: self._g.edge_index)
+        rev_index = property(lambda self: self._g.rev_index)
+
+    Gs = make_batch("qm9", 12, seed=13).to_graphs()
+    ref = fast.graph_arrays(Gs)
+    for wrap in (Slotted, Props):
+        r = fast.graph_arrays([wrap(G) for G in Gs])
+        assert r[0] == 0 and r[4:] == ref[4:]
+        for x, y in zip(r[1:4], ref[1:4]):
+            assert torch.equal(x, y)
+
+    class Missing:
+        node_feats = edge_feats = edge_index = None
+
+    assert fast.graph_arrays([Missing()]) == (1,)
