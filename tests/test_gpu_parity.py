@@ -100,6 +100,28 @@ def test_dmpnn_aggregate(reduce, h):
         assert torch.equal(out.cpu(), ref)
 
 
+@pytest.mark.parametrize("h", [128, 200, 300, 320, 336])
+@pytest.mark.parametrize("reduce", ["sum", "mean", "max", "min"])
+def test_segment_reduce_contiguous_segments(h, reduce):
+    """perm = None (the readouts' node rows, stored molecule by molecule): segments of 0..27 rows, so
+    the block kernel's 10-row chunks, ragged last chunks and empty segments are all hit; h 128..320
+    takes segment_reduce_block, 336 the row-piece kernel.  Sum is the CPU scatter_add_ order: bit-exact;
+    max / min / empty bit-exact too."""
+    K = _K()
+    g = torch.Generator().manual_seed(h)
+    sizes = torch.randint(0, 28, (300,), generator=g)
+    sizes[::17] = 0
+    idx = torch.repeat_interleave(torch.arange(len(sizes)), sizes)
+    X = torch.randn(len(idx), h, generator=g)
+    seg_ptr = torch.zeros(len(sizes) + 1, dtype=torch.int32)
+    seg_ptr[1:] = torch.cumsum(sizes, 0)
+    out = K.segment_reduce(X.to(DEV), seg_ptr.to(DEV), None, len(sizes), reduce=reduce)
+    ref = dmpnn_ref.scatter(X, idx, len(sizes), reduce)
+    assert_parity(out, ref, 1e-6, f"contiguous segment_reduce {reduce} h={h}")
+    if reduce != "mean":
+        assert torch.equal(out.cpu(), ref)
+
+
 def test_segment_reduce_empty_segments():
     K = _K()
     X = torch.randn(3, 8)
