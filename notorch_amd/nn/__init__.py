@@ -11,8 +11,9 @@ from notorch_amd.nn.gnn import (
     Min,
     Sum,
 )
+from notorch_amd.nn.mlp import MLP
 from notorch_amd.nn.residual import Residual
 
 __all__ = [
-    "Aggregation", "Gated", "SDPAttention", "ChempropBlock", "ChempropLayer", "GraphEmbedding", "EmbeddedChempropBlock", "Max", "Mean", "Min", "Sum", "Residual",
+    "Aggregation", "Gated", "SDPAttention", "ChempropBlock", "ChempropLayer", "GraphEmbedding", "EmbeddedChempropBlock", "Max", "Mean", "Min", "Sum", "Residual", "MLP",
 ]

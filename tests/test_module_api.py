@@ -86,3 +86,23 @@ def test_graph_update_is_shallow_copy():
     assert G.update(in_place=True, edge_feats=Xe) is G
     assert G.num_nodes == 3 and G.num_edges == 4
     assert G.dense2sparse[1, 2] == 2 and G.A.sum() == 4
+
+
+def test_mlp_head_module_tree_matches_reference_layout():
+    """MLP (reference nn/mlp.py:9-68): Linear, act, Dropout, ..., Linear (+ Unflatten), so state_dict keys
+    and the output shape are the reference's; default hidden_dim 256 (notorch/conf.py:11)."""
+    import torch.nn as nn
+
+    from notorch_amd.nn import MLP
+
+    m = MLP(300, 1)
+    assert [type(x) for x in m] == [nn.Linear, nn.ReLU, nn.Dropout, nn.Linear]
+    assert list(m.state_dict()) == ["0.weight", "0.bias", "3.weight", "3.bias"]
+    assert m[0].out_features == 256 and m[3].out_features == 1
+    m = MLP(300, (2, 3), hidden_dim=64, num_layers=2, dropout=0.1, activation=nn.SiLU)
+    assert [type(x) for x in m] == [nn.Linear, nn.SiLU, nn.Dropout, nn.Linear, nn.SiLU, nn.Dropout, nn.Linear,
+                                    nn.Unflatten]
+    assert m[2].p == 0.1 and m[6].out_features == 6
+    assert m(torch.randn(5, 300)).shape == (5, 2, 3)
+    m = MLP(300, 5, num_layers=0)
+    assert [type(x) for x in m] == [nn.Linear] and m[0].in_features == 300 and m[0].out_features == 5
